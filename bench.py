@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Benchmark: simplex pivots/s + achieved HBM GB/s of the rank-1 update on a
+dense fp64 tableau (BASELINE.json metric), 1/2/4/8 MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2]
+
+A "step" is one simplex pivot (pricing + ratio test + pivot-row exchange +
+rank-1 elimination) of ONE LP whose tableau is resident in HBM, row-block
+partitioned over the N ranks (launched by torch.distributed.run for N > 1,
+one process per GPU, exchange over RCCL inside libdlp).  The LP is fixed as N
+grows, so scaling is strong.  Default workload C3: m = n = 32768 (N = 65536,
+17.2 GB tableau), generated on the device (synthetic, seed 3 = config id).
+
+Rank 0 prints ONE JSON line.  The roofline object prices the update kernel:
+algorithmic bytes per launch = 16 (m_local + 1)(N + 1) (one read + one write of
+every resident tableau element) over its mean launch time from
+HIP events on the session stream.  cpu_baseline (rank 0, N = 1 only) is the
+in-repo CPU oracle (same pivot rule) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+WORKLOADS = {
+    # name: (m, n, seed, description)
+    "c3": (32768, 32768, 3, "C3 dense LP 32768 x 32768 (+32768 slack): fp64 tableau 32769 x 65537, "
+                            "row-block over the GPUs"),
+    "c2": (4096, 4096, 2, "C2 dense LP 4096 x 4096 (+4096 slack): fp64 tableau 4097 x 8193"),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-pivots", type=int, default=3)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--rows-per-block", type=int, default=0)
+    ap.add_argument("--nontemporal", type=int, default=1)
+    ap.add_argument("--timing", type=int, default=2)
+    ap.add_argument("--pmc-dir", default=None,
+                    help="rocprofv3 --pmc output dir (FETCH_SIZE / WRITE_SIZE) to fill roofline.traffic")
+    return ap.parse_args()
+
+
+def pmc_traffic(pmc_dir: str, kernel_substr: str = "update_kernel"):
+    """Per-launch HBM bytes of the update kernel from rocprofv3 counter CSVs:
+    (2 x FETCH_SIZE + WRITE_SIZE) KiB -> bytes (gfx950 FETCH_SIZE reads 1/2 of a
+    wide coalesced stream: MI355X_MICROARCH.md §HBM)."""
+    import csv
+    import glob
+    fetch, write = [], []
+    for path in glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if kernel_substr not in row.get("Kernel_Name", ""):
+                    continue
+                name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+                if name == "FETCH_SIZE":
+                    fetch.append(val)
+                elif name == "WRITE_SIZE":
+                    write.append(val)
+    if not fetch or not write:
+        return None
+    return (2.0 * sum(fetch) / len(fetch) + sum(write) / len(write)) * 1024.0
+
+
+def cpu_baseline(m, n, seed, k, threads):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py  # test infrastructure: the CPU comparator only
+    secs, done, gen = oracle_py.bench_pivots(m, n, seed, 1, k, threads)
+    return {"value": done / secs, "unit": "pivots/s", "cores": threads, "kind": "port",
+            "sample": f"in-repo C++ oracle (same pivot rule, OpenMP over rows), same LP "
+                      f"{m}x{n} seed {seed}: 1 warm-up + {done} timed pivots in {secs:.2f} s "
+                      f"(host tableau generation {gen:.1f} s not timed)"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import distributedlpsolver_amd as dlp
+
+    m, n, seed, desc = WORKLOADS[args.workload]
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        obj = [dlp.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        rccl_id = obj[0]
+    else:
+        dist = None
+        rccl_id = None
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    sess = dlp.Session(dlp.Problem.random(m, n, seed), rank=rank, nranks=world, rccl_id=rccl_id,
+                       device=local, check_interval=max(args.steps, args.warmup, 1),
+                       timing=args.timing, nontemporal=args.nontemporal,
+                       rows_per_block=args.rows_per_block, max_pivots=args.warmup + args.steps + 1,
+                       log_pivots=1)
+    st, done = sess.run(args.warmup)
+    if done != args.warmup:
+        raise SystemExit(f"warm-up ended early: status {st} after {done} pivots")
+    sess.reset_timings()
+
+    barrier_sync()
+    t0 = time.perf_counter()
+    st, done = sess.run(args.steps)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if done != args.steps:
+        raise SystemExit(f"timed window ended early: status {st} after {done} pivots")
+
+    tm, nsamp = sess.timings()
+    rows_local, N1 = sess.rows, sess.ncols + 1
+    upd_ms = tm[3] / max(nsamp, 1)
+    bytes_launch = 16.0 * (rows_local + 1) * N1
+    achieved = bytes_launch / (upd_ms * 1e-3) / 1e9
+
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    res = sess.result()
+    sess.close()
+
+    if rank == 0:
+        traffic = pmc_traffic(args.pmc_dir) if args.pmc_dir else None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(m, n, seed, args.cpu_pivots, args.cpu_threads)
+        value = args.steps / elapsed
+        line = {
+            "metric": "simplex pivots/s (dense fp64 tableau, rank-1 update HBM roofline)",
+            "value": value,
+            "unit": "pivots/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (device-generated splitmix64 dense LP, seed = config id)",
+            "config": {"workload": desc, "m": m, "n": n, "N": m + n, "ld": dlp.tableau_ld(m, n), "seed": seed, "rows_per_rank": rows_local,
+                       "parallelism": f"rowblock{world}", "pricing": "dantzig->bland on degeneracy"},
+            "achieved_hbm_gbs": achieved,
+            "phases_ms_per_pivot": {"ratio": tm[0] / max(nsamp, 1), "exchange": tm[1] / max(nsamp, 1),
+                                    "prow": tm[2] / max(nsamp, 1), "update": upd_ms},
+            "objective_after_window": res.objective,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch,
+                         "kernel": "update_kernel<nt=1,U=4>", "launch_ms": upd_ms},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,327 @@
+// dlp_batched.hip — C5: thousands of independent small LPs, one workgroup per
+// LP, the whole (m+1) x (N+1) fp64 tableau resident in LDS (65 x 129 x 8 B =
+// 67 KB at m = n = 64, so two workgroups per CU of 160 KB).  HBM is touched
+// once per LP (load the generated tableau, store the outputs); every pivot is
+// LDS traffic plus workgroup barriers.
+//
+// Pivot rule and arithmetic are exactly the big-tableau path's (dlp.h header):
+// Dantzig/Bland pricing with index ties, ratio test with basis-index ties,
+// IEEE division for the pivot row, fma elimination, colq == 0 rows untouched.
+// Reference analog: the per-impression subproblems solved independently in
+// GlobalProblem::ConstructPrimal, R/global_problem.cpp:270-274.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "dlp_host.h"
+#include "dlp_internal.h"
+
+namespace dlp {
+namespace {
+
+__device__ inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ inline uint64_t skey(uint64_t seed, uint64_t s) {
+    return mix64(seed ^ (0x9E3779B97F4A7C15ULL * (s + 1)));
+}
+__device__ inline double u01(uint64_t key, uint64_t idx) {
+    return (double)(mix64(key + idx) >> 11) * 0x1.0p-53;
+}
+
+// Tableaus of the batch in HBM: LP k at T + k*(m+1)*ld, generated with seed+k
+// (same spec as generate_rows_kernel: one wave per row, strided fma chains +
+// fixed halving tree for b).  blockIdx.y = LP, waves of blockIdx.x = rows.
+__global__ __launch_bounds__(256) void batched_generate_kernel(double* __restrict__ T, int64_t ld,
+                                                               int64_t m, int64_t n, int kind,
+                                                               uint64_t seed) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t sk = seed + blockIdx.y;
+    double* base = T + (int64_t)blockIdx.y * (m + 1) * ld;
+    const int64_t N = n + m;
+    if (i < m) {
+        const uint64_t kA = skey(sk, 1), kX = skey(sk, 2), kU = skey(sk, 3), kD = skey(sk, 5);
+        double* r = base + i * ld;
+        // degenerate family: ~50% "cone" rows with A in [-1,1) and b = 0
+        const bool cone = kind == DLP_GEN_DEGENERATE && (mix64(kD + (uint64_t)i) >> 63) == 0;
+        double acc = 0.0;
+        for (int64_t j = lane; j < n; j += 64) {
+            const double u = u01(kA, (uint64_t)(i * n + j));
+            const double a = cone ? 2.0 * u - 1.0 : u;
+            r[j] = a;
+            acc = __builtin_fma(a, u01(kX, (uint64_t)j), acc);
+        }
+#pragma unroll
+        for (int w = 32; w >= 1; w >>= 1) acc = acc + __shfl_down(acc, w);
+        double bi = __shfl(acc, 0) + u01(kU, (uint64_t)i);
+        if (cone) bi = 0.0;
+        for (int64_t j = n + lane; j < ld; j += 64) r[j] = (j == n + i) ? 1.0 : (j == N ? bi : 0.0);
+    } else if (i == m) {
+        double* z = base + m * ld;
+        const uint64_t kC = skey(sk, 4);
+        for (int64_t j = lane; j < ld; j += 64) z[j] = (j < n) ? -u01(kC, (uint64_t)j) : 0.0;
+    }
+}
+
+struct BatchOut {
+    double* objective;
+    int32_t* status;
+    int64_t* npivots;
+    int32_t* basis;
+    dlp_pivot* logs;
+    int64_t log_cap;
+};
+
+// One workgroup = one LP.  LDS image: T[(m+1)][W] with W = N+1 (row stride
+// W is odd for even N, so a column read by consecutive rows walks the banks),
+// then prow[W], colq[m+1], basis[m], and a small reduction scratch.
+__global__ __launch_bounds__(256) void batched_solve_kernel(const double* __restrict__ Tg,
+                                                            int64_t ldg, int m, int n,
+                                                            int64_t max_pivots, int pricing,
+                                                            double tol_dj, double tol_piv,
+                                                            BatchOut out) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int N = n + m, W = N + 1;
+    double* T = smem;
+    double* prow = T + (m + 1) * W;
+    double* colq = prow + W;
+    int32_t* basis = (int32_t*)(colq + (m + 1));
+    // scratch: [0] q, [1] p, [2] status, [3] bland ; doubles: piv, ratio
+    int32_t* sI = basis + m + (m & 1);
+    double* sD = (double*)(sI + 4);
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t lp = blockIdx.x;
+    const double* src = Tg + lp * (m + 1) * ldg;
+    for (int e = tid; e < (m + 1) * W; e += blockDim.x) {
+        const int r = e / W, c = e - r * W;
+        T[e] = src[(int64_t)r * ldg + c];
+    }
+    for (int i = tid; i < m; i += blockDim.x) basis[i] = n + i;
+    if (tid == 0) {
+        sI[2] = DLP_RUNNING;
+        sI[3] = pricing == DLP_PRICING_BLAND ? 1 : 0;
+    }
+    __syncthreads();
+
+    int64_t k = 0;
+    for (; k < max_pivots; ++k) {
+        // ---- a1 pricing (wave 0): lexicographic (z, j) min + first j < -tol
+        if (wid == 0) {
+            double zmin = __builtin_inf();
+            int jmin = kNoIndex, jb = kNoIndex;
+            const double* z = T + m * W;
+            for (int j = lane; j < N; j += 64) {
+                const double v = z[j];
+                if (v < zmin) { zmin = v; jmin = j; }
+                if (v < -tol_dj && jb == kNoIndex) jb = j;
+            }
+#pragma unroll
+            for (int s = 32; s >= 1; s >>= 1) {
+                const double oz = __shfl_xor(zmin, s);
+                const int oj = __shfl_xor(jmin, s), ob = __shfl_xor(jb, s);
+                if (oz < zmin || (oz == zmin && oj < jmin)) { zmin = oz; jmin = oj; }
+                jb = ob < jb ? ob : jb;
+            }
+            if (lane == 0) {
+                int q;
+                if (sI[3]) q = jb;
+                else q = (jmin != kNoIndex && zmin < -tol_dj) ? jmin : kNoIndex;
+                sI[0] = (q == kNoIndex) ? -1 : q;
+            }
+        }
+        __syncthreads();
+        const int q = sI[0];
+        if (q < 0) {
+            if (tid == 0) sI[2] = DLP_OK;
+            break;
+        }
+        // ---- a2 ratio test (wave 0) + colq capture (all)
+        for (int i = tid; i <= m; i += blockDim.x) colq[i] = T[i * W + q];
+        if (wid == 0) {
+            Cand best;
+            best.valid = 0; best.ratio = 0.0; best.basis_var = kNoIndex; best.row = -1;
+            best.pad0 = 0; best.pivot = 0.0;
+            for (int i = lane; i < m; i += 64) {
+                const double a = T[i * W + q];
+                if (a > tol_piv) {
+                    double rhs = T[i * W + N];
+                    if (!(rhs > 0.0)) rhs = 0.0;
+                    Cand c;
+                    c.ratio = rhs / a; c.basis_var = basis[i]; c.row = i; c.valid = 1;
+                    c.pad0 = 0; c.pivot = a;
+                    if (cand_better(c, best)) best = c;
+                }
+            }
+#pragma unroll
+            for (int s = 32; s >= 1; s >>= 1) {
+                Cand o;
+                o.ratio = __shfl_xor(best.ratio, s);
+                o.basis_var = __shfl_xor(best.basis_var, s);
+                o.row = __shfl_xor(best.row, s);
+                o.valid = __shfl_xor(best.valid, s);
+                o.pad0 = 0;
+                o.pivot = __shfl_xor(best.pivot, s);
+                if (cand_better(o, best)) best = o;
+            }
+            if (lane == 0) {
+                if (!best.valid) {
+                    sI[1] = -1;
+                } else {   // a4 select + log
+                    const int p = best.row;
+                    const int leaving = basis[p];
+                    basis[p] = q;
+                    sI[1] = p;
+                    sI[3] = (pricing == DLP_PRICING_BLAND) ? 1 : (best.ratio == 0.0 ? 1 : 0);
+                    sD[0] = best.pivot;
+                    sD[1] = best.ratio;
+                    if (out.logs && k < out.log_cap) {
+                        dlp_pivot e;
+                        e.q = q; e.p = p; e.leaving = leaving; e.pad = 0;
+                        e.ratio = best.ratio; e.objective = 0.0;
+                        out.logs[lp * out.log_cap + k] = e;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const int p = sI[1];
+        if (p < 0) {
+            if (tid == 0) sI[2] = DLP_UNBOUNDED;
+            break;
+        }
+        // ---- a3 pivot row (IEEE division) then elimination
+        const double piv = sD[0];
+        for (int j = tid; j < W; j += blockDim.x) prow[j] = T[p * W + j] / piv;
+        __syncthreads();
+        {
+            int i = tid / W, j = tid - (tid / W) * W;
+            const int step_i = blockDim.x / W, step_j = blockDim.x - step_i * W;
+            for (; i <= m;) {
+                if (i == p) {
+                    T[i * W + j] = prow[j];
+                } else {
+                    const double f = colq[i];
+                    if (f != 0.0) T[i * W + j] = __builtin_fma(-f, prow[j], T[i * W + j]);
+                }
+                i += step_i;
+                j += step_j;
+                if (j >= W) { j -= W; ++i; }
+            }
+        }
+        __syncthreads();
+        if (tid == 0 && out.logs && k < out.log_cap)
+            out.logs[lp * out.log_cap + k].objective = T[m * W + N];
+    }
+    if (tid == 0) {
+        int stt = sI[2];
+        if (stt == DLP_RUNNING) stt = DLP_PIVOT_LIMIT;
+        if (out.status) out.status[lp] = stt;
+        if (out.npivots) out.npivots[lp] = k;
+        if (out.objective) out.objective[lp] = T[m * W + N];
+    }
+    if (out.basis)
+        for (int i = tid; i < m; i += blockDim.x) out.basis[lp * m + i] = basis[i];
+}
+
+}  // namespace
+}  // namespace dlp
+
+#define HIP_BTRY(expr)                                                               \
+    do {                                                                             \
+        hipError_t e_ = (expr);                                                      \
+        if (e_ != hipSuccess) {                                                      \
+            dlp::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));       \
+            rc = DLP_ERR_HIP;                                                        \
+            goto done;                                                               \
+        }                                                                            \
+    } while (0)
+
+extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, uint64_t seed,
+                                 const dlp_options* opt, double* objective, int32_t* status,
+                                 int64_t* npivots, int32_t* basis, dlp_pivot* logs,
+                                 int64_t log_cap, double* kernel_ms) {
+    dlp_options o;
+    if (opt) o = *opt; else dlp_options_default(&o);
+    if (nlp <= 0 || m <= 0 || n <= 0 || (kind != DLP_GEN_DENSE && kind != DLP_GEN_DEGENERATE) ||
+        nlp > 65535 * 16 || log_cap < 0) {
+        dlp::set_error("dlp_batched_solve: bad arguments");
+        return DLP_ERR_ARG;
+    }
+    const int64_t N = n + m, W = N + 1, ldg = (N + 1 + 15) / 16 * 16;
+    const size_t lds = sizeof(double) * ((m + 1) * W + W + (m + 1)) + sizeof(int32_t) * (m + 1 + 4) +
+                       sizeof(double) * 4 + 16;
+    int rc = DLP_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        dlp::set_error("no HIP device visible (libdlp has no CPU fallback)");
+        return DLP_ERR_NODEVICE;
+    }
+    if (lds > 160 * 1024) {
+        dlp::set_error("dlp_batched_solve: tableau does not fit in 160 KiB of LDS");
+        return DLP_ERR_UNSUPPORTED;
+    }
+    double* dT = nullptr;
+    double* dObj = nullptr;
+    int32_t* dSt = nullptr;
+    int64_t* dNp = nullptr;
+    int32_t* dBasis = nullptr;
+    dlp_pivot* dLog = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    dlp::BatchOut bo{};
+    HIP_BTRY(hipSetDevice(o.device));
+    HIP_BTRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_BTRY(hipMalloc(&dT, sizeof(double) * nlp * (m + 1) * ldg));
+    HIP_BTRY(hipMalloc(&dObj, sizeof(double) * nlp));
+    HIP_BTRY(hipMalloc(&dSt, sizeof(int32_t) * nlp));
+    HIP_BTRY(hipMalloc(&dNp, sizeof(int64_t) * nlp));
+    if (basis) HIP_BTRY(hipMalloc(&dBasis, sizeof(int32_t) * nlp * m));
+    if (logs && log_cap > 0) HIP_BTRY(hipMalloc(&dLog, sizeof(dlp_pivot) * nlp * log_cap));
+    HIP_BTRY(hipEventCreate(&e0));
+    HIP_BTRY(hipEventCreate(&e1));
+    {
+        dim3 gg((unsigned)((m + 1 + 3) / 4), (unsigned)nlp);
+        dlp::batched_generate_kernel<<<gg, 256, 0, s>>>(dT, ldg, m, n, kind, seed);
+        HIP_BTRY(hipGetLastError());
+        bo.objective = dObj;
+        bo.status = dSt;
+        bo.npivots = dNp;
+        bo.basis = dBasis;
+        bo.logs = dLog;
+        bo.log_cap = dLog ? log_cap : 0;
+        HIP_BTRY(hipFuncSetAttribute((const void*)dlp::batched_solve_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        HIP_BTRY(hipEventRecord(e0, s));
+        dlp::batched_solve_kernel<<<(unsigned)nlp, 256, lds, s>>>(
+            dT, ldg, (int)m, (int)n, o.max_pivots, o.pricing, o.tol_dj, o.tol_piv, bo);
+        HIP_BTRY(hipGetLastError());
+        HIP_BTRY(hipEventRecord(e1, s));
+        HIP_BTRY(hipStreamSynchronize(s));
+        if (kernel_ms) {
+            float ms = 0.f;
+            HIP_BTRY(hipEventElapsedTime(&ms, e0, e1));
+            *kernel_ms = ms;
+        }
+        if (objective) HIP_BTRY(hipMemcpy(objective, dObj, sizeof(double) * nlp, hipMemcpyDeviceToHost));
+        if (status) HIP_BTRY(hipMemcpy(status, dSt, sizeof(int32_t) * nlp, hipMemcpyDeviceToHost));
+        if (npivots) HIP_BTRY(hipMemcpy(npivots, dNp, sizeof(int64_t) * nlp, hipMemcpyDeviceToHost));
+        if (basis) HIP_BTRY(hipMemcpy(basis, dBasis, sizeof(int32_t) * nlp * m, hipMemcpyDeviceToHost));
+        if (dLog)
+            HIP_BTRY(hipMemcpy(logs, dLog, sizeof(dlp_pivot) * nlp * log_cap, hipMemcpyDeviceToHost));
+    }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    for (void* p : {(void*)dT, (void*)dObj, (void*)dSt, (void*)dNp, (void*)dBasis, (void*)dLog})
+        if (p) (void)hipFree(p);
+    if (s) (void)hipStreamDestroy(s);
+    return rc;
+}

@@ -1,0 +1,97 @@
+// dlp_internal.h — types shared by the HIP kernels (dlp_kernels.hip) and the
+// host runtime (dlp_session.cpp).  Not part of the public C ABI.
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#include "dlp.h"
+
+namespace dlp {
+
+// Update-kernel geometry: 256 lanes x 2 doubles (one 16-B dwordx4 per lane)
+// = one 4 KiB column tile of one tableau row per workgroup-row step.
+constexpr int kUpdThreads = 256;
+constexpr int kUpdVec = 2;
+constexpr int kUpdTile = kUpdThreads * kUpdVec;   // doubles per column tile
+constexpr int kRatioThreads = 256;
+constexpr int kProwThreads = 256;
+constexpr int32_t kNoIndex = 0x7fffffff;
+constexpr int kColqPad = 16;   // colq allocated with rows + 1 + kColqPad entries
+
+// Pricing partial of one column tile of the objective row.
+struct alignas(16) PricePart {
+    double zmin;     // min z_j in the tile (+inf when none)
+    int32_t jmin;    // first j attaining zmin (kNoIndex when none)
+    int32_t jbland;  // first j with z_j < -tol_dj (kNoIndex when none)
+};
+
+// Candidate = dlp_candidate (32 B): ratio, basis_var, row, valid, pad, pivot.
+struct alignas(16) Cand {
+    double ratio;
+    int32_t basis_var;
+    int32_t row;
+    int32_t valid;
+    int32_t pad0;
+    double pivot;    // T[row][q] (the pivot element if this row wins)
+};
+static_assert(sizeof(Cand) == 32, "Cand must match dlp_candidate");
+
+// Device-resident solver state (one per rank).  Every decision of a pivot
+// lives here, so a window of pivots runs with no host round trip.
+struct alignas(16) DevState {
+    int32_t status;    // DLP_RUNNING, DLP_OK (optimal), DLP_UNBOUNDED
+    int32_t q;         // entering column
+    int32_t p;         // pivot row, global index
+    int32_t p_local;   // pivot row on this rank, -1 elsewhere
+    int32_t leaving;
+    int32_t bland;     // current pricing mode
+    int64_t npivots;
+    double piv;        // pivot element T[p][q]
+    double ratio;      // r_p
+    uint32_t ticket;   // last-workgroup election of the ratio kernel
+    uint32_t pad[3];
+};
+
+// Candidate order: valid first, then smaller ratio, then smaller basis index.
+// Total and order-independent, so any reduction tree picks the same winner.
+__host__ __device__ inline bool cand_better(const Cand& a, const Cand& b) {
+    if (a.valid != b.valid) return a.valid != 0;
+    if (!a.valid) return false;
+    if (a.ratio != b.ratio) return a.ratio < b.ratio;
+    return a.basis_var < b.basis_var;
+}
+
+// Launchers (dlp_kernels.hip).  All asynchronous on `stream`.
+struct Geometry {
+    double* T;            // (rows+1) x ld, objective row last
+    int64_t ld;
+    int64_t rows;         // local constraint rows
+    int64_t row_first;    // global index of local row 0
+    int64_t ncols;        // N = n + m (pricing columns; RHS column index)
+    int ntiles;           // ceil(ld / kUpdTile)
+    int rows_per_block;   // update kernel
+};
+
+hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, hipStream_t s);
+hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* basis_out,
+                        const PricePart* pp, DevState* st, double* colq, Cand* partials,
+                        int nblocks, Cand* cand_out, int nranks, double tol_dj, double tol_piv,
+                        int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s);
+int ratio_blocks(const Geometry& g);
+hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32_t* basis,
+                         DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
+                         hipStream_t s);
+hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits, int nranks,
+                       hipStream_t s);
+hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,
+                         const DevState* st, PricePart* pp, double tol_dj, dlp_pivot* log,
+                         int64_t log_cap, bool nontemporal, hipStream_t s);
+// Synthetic tableau rows [row_first, row_first+rows) + objective row, on device.
+hipError_t launch_generate(const Geometry& g, int kind, int64_t m, int64_t n, uint64_t seed,
+                           hipStream_t s);
+// Gather column `col` of rows [0, nrows) into out (nrows doubles).
+hipError_t launch_gather_column(const double* T, int64_t ld, int64_t nrows, int64_t col,
+                                double* out, hipStream_t s);
+
+}  // namespace dlp

@@ -1,0 +1,522 @@
+// dlp_kernels.hip — CDNA4 (gfx950) kernels of one simplex pivot on an
+// HBM-resident fp64 tableau.  SURVEY.md §8a rows a1-a4.  The reference has no
+// simplex; nearest reference analogs are cited per kernel.
+//
+// Per pivot, stream-ordered, no host round trip:
+//   ratio_kernel    pricing reduce (q) + ratio test + colq capture + last-WG
+//                   argmin (+ select when single rank)                [a1,a2,a4]
+//   select_kernel   winner of the all-gathered rank candidates (nranks > 1) [a4]
+//   prow_kernel     prow = T[p]/T[p][q] (owner) / INT64_MIN sentinel        [a3]
+//   update_kernel   T -= colq (x) prow, streaming 16 B/lane, nt loads/stores,
+//                   fused pricing partials of the next pivot             [a3,a1]
+//
+// Arithmetic is bit-for-bit the oracle's: explicit fma, IEEE division, argmins
+// with exact compares and index tie-breaks (reduction-order independent).
+// Built with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "dlp_internal.h"
+
+namespace dlp {
+namespace {
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+// ------------------------------------------------------------- reductions
+__device__ inline void pp_combine(PricePart& a, const PricePart& b) {
+    if (b.zmin < a.zmin || (b.zmin == a.zmin && b.jmin < a.jmin)) {
+        a.zmin = b.zmin;
+        a.jmin = b.jmin;
+    }
+    a.jbland = b.jbland < a.jbland ? b.jbland : a.jbland;
+}
+
+__device__ inline PricePart pp_empty() {
+    PricePart p;
+    p.zmin = __builtin_inf();
+    p.jmin = kNoIndex;
+    p.jbland = kNoIndex;
+    return p;
+}
+
+__device__ inline PricePart pp_shfl_xor(const PricePart& v, int m) {
+    PricePart o;
+    o.zmin = __shfl_xor(v.zmin, m);
+    o.jmin = __shfl_xor(v.jmin, m);
+    o.jbland = __shfl_xor(v.jbland, m);
+    return o;
+}
+
+__device__ inline Cand cand_empty() {
+    Cand c;
+    c.ratio = 0.0;
+    c.basis_var = kNoIndex;
+    c.row = -1;
+    c.valid = 0;
+    c.pad0 = 0;
+    c.pivot = 0.0;
+    return c;
+}
+
+__device__ inline Cand cand_shfl_xor(const Cand& v, int m) {
+    Cand o;
+    o.ratio = __shfl_xor(v.ratio, m);
+    o.basis_var = __shfl_xor(v.basis_var, m);
+    o.row = __shfl_xor(v.row, m);
+    o.valid = __shfl_xor(v.valid, m);
+    o.pad0 = 0;
+    o.pivot = __shfl_xor(v.pivot, m);
+    return o;
+}
+
+// Block-wide reduction (blockDim.x = 256 = 4 waves): wave shuffles, then LDS.
+template <typename T, typename Shfl, typename Comb>
+__device__ inline T block_reduce(T v, T* lds4, Shfl shfl, Comb comb) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        T o = shfl(v, m);
+        comb(v, o);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) lds4[wid] = v;
+    __syncthreads();
+    T r = lds4[0];
+    const int nw = blockDim.x >> 6;
+    for (int w = 1; w < nw; ++w) comb(r, lds4[w]);
+    __syncthreads();
+    return r;
+}
+
+__device__ inline PricePart block_price(PricePart v, PricePart* lds4) {
+    return block_reduce(
+        v, lds4, [](const PricePart& x, int m) { return pp_shfl_xor(x, m); },
+        [](PricePart& a, const PricePart& b) { pp_combine(a, b); });
+}
+
+__device__ inline Cand block_cand(Cand v, Cand* lds4) {
+    return block_reduce(
+        v, lds4, [](const Cand& x, int m) { return cand_shfl_xor(x, m); },
+        [](Cand& a, const Cand& b) {
+            if (cand_better(b, a)) a = b;
+        });
+}
+
+// Lane-level pricing of two adjacent columns j, j+1 (ascending).
+__device__ inline void price_pair(PricePart& acc, double z0, double z1, int64_t j, int64_t ncols,
+                                  double tol_dj) {
+    if (j < ncols) {
+        if (z0 < acc.zmin) { acc.zmin = z0; acc.jmin = (int32_t)j; }
+        if (z0 < -tol_dj && acc.jbland == kNoIndex) acc.jbland = (int32_t)j;
+    }
+    if (j + 1 < ncols) {
+        if (z1 < acc.zmin) { acc.zmin = z1; acc.jmin = (int32_t)(j + 1); }
+        if (z1 < -tol_dj && acc.jbland == kNoIndex) acc.jbland = (int32_t)(j + 1);
+    }
+}
+
+// a4: select + basis bookkeeping + pivot log (one lane).
+__device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* basis,
+                          int64_t row_first, int64_t rows, int pricing, dlp_pivot* log,
+                          int64_t log_cap) {
+    if (!best.valid) {
+        st->status = DLP_UNBOUNDED;
+        return;
+    }
+    const int32_t p = best.row;
+    const int32_t leaving = basis[p];
+    basis[p] = q;
+    st->q = q;
+    st->p = p;
+    st->leaving = leaving;
+    st->ratio = best.ratio;
+    st->bland = (pricing == DLP_PRICING_BLAND) ? 1 : (best.ratio == 0.0 ? 1 : 0);
+    const int64_t pl = (int64_t)p - row_first;
+    st->p_local = (pl >= 0 && pl < rows) ? (int32_t)pl : -1;
+    st->piv = best.pivot;
+    const int64_t k = st->npivots;
+    if (log && k < log_cap) {
+        dlp_pivot e;
+        e.q = q;
+        e.p = p;
+        e.leaving = leaving;
+        e.pad = 0;
+        e.ratio = best.ratio;
+        e.objective = __builtin_nan("");
+        log[k] = e;
+    }
+    st->npivots = k + 1;
+}
+
+// ------------------------------------------------------------------ kernels
+
+// a1 at start-up: pricing partials of the initial objective row, one per
+// 512-column tile (the same tiling the update kernel's fused epilogue uses).
+__global__ __launch_bounds__(kUpdThreads) void price_init_kernel(const double* __restrict__ zrow,
+                                                                 int64_t ncols, PricePart* pp,
+                                                                 double tol_dj) {
+    __shared__ PricePart lds[4];
+    const int64_t j = (int64_t)blockIdx.x * kUpdTile + threadIdx.x * kUpdVec;
+    PricePart acc = pp_empty();
+    if (j < ncols) {
+        const double z0 = zrow[j];
+        const double z1 = (j + 1 < ncols) ? zrow[j + 1] : 0.0;
+        price_pair(acc, z0, z1, j, ncols, tol_dj);
+    }
+    acc = block_price(acc, lds);
+    if (threadIdx.x == 0) pp[blockIdx.x] = acc;
+}
+
+// a1 + a2 (+ a4 when single rank).  Every workgroup re-derives q from the
+// tile partials (<= a few KB, L2-resident) so no extra launch is needed; then
+// one lane per local row (objective row included for colq) reads T[i][q] and
+// T[i][N] (two strided 8-B loads), captures colq[i], and forms the ratio
+// candidate.  The last workgroup to arrive (agent-scope release/acquire
+// ticket, cdna_hip_programming.md Guideline 16) reduces the per-WG partials.
+// Nearest reference analog: the tolerance-gated tight-set test
+// R/global_problem.cpp:372-380 and first-wins scans :335-361.
+__global__ __launch_bounds__(kRatioThreads) void ratio_kernel(
+    const double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t row_first,
+    const int32_t* basis, int32_t* basis_w, const PricePart* __restrict__ pp, int ntiles,
+    DevState* st, double* __restrict__ colq, Cand* partials, Cand* cand_out, int nranks,
+    double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap) {
+    __shared__ PricePart lds_pp[4];
+    __shared__ Cand lds_c[4];
+    __shared__ int s_last;
+    if (st->status != DLP_RUNNING) return;
+
+    // ---- pricing: q from the column-tile partials
+    PricePart acc = pp_empty();
+    for (int k = threadIdx.x; k < ntiles; k += blockDim.x) pp_combine(acc, pp[k]);
+    acc = block_price(acc, lds_pp);
+    const int bland = st->bland;
+    int32_t q;
+    if (bland)
+        q = acc.jbland;
+    else
+        q = (acc.jmin != kNoIndex && acc.zmin < -tol_dj) ? acc.jmin : kNoIndex;
+    if (q == kNoIndex) {   // optimal: every WG agrees; WG 0 records it
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->q = -1;
+            st->status = DLP_OK;
+        }
+        return;
+    }
+
+    // ---- ratio test over local rows
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    Cand c = cand_empty();
+    if (i <= rows) {
+        const double a = T[i * ld + q];
+        colq[i] = a;
+        if (i < rows && a > tol_piv) {
+            double rhs = T[i * ld + ncols];
+            if (!(rhs > 0.0)) rhs = 0.0;
+            c.ratio = rhs / a;
+            c.row = (int32_t)(row_first + i);
+            c.basis_var = basis[row_first + i];
+            c.valid = 1;
+            c.pivot = a;
+        }
+    }
+    c = block_cand(c, lds_c);
+
+    // ---- last-arriving workgroup reduces the partials
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = c;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev =
+            __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    Cand best = cand_empty();
+    for (int k = threadIdx.x; k < (int)gridDim.x; k += blockDim.x) {
+        const Cand o = partials[k];
+        if (cand_better(o, best)) best = o;
+    }
+    best = block_cand(best, lds_c);
+    if (threadIdx.x == 0) {
+        st->ticket = 0;
+        st->q = q;
+        if (nranks == 1)
+            do_select(st, best, q, basis_w, row_first, rows, pricing, log, log_cap);
+        else
+            cand_out[0] = best;
+    }
+}
+
+// a4 for nranks > 1: every rank reduces the same all-gathered candidates in
+// the same order, so all ranks agree on p with no MINLOC collective.
+__global__ void select_kernel(const Cand* cands, int nranks, int32_t* basis, DevState* st,
+                              int64_t row_first, int64_t rows, int pricing, dlp_pivot* log,
+                              int64_t log_cap) {
+    if (st->status != DLP_RUNNING || threadIdx.x != 0) return;
+    Cand best = cand_empty();
+    for (int r = 0; r < nranks; ++r)
+        if (cand_better(cands[r], best)) best = cands[r];
+    do_select(st, best, st->q, basis, row_first, rows, pricing, log, log_cap);
+}
+
+// a3 (first half): normalised pivot row, IEEE division (never a reciprocal
+// multiply).  Non-owner ranks write INT64_MIN, the identity of the int64 MAX
+// all-reduce, which therefore delivers the owner's exact bits (signed zeros
+// included) to every rank without a host-known broadcast root.
+__global__ __launch_bounds__(kProwThreads) void prow_kernel(const double* __restrict__ T,
+                                                            int64_t ld, const DevState* st,
+                                                            int64_t* __restrict__ out) {
+    if (st->status != DLP_RUNNING) return;
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    if (j >= ld) return;
+    const int32_t pl = st->p_local;
+    if (pl >= 0) {
+        const double piv = st->piv;
+        const d2 v = *(const d2*)(T + (int64_t)pl * ld + j);
+        d2 r;
+        r.x = v.x / piv;
+        r.y = v.y / piv;
+        *(d2*)(out + j) = r;
+    } else {
+        out[j] = INT64_MIN;
+        out[j + 1] = INT64_MIN;
+    }
+}
+
+template <bool NT>
+__device__ inline d2 ld2(const double* p) {
+    if constexpr (NT)
+        return __builtin_nontemporal_load((const d2*)p);
+    else
+        return *(const d2*)p;
+}
+template <bool NT>
+__device__ inline void st2(double* p, d2 v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, (d2*)p);
+    else
+        *(d2*)p = v;
+}
+
+// a3 (second half): the rank-1 elimination, the HBM-bound ~100% of a pivot.
+// Workgroup (tile, band) owns columns [tile*512, +512) of rows
+// [band*rb, +rb): each lane keeps its 2 prow values in registers for the whole
+// band, colq[i] is a wave-uniform scalar load, and U rows are loaded before
+// any is stored so every lane has U x 16 B in flight.  Rows with colq == 0
+// are skipped (no traffic); row p becomes prow.  The band holding the
+// objective row also emits the next pivot's pricing partial for its tile and
+// the objective value into the pivot log.
+// Nearest reference analog: the 2x2 basis solve R/global_problem.cpp:393-405.
+template <bool NT, int U>
+__global__ __launch_bounds__(kUpdThreads) void update_kernel(
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+    const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
+    PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
+    __shared__ PricePart lds_pp[4];
+    if (st->status != DLP_RUNNING) return;
+    const int tile = blockIdx.x;
+    const int64_t j = (int64_t)tile * kUpdTile + threadIdx.x * kUpdVec;
+    const bool colok = j < ld;
+    // Lanes past ld (last, partial tile only) read a valid in-row address and
+    // never store, so every load below is issued without a branch.
+    const int64_t jc = colok ? j : ld - kUpdVec;
+    const d2 pr = *(const d2*)(prow + jc);
+    const int64_t pl = st->p_local;
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;   // constraint rows only
+
+    for (int64_t i = i0; i < iend; i += U) {
+        d2 t[U];
+        double f[U];
+        // All U loads in flight before the first use; a row that needs no
+        // load (out of band, colq == 0, or the pivot row) reads the L2-hot
+        // prow line instead of branching.
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t ii = i + u;
+            f[u] = colq[ii];   // colq is padded by kColqPad: always a valid read
+            const bool need = (ii < iend) && (ii != pl) && (f[u] != 0.0);
+            const double* src = need ? (T + ii * ld + jc) : (prow + jc);
+            t[u] = ld2<NT>(src);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t ii = i + u;
+            if ((ii < iend) && (ii == pl || f[u] != 0.0)) {   // wave-uniform
+                d2 o;
+                o.x = __builtin_fma(-f[u], pr.x, t[u].x);
+                o.y = __builtin_fma(-f[u], pr.y, t[u].y);
+                if (ii == pl) o = pr;
+                if (colok) st2<NT>(T + ii * ld + j, o);
+            }
+        }
+    }
+
+    if (i0 + rb > rows) {   // this band holds the objective row (local index `rows`)
+        const double f = colq[rows];
+        double* zp = T + rows * ld + jc;
+        d2 z = *(const d2*)zp;
+        if (f != 0.0 && colok) {
+            z.x = __builtin_fma(-f, pr.x, z.x);
+            z.y = __builtin_fma(-f, pr.y, z.y);
+            *(d2*)zp = z;
+        }
+        PricePart acc = pp_empty();
+        if (colok) price_pair(acc, z.x, z.y, j, ncols, tol_dj);
+        acc = block_price(acc, lds_pp);
+        if (threadIdx.x == 0) pp[tile] = acc;
+        if (log && colok && j <= ncols && ncols < j + 2) {
+            const int64_t k = st->npivots - 1;
+            if (k >= 0 && k < log_cap) log[k].objective = (ncols == j) ? z.x : z.y;
+        }
+    }
+}
+
+// -------------------------------------------------------------- generators
+// SURVEY.md §8a row a7 (build spec; restated independently in oracle/oracle.cpp).
+__device__ inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ inline uint64_t stream_key(uint64_t seed, uint64_t s) {
+    return mix64(seed ^ (0x9E3779B97F4A7C15ULL * (s + 1)));
+}
+__device__ inline double unit01(uint64_t key, uint64_t idx) {
+    return (double)(mix64(key + idx) >> 11) * 0x1.0p-53;
+}
+
+// One wavefront per local row: lane l writes A[i][l + 64k] (coalesced) and
+// accumulates the strided fma chain of b_i; the 64 chains are combined by the
+// fixed halving tree (shfl_down 32..1) that the oracle restates.
+__global__ __launch_bounds__(256) void generate_rows_kernel(double* __restrict__ T, int64_t ld,
+                                                            int64_t rows, int64_t row_first,
+                                                            int64_t m, int64_t n, int kind,
+                                                            uint64_t seed) {
+    const int lane = threadIdx.x & 63;
+    const int64_t il = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (il >= rows) return;
+    const int64_t i = row_first + il;
+    const int64_t N = n + m;
+    const uint64_t kA = stream_key(seed, 1), kX = stream_key(seed, 2), kU = stream_key(seed, 3),
+                   kD = stream_key(seed, 5);
+    double* r = T + il * ld;
+    // degenerate family: ~50% "cone" rows with A in [-1,1) (2u-1, exact) and b = 0
+    const bool cone = kind == DLP_GEN_DEGENERATE && (mix64(kD + (uint64_t)i) >> 63) == 0;
+    double acc = 0.0;
+    for (int64_t j = lane; j < n; j += 64) {
+        const double u = unit01(kA, (uint64_t)(i * n + j));
+        const double a = cone ? 2.0 * u - 1.0 : u;
+        r[j] = a;
+        acc = __builtin_fma(a, unit01(kX, (uint64_t)j), acc);
+    }
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) acc = acc + __shfl_down(acc, w);
+    double bi = __shfl(acc, 0) + unit01(kU, (uint64_t)i);
+    if (kind == DLP_GEN_DEGENERATE && (mix64(kD + (uint64_t)i) >> 63) == 0) bi = 0.0;
+    // slack identity column, RHS and zero padding: each cell written by one lane
+    for (int64_t j = n + lane; j < ld; j += 64) r[j] = (j == n + i) ? 1.0 : (j == N ? bi : 0.0);
+}
+
+__global__ __launch_bounds__(256) void generate_objective_kernel(double* __restrict__ z,
+                                                                 int64_t ld, int64_t n,
+                                                                 uint64_t seed) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ld) return;
+    z[j] = (j < n) ? -unit01(stream_key(seed, 4), (uint64_t)j) : 0.0;
+}
+
+__global__ void gather_column_kernel(const double* __restrict__ T, int64_t ld, int64_t nrows,
+                                     int64_t col, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nrows) out[i] = T[i * ld + col];
+}
+
+}  // namespace
+
+// --------------------------------------------------------------- launchers
+int ratio_blocks(const Geometry& g) {
+    return (int)((g.rows + 1 + kRatioThreads - 1) / kRatioThreads);
+}
+
+hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, hipStream_t s) {
+    const double* z = g.T + g.rows * g.ld;
+    price_init_kernel<<<g.ntiles, kUpdThreads, 0, s>>>(z, g.ncols, pp, tol_dj);
+    return hipGetLastError();
+}
+
+hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* basis_out,
+                        const PricePart* pp, DevState* st, double* colq, Cand* partials,
+                        int nblocks, Cand* cand_out, int nranks, double tol_dj, double tol_piv,
+                        int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+    ratio_kernel<<<nblocks, kRatioThreads, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.row_first,
+                                                   basis_in, basis_out, pp, g.ntiles, st, colq,
+                                                   partials, cand_out, nranks, tol_dj, tol_piv,
+                                                   pricing, log, log_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32_t* basis,
+                         DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
+                         hipStream_t s) {
+    select_kernel<<<1, 64, 0, s>>>(cands, nranks, basis, st, g.row_first, g.rows, pricing, log,
+                                   log_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits, int nranks,
+                       hipStream_t s) {
+    (void)nranks;
+    const int64_t pairs = g.ld / 2;
+    const int blocks = (int)((pairs + kProwThreads - 1) / kProwThreads);
+    prow_kernel<<<blocks, kProwThreads, 0, s>>>(g.T, g.ld, st, prow_bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,
+                         const DevState* st, PricePart* pp, double tol_dj, dlp_pivot* log,
+                         int64_t log_cap, bool nontemporal, hipStream_t s) {
+    const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
+    dim3 grid(g.ntiles, (unsigned)bands);
+    if (nontemporal)
+        update_kernel<true, 4><<<grid, kUpdThreads, 0, s>>>(g.T, g.ld, g.rows, g.ncols, colq,
+                                                            prow, st, pp, g.rows_per_block,
+                                                            tol_dj, log, log_cap);
+    else
+        update_kernel<false, 4><<<grid, kUpdThreads, 0, s>>>(g.T, g.ld, g.rows, g.ncols, colq,
+                                                             prow, st, pp, g.rows_per_block,
+                                                             tol_dj, log, log_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_generate(const Geometry& g, int kind, int64_t m, int64_t n, uint64_t seed,
+                           hipStream_t s) {
+    if (g.rows > 0) {
+        const int wpb = 4;   // wavefronts (rows) per workgroup
+        const int64_t blocks = (g.rows + wpb - 1) / wpb;
+        generate_rows_kernel<<<(unsigned)blocks, 64 * wpb, 0, s>>>(g.T, g.ld, g.rows,
+                                                                   g.row_first, m, n, kind, seed);
+    }
+    const int64_t zb = (g.ld + 255) / 256;
+    generate_objective_kernel<<<(unsigned)zb, 256, 0, s>>>(g.T + g.rows * g.ld, g.ld, n, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_column(const double* T, int64_t ld, int64_t nrows, int64_t col,
+                                double* out, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    const int64_t blocks = (nrows + 255) / 256;
+    gather_column_kernel<<<(unsigned)blocks, 256, 0, s>>>(T, ld, nrows, col, out);
+    return hipGetLastError();
+}
+
+}  // namespace dlp

@@ -1,0 +1,821 @@
+// dlp_session.cpp — host runtime behind the C ABI (include/dlp.h): problem
+// objects, the HBM-resident tableau session, the pivot loop with device-side
+// decisions (no host round trip per pivot), RCCL row-block exchange, results.
+//
+// Replaces the reference's solver entry and result store:
+//   Instance::RunMultiplicativeWeights  R/instance.cpp:117-134  -> dlp_solve
+//   AllocationMW::RunAllocationMW loop  R/allocation_mw.cpp:271-326 -> dlp_session_run
+//   Instance::solution_                 R/instance.h:34 -> dlp_result_x / _y
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "dlp_host.h"
+#include "dlp_internal.h"
+
+namespace dlp {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+}  // namespace dlp
+
+using dlp::set_error;
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                \
+            return DLP_ERR_HIP;                                                          \
+        }                                                                                \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                   \
+    do {                                                                                 \
+        ncclResult_t r_ = (expr);                                                        \
+        if (r_ != ncclSuccess) {                                                         \
+            set_error(std::string(#expr) + ": " + ncclGetErrorString(r_));               \
+            return DLP_ERR_RCCL;                                                         \
+        }                                                                                \
+    } while (0)
+
+#define CALL_TRY(expr)                                                                   \
+    do {                                                                                 \
+        int rc_ = (expr);                                                                \
+        if (rc_ != DLP_OK) return rc_;                                                   \
+    } while (0)
+
+struct dlp_session {
+    dlp_options opt{};
+    int device = 0, rank = 0, nranks = 1;
+    int64_t m = 0, n = 0, N = 0, ld = 0, row_first = 0, rows = 0;
+    hipStream_t stream = nullptr;
+    dlp::Geometry g{};
+    double* T = nullptr;
+    double* colq = nullptr;
+    int64_t* prow_send = nullptr;
+    int64_t* prow_recv = nullptr;   // == prow_send when nranks == 1
+    dlp::Cand* partials = nullptr;
+    int ratio_blocks = 0;
+    dlp::Cand* cand_send = nullptr;
+    dlp::Cand* cand_recv = nullptr;
+    dlp::PricePart* pp = nullptr;
+    int32_t* basis = nullptr;
+    dlp::DevState* st = nullptr;
+    dlp_pivot* log = nullptr;
+    int64_t log_cap = 0;
+    dlp::DevState* host_st = nullptr;   // pinned
+    ncclComm_t comm = nullptr;
+    bool use_rccl = false;
+    bool exchange = false;          // candidate all-gather + prow all-reduce path
+    int64_t launched = 0;
+    int status = DLP_RUNNING;
+    int64_t npivots = 0;
+    // timing (HIP events on the session stream)
+    int ev_per_pivot = 0;
+    std::vector<hipEvent_t> ev;
+    int64_t ev_pending = 0;   // pivots with recorded events since the last poll
+    double timings[DLP_NUM_PHASES] = {0, 0, 0, 0};
+    int64_t nsamples = 0;
+    // graph replay of one poll window (single rank, no events)
+    hipGraphExec_t gexec = nullptr;
+    hipGraph_t graph = nullptr;
+    int64_t graph_chunk = 0;
+    // problem copy for results
+    dlp_problem prob_dims{};
+};
+
+namespace {
+
+int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
+
+int auto_rows_per_block(int64_t rows_total, int ntiles) {
+    // Aim for ~8 K workgroups (>= 32 per CU of 256) with bands of 4..128 rows.
+    int64_t rb = (rows_total * ntiles + 8191) / 8192;
+    rb = std::max<int64_t>(4, std::min<int64_t>(128, rb));
+    rb = (rb + 3) / 4 * 4;
+    return (int)rb;
+}
+
+// Host build of a tableau slice (dense / ad-allocation problems).
+void host_tableau(const dlp_problem* p, int64_t row_first, int64_t rows, int64_t ld,
+                  std::vector<double>& T) {
+    const int64_t m = p->m, n = p->n, N = n + m;
+    T.assign((size_t)(rows + 1) * ld, 0.0);
+    if (p->kind == dlp::PROB_DENSE) {
+        for (int64_t il = 0; il < rows; ++il) {
+            const int64_t i = row_first + il;
+            double* r = T.data() + il * ld;
+            std::memcpy(r, p->A.data() + i * n, sizeof(double) * n);
+            r[n + i] = 1.0;
+            r[N] = p->b[i];
+        }
+        double* z = T.data() + rows * ld;
+        for (int64_t j = 0; j < n; ++j) z[j] = -p->c[j];
+    } else {   // PROB_ADALLOC: rows [0,A) budgets, rows [A, A+I) assignment
+        const auto& ad = p->ad;
+        const int64_t A = ad.num_advertisers;
+        for (int64_t k = 0; k < (int64_t)ad.adv.size(); ++k) {
+            const int64_t ib = ad.adv[k] - row_first;
+            if (ib >= 0 && ib < rows) T[ib * ld + k] = ad.bid[k];
+            const int64_t ia = A + ad.imp[k] - row_first;
+            if (ia >= 0 && ia < rows) T[ia * ld + k] = 1.0;
+        }
+        for (int64_t il = 0; il < rows; ++il) {
+            const int64_t i = row_first + il;
+            T[il * ld + n + i] = 1.0;
+            T[il * ld + N] = (i < A) ? ad.budget[i] : 1.0;
+        }
+        double* z = T.data() + rows * ld;
+        for (int64_t k = 0; k < n; ++k) z[k] = -ad.bid[k];
+    }
+}
+
+void free_session(dlp_session* s) {
+    if (!s) return;
+    if (s->device >= 0) (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+    if (s->graph) (void)hipGraphDestroy(s->graph);
+    for (auto e : s->ev) (void)hipEventDestroy(e);
+    if (s->comm) (void)ncclCommDestroy(s->comm);
+    void* dev[] = {s->T, s->colq, s->prow_send, s->partials, s->cand_send, s->cand_recv,
+                   s->pp, s->basis, s->st, s->log};
+    for (void* p : dev)
+        if (p) (void)hipFree(p);
+    if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
+    if (s->host_st) (void)hipHostFree(s->host_st);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+int validate_options(const dlp_options* o) {
+    if (!o) { set_error("options is NULL"); return DLP_ERR_ARG; }
+    if (o->pricing != DLP_PRICING_DANTZIG_BLAND && o->pricing != DLP_PRICING_BLAND) {
+        set_error("unknown pricing rule");
+        return DLP_ERR_ARG;
+    }
+    if (!(o->tol_dj >= 0.0) || !(o->tol_piv >= 0.0) || o->max_pivots < 0 || o->check_interval <= 0) {
+        set_error("invalid tolerance / pivot limit / check interval");
+        return DLP_ERR_ARG;
+    }
+    return DLP_OK;
+}
+
+int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int nranks,
+                 const void* uid, dlp_session* s) {
+    s->opt = *opt;
+    s->device = opt->device;
+    s->rank = rank;
+    s->nranks = nranks;
+    s->m = prob->m;
+    s->n = prob->n;
+    s->N = prob->n + prob->m;
+    s->ld = round16(s->N + 1);
+    CALL_TRY(dlp_rank_rows(s->m, rank, nranks, &s->row_first, &s->rows));
+    s->prob_dims.m = prob->m;
+    s->prob_dims.n = prob->n;
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_error("no HIP device visible (libdlp has no CPU fallback)");
+        return DLP_ERR_NODEVICE;
+    }
+    if (s->device < 0 || s->device >= ndev) { set_error("device ordinal out of range"); return DLP_ERR_ARG; }
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+
+    const int64_t rows_total = s->rows + 1;
+    dlp::Geometry& g = s->g;
+    g.ld = s->ld;
+    g.rows = s->rows;
+    g.row_first = s->row_first;
+    g.ncols = s->N;
+    g.ntiles = (int)((s->ld + dlp::kUpdTile - 1) / dlp::kUpdTile);
+    g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block
+                                               : auto_rows_per_block(rows_total, g.ntiles);
+    const size_t tbytes = (size_t)rows_total * s->ld * sizeof(double);
+    if (hipMalloc(&s->T, tbytes) != hipSuccess) {
+        set_error("hipMalloc of the tableau failed (" + std::to_string(tbytes) + " bytes)");
+        return DLP_ERR_OOM;
+    }
+    g.T = s->T;
+    s->ratio_blocks = dlp::ratio_blocks(g);
+    HIP_TRY(hipMalloc(&s->colq, sizeof(double) * (rows_total + dlp::kColqPad)));
+    HIP_TRY(hipMemsetAsync(s->colq, 0, sizeof(double) * (rows_total + dlp::kColqPad), s->stream));
+    s->exchange = nranks > 1 || uid != nullptr;
+    HIP_TRY(hipMalloc(&s->prow_send, sizeof(int64_t) * s->ld));
+    if (s->exchange)
+        HIP_TRY(hipMalloc(&s->prow_recv, sizeof(int64_t) * s->ld));
+    else
+        s->prow_recv = s->prow_send;
+    HIP_TRY(hipMalloc(&s->partials, sizeof(dlp::Cand) * s->ratio_blocks));
+    HIP_TRY(hipMalloc(&s->cand_send, sizeof(dlp::Cand)));
+    HIP_TRY(hipMalloc(&s->cand_recv, sizeof(dlp::Cand) * nranks));
+    HIP_TRY(hipMalloc(&s->pp, sizeof(dlp::PricePart) * g.ntiles));
+    HIP_TRY(hipMalloc(&s->basis, sizeof(int32_t) * s->m));
+    HIP_TRY(hipMalloc(&s->st, sizeof(dlp::DevState)));
+    s->log_cap = opt->log_pivots ? std::max<int64_t>(1, opt->max_pivots) : 0;
+    if (s->log_cap > 0) HIP_TRY(hipMalloc(&s->log, sizeof(dlp_pivot) * s->log_cap));
+    HIP_TRY(hipHostMalloc(&s->host_st, sizeof(dlp::DevState), hipHostMallocDefault));
+    HIP_TRY(hipMemsetAsync(s->prow_send, 0, sizeof(int64_t) * s->ld, s->stream));
+
+    // tableau
+    if (prob->kind == dlp::PROB_RANDOM) {
+        HIP_TRY(dlp::launch_generate(g, prob->gen_kind, s->m, s->n, prob->seed, s->stream));
+    } else {
+        std::vector<double> host;
+        host_tableau(prob, s->row_first, s->rows, s->ld, host);
+        HIP_TRY(hipMemcpyAsync(s->T, host.data(), tbytes, hipMemcpyHostToDevice, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
+    std::vector<int32_t> basis(s->m);
+    for (int64_t i = 0; i < s->m; ++i) basis[i] = (int32_t)(s->n + i);
+    HIP_TRY(hipMemcpyAsync(s->basis, basis.data(), sizeof(int32_t) * s->m, hipMemcpyHostToDevice,
+                           s->stream));
+    dlp::DevState st0{};
+    st0.status = DLP_RUNNING;
+    st0.q = -1;
+    st0.p = -1;
+    st0.p_local = -1;
+    st0.leaving = -1;
+    st0.bland = opt->pricing == DLP_PRICING_BLAND ? 1 : 0;
+    *s->host_st = st0;
+    HIP_TRY(hipMemcpyAsync(s->st, s->host_st, sizeof(st0), hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(dlp::launch_price_init(g, s->pp, opt->tol_dj, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+
+    if (uid) {
+        ncclUniqueId id;
+        std::memcpy(&id, uid, sizeof(id));
+        NCCL_TRY(ncclCommInitRank(&s->comm, nranks, id, rank));
+        s->use_rccl = true;
+    }
+    s->ev_per_pivot = opt->timing == 1 ? 2 : (opt->timing >= 2 ? 5 : 0);
+    if (s->ev_per_pivot) {
+        s->ev.resize((size_t)s->ev_per_pivot * opt->check_interval);
+        for (auto& e : s->ev) HIP_TRY(hipEventCreate(&e));
+    }
+    return DLP_OK;
+}
+
+// ---- one pivot, as stream-ordered launches ------------------------------
+int enqueue_candidate(dlp_session* s) {
+    const dlp_options& o = s->opt;
+    HIP_TRY(dlp::launch_ratio(s->g, s->basis, s->basis, s->pp, s->st, s->colq, s->partials,
+                              s->ratio_blocks, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
+                              o.tol_piv,
+                              o.pricing, s->log, s->log_cap, s->stream));
+    return DLP_OK;
+}
+int enqueue_select(dlp_session* s) {
+    const dlp_options& o = s->opt;
+    if (s->exchange)
+        HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, o.pricing,
+                                   s->log, s->log_cap, s->stream));
+    return DLP_OK;
+}
+int enqueue_prow(dlp_session* s) {
+    HIP_TRY(dlp::launch_prow(s->g, s->st, s->prow_send, s->nranks, s->stream));
+    return DLP_OK;
+}
+int enqueue_update(dlp_session* s) {
+    const dlp_options& o = s->opt;
+    HIP_TRY(dlp::launch_update(s->g, s->colq, (const double*)s->prow_recv, s->st, s->pp, o.tol_dj,
+                               s->log, s->log_cap, o.nontemporal != 0, s->stream));
+    return DLP_OK;
+}
+
+int enqueue_pivot(dlp_session* s, int64_t slot) {
+    hipEvent_t* ev = s->ev_per_pivot ? &s->ev[(size_t)slot * s->ev_per_pivot] : nullptr;
+    const bool all = s->ev_per_pivot == 5;
+    if (all) HIP_TRY(hipEventRecord(ev[0], s->stream));
+    CALL_TRY(enqueue_candidate(s));
+    if (all) HIP_TRY(hipEventRecord(ev[1], s->stream));
+    if (s->exchange) {
+        NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
+                               s->stream));
+        CALL_TRY(enqueue_select(s));
+    }
+    if (all) HIP_TRY(hipEventRecord(ev[2], s->stream));
+    CALL_TRY(enqueue_prow(s));
+    if (s->exchange)
+        NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
+                               s->comm, s->stream));
+    if (all) HIP_TRY(hipEventRecord(ev[3], s->stream));
+    if (s->ev_per_pivot == 2) HIP_TRY(hipEventRecord(ev[0], s->stream));
+    CALL_TRY(enqueue_update(s));
+    if (all) HIP_TRY(hipEventRecord(ev[4], s->stream));
+    if (s->ev_per_pivot == 2) HIP_TRY(hipEventRecord(ev[1], s->stream));
+    return DLP_OK;
+}
+
+// Sync, read the device state, fold event timings of pivots that really ran.
+int poll(dlp_session* s) {
+    const int64_t before = s->npivots;
+    HIP_TRY(hipMemcpyAsync(s->host_st, s->st, sizeof(dlp::DevState), hipMemcpyDeviceToHost,
+                           s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->npivots = s->host_st->npivots;
+    if (s->host_st->status != DLP_RUNNING) s->status = s->host_st->status;
+    if (s->ev_per_pivot && s->ev_pending > 0) {
+        const int64_t real = std::min<int64_t>(s->ev_pending, s->npivots - before);
+        for (int64_t k = 0; k < real; ++k) {
+            hipEvent_t* ev = &s->ev[(size_t)k * s->ev_per_pivot];
+            float ms = 0.f;
+            if (s->ev_per_pivot == 2) {
+                HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+                s->timings[DLP_PHASE_UPDATE] += ms;
+            } else {
+                for (int ph = 0; ph < 4; ++ph) {
+                    HIP_TRY(hipEventElapsedTime(&ms, ev[ph], ev[ph + 1]));
+                    s->timings[ph] += ms;
+                }
+            }
+        }
+        s->nsamples += real;
+    }
+    s->ev_pending = 0;
+    return DLP_OK;
+}
+
+int run_window_graph(dlp_session* s, int64_t chunk) {
+    if (!s->gexec || s->graph_chunk != chunk) {
+        if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
+        if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
+        HIP_TRY(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+        int rc = DLP_OK;
+        for (int64_t k = 0; k < chunk && rc == DLP_OK; ++k) rc = enqueue_pivot(s, 0);
+        hipGraph_t gr = nullptr;
+        hipError_t e = hipStreamEndCapture(s->stream, &gr);
+        if (rc != DLP_OK) return rc;
+        HIP_TRY(e);
+        s->graph = gr;
+        HIP_TRY(hipGraphInstantiate(&s->gexec, s->graph, nullptr, nullptr, 0));
+        s->graph_chunk = chunk;
+    }
+    HIP_TRY(hipGraphLaunch(s->gexec, s->stream));
+    return DLP_OK;
+}
+
+int extract_result(dlp_session* s, dlp_result* r) {
+    HIP_TRY(hipSetDevice(s->device));
+    CALL_TRY(poll(s));
+    r->m = s->m;
+    r->n = s->n;
+    r->status = s->status == DLP_RUNNING ? DLP_PIVOT_LIMIT : s->status;
+    r->npivots = s->npivots;
+    std::vector<double> z(s->ld), rhs(s->rows);
+    HIP_TRY(hipMemcpyAsync(z.data(), s->T + s->rows * s->ld, sizeof(double) * s->ld,
+                           hipMemcpyDeviceToHost, s->stream));
+    if (s->rows > 0) {
+        HIP_TRY(dlp::launch_gather_column(s->T, s->ld, s->rows, s->N, s->colq, s->stream));
+        HIP_TRY(hipMemcpyAsync(rhs.data(), s->colq, sizeof(double) * s->rows,
+                               hipMemcpyDeviceToHost, s->stream));
+    }
+    r->basis.resize(s->m);
+    HIP_TRY(hipMemcpyAsync(r->basis.data(), s->basis, sizeof(int32_t) * s->m,
+                           hipMemcpyDeviceToHost, s->stream));
+    const int64_t nlog = std::min(s->npivots, s->log_cap);
+    r->log.resize(nlog);
+    if (nlog > 0)
+        HIP_TRY(hipMemcpyAsync(r->log.data(), s->log, sizeof(dlp_pivot) * nlog,
+                               hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    r->objective = z[s->N];
+    r->x.assign(s->n, 0.0);
+    for (int64_t il = 0; il < s->rows; ++il) {
+        const int32_t v = r->basis[s->row_first + il];
+        if (v < s->n) r->x[v] = rhs[il];
+    }
+    r->y.resize(s->m);
+    for (int64_t i = 0; i < s->m; ++i) r->y[i] = z[s->n + i];
+    for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) r->timings[ph] = s->timings[ph];
+    return DLP_OK;
+}
+
+}  // namespace
+
+// =========================================================================
+extern "C" {
+
+void dlp_options_default(dlp_options* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->device = 0;
+    o->pricing = DLP_PRICING_DANTZIG_BLAND;
+    o->tol_dj = 1e-9;
+    o->tol_piv = 1e-9;
+    o->max_pivots = 1000000;
+    o->log_pivots = 1;
+    o->check_interval = 64;
+    o->timing = 0;
+    o->nontemporal = 1;
+    o->rows_per_block = 0;
+    o->use_graph = 1;
+}
+
+const char* dlp_status_string(int st) {
+    switch (st) {
+        case DLP_OK: return "optimal";
+        case DLP_INFEASIBLE: return "infeasible";
+        case DLP_UNBOUNDED: return "unbounded";
+        case DLP_PIVOT_LIMIT: return "pivot limit";
+        case DLP_RUNNING: return "running";
+        case DLP_ERR_ARG: return "invalid argument";
+        case DLP_ERR_OOM: return "out of device memory";
+        case DLP_ERR_HIP: return "HIP error";
+        case DLP_ERR_RCCL: return "RCCL error";
+        case DLP_ERR_NODEVICE: return "no HIP device";
+        case DLP_ERR_STATE: return "invalid state";
+        case DLP_ERR_UNSUPPORTED: return "unsupported";
+        default: return "unknown status";
+    }
+}
+
+const char* dlp_last_error(void) { return dlp::g_err.c_str(); }
+
+int dlp_device_count(int* count) {
+    if (!count) return DLP_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return DLP_OK;
+}
+
+int dlp_rank_rows(int64_t m, int rank, int nranks, int64_t* first, int64_t* count) {
+    if (m < 0 || nranks <= 0 || rank < 0 || rank >= nranks || !first || !count) {
+        set_error("dlp_rank_rows: bad arguments");
+        return DLP_ERR_ARG;
+    }
+    const int64_t a = (m * rank) / nranks, b = (m * (rank + 1)) / nranks;
+    *first = a;
+    *count = b - a;
+    return DLP_OK;
+}
+
+int dlp_candidate_select(const dlp_candidate* cands, int n, int* winner) {
+    if (!cands || n <= 0 || !winner) return DLP_ERR_ARG;
+    int w = -1;
+    dlp::Cand best{};
+    best.valid = 0;
+    for (int r = 0; r < n; ++r) {
+        dlp::Cand c;
+        std::memcpy(&c, &cands[r], sizeof(c));
+        if (dlp::cand_better(c, best)) { best = c; w = r; }
+    }
+    *winner = w;
+    return DLP_OK;
+}
+
+int64_t dlp_tableau_ld(int64_t m, int64_t n) { return round16(n + m + 1); }
+
+int dlp_problem_create_dense(int64_t m, int64_t n, const double* A, const double* b,
+                             const double* c, dlp_problem** out) {
+    if (!out || m <= 0 || n <= 0 || !A || !b || !c || n + m + 1 > INT32_MAX) {
+        set_error("dlp_problem_create_dense: bad arguments");
+        return DLP_ERR_ARG;
+    }
+    for (int64_t i = 0; i < m; ++i)
+        if (!(b[i] >= 0.0)) {
+            set_error("b must be >= 0 (slack starting basis; Phase I is not implemented)");
+            return DLP_ERR_UNSUPPORTED;
+        }
+    auto* p = new (std::nothrow) dlp_problem();
+    if (!p) return DLP_ERR_OOM;
+    p->kind = dlp::PROB_DENSE;
+    p->m = m;
+    p->n = n;
+    p->A.assign(A, A + m * n);
+    p->b.assign(b, b + m);
+    p->c.assign(c, c + n);
+    *out = p;
+    return DLP_OK;
+}
+
+int dlp_problem_create_random(int kind, int64_t m, int64_t n, uint64_t seed, dlp_problem** out) {
+    if (!out || m <= 0 || n <= 0 || (kind != DLP_GEN_DENSE && kind != DLP_GEN_DEGENERATE) ||
+        n + m + 1 > INT32_MAX) {
+        set_error("dlp_problem_create_random: bad arguments");
+        return DLP_ERR_ARG;
+    }
+    auto* p = new (std::nothrow) dlp_problem();
+    if (!p) return DLP_ERR_OOM;
+    p->kind = dlp::PROB_RANDOM;
+    p->m = m;
+    p->n = n;
+    p->gen_kind = kind;
+    p->seed = seed;
+    *out = p;
+    return DLP_OK;
+}
+
+int dlp_problem_create_adalloc(int num_advertisers, int num_impressions, int num_slots,
+                               double bid_sparsity, double scaling_factor, dlp_problem** out) {
+    if (!out || num_slots != 1) {
+        set_error("dlp_problem_create_adalloc: num_slots must be 1 (as every reference scenario)");
+        return DLP_ERR_ARG;
+    }
+    auto* p = new (std::nothrow) dlp_problem();
+    if (!p) return DLP_ERR_OOM;
+    int rc = dlp::build_adalloc(num_advertisers, num_impressions, bid_sparsity, scaling_factor,
+                                &p->ad);
+    if (rc != DLP_OK) {
+        delete p;
+        set_error("dlp_problem_create_adalloc: bad arguments");
+        return rc;
+    }
+    p->kind = dlp::PROB_ADALLOC;
+    p->m = (int64_t)num_advertisers + num_impressions;
+    p->n = (int64_t)p->ad.adv.size();
+    *out = p;
+    return DLP_OK;
+}
+
+int dlp_problem_dims(const dlp_problem* p, int64_t* m, int64_t* n) {
+    if (!p) return DLP_ERR_ARG;
+    if (m) *m = p->m;
+    if (n) *n = p->n;
+    return DLP_OK;
+}
+
+int dlp_problem_get_dense(const dlp_problem* p, double* A, double* b, double* c) {
+    if (!p) return DLP_ERR_ARG;
+    if (p->kind == dlp::PROB_RANDOM) {
+        set_error("random problems are generated on the device; use dlp_session_tableau");
+        return DLP_ERR_UNSUPPORTED;
+    }
+    std::vector<double> T;
+    const int64_t ld = round16(p->n + p->m + 1);
+    host_tableau(p, 0, p->m, ld, T);
+    for (int64_t i = 0; i < p->m; ++i) {
+        if (A) std::memcpy(A + i * p->n, T.data() + i * ld, sizeof(double) * p->n);
+        if (b) b[i] = T[i * ld + p->n + p->m];
+    }
+    if (c)
+        for (int64_t j = 0; j < p->n; ++j) c[j] = -T[p->m * ld + j];
+    return DLP_OK;
+}
+
+int dlp_problem_adalloc_bids(const dlp_problem* p, int64_t* nnz, int32_t* adv, int32_t* imp,
+                             double* bid) {
+    if (!p || !nnz || p->kind != dlp::PROB_ADALLOC) return DLP_ERR_ARG;
+    *nnz = (int64_t)p->ad.adv.size();
+    if (adv) std::memcpy(adv, p->ad.adv.data(), sizeof(int32_t) * p->ad.adv.size());
+    if (imp) std::memcpy(imp, p->ad.imp.data(), sizeof(int32_t) * p->ad.imp.size());
+    if (bid) std::memcpy(bid, p->ad.bid.data(), sizeof(double) * p->ad.bid.size());
+    return DLP_OK;
+}
+
+void dlp_problem_free(dlp_problem* p) { delete p; }
+
+int dlp_session_create_rank(const dlp_problem* prob, const dlp_options* opt, int rank,
+                            int nranks, const void* uid, dlp_session** out) {
+    if (!prob || !out || nranks <= 0 || rank < 0 || rank >= nranks) {
+        set_error("dlp_session_create_rank: bad arguments");
+        return DLP_ERR_ARG;
+    }
+    CALL_TRY(validate_options(opt));
+    auto* s = new (std::nothrow) dlp_session();
+    if (!s) return DLP_ERR_OOM;
+    int rc = DLP_OK;
+    try {
+        rc = session_init(prob, opt, rank, nranks, uid, s);
+    } catch (const std::exception& e) {
+        set_error(std::string("session_init: ") + e.what());
+        rc = DLP_ERR_OOM;
+    }
+    if (rc != DLP_OK) {
+        free_session(s);
+        return rc;
+    }
+    *out = s;
+    return DLP_OK;
+}
+
+int dlp_session_create(const dlp_problem* prob, const dlp_options* opt, dlp_session** out) {
+    return dlp_session_create_rank(prob, opt, 0, 1, nullptr, out);
+}
+
+int dlp_comm_unique_id(void* out128) {
+    if (!out128) return DLP_ERR_ARG;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(out128, &id, sizeof(id));
+    return DLP_OK;
+}
+
+int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
+    if (!s || max_pivots < 0) return DLP_ERR_ARG;
+    if (s->exchange && !s->use_rccl) {
+        set_error("session has no RCCL communicator: drive it with dlp_session_step_*");
+        return DLP_ERR_STATE;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    const int64_t start = s->npivots;
+    int64_t budget = std::min<int64_t>(max_pivots, s->opt.max_pivots - s->launched);
+    const bool graph = s->opt.use_graph && !s->exchange && s->ev_per_pivot == 0;
+    while (s->status == DLP_RUNNING && budget > 0) {
+        const int64_t chunk = std::min<int64_t>(budget, s->opt.check_interval);
+        if (graph && chunk == s->opt.check_interval) {
+            CALL_TRY(run_window_graph(s, chunk));
+        } else {
+            for (int64_t k = 0; k < chunk; ++k) CALL_TRY(enqueue_pivot(s, k));
+            s->ev_pending = s->ev_per_pivot ? chunk : 0;
+        }
+        s->launched += chunk;
+        budget -= chunk;
+        CALL_TRY(poll(s));
+    }
+    if (pivots_done) *pivots_done = s->npivots - start;
+    if (s->status != DLP_RUNNING) return s->status;
+    if (s->launched >= s->opt.max_pivots) return DLP_PIVOT_LIMIT;
+    return DLP_RUNNING;
+}
+
+int dlp_session_step_candidate(dlp_session* s) {
+    if (!s) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    return enqueue_candidate(s);
+}
+
+int dlp_session_step_select(dlp_session* s) {
+    if (!s) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    CALL_TRY(enqueue_select(s));
+    return enqueue_prow(s);
+}
+
+int dlp_session_step_update(dlp_session* s) {
+    if (!s) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    CALL_TRY(enqueue_update(s));
+    s->launched += 1;
+    return DLP_OK;
+}
+
+int dlp_session_buffer(dlp_session* s, int which, void** dev_ptr, size_t* bytes) {
+    if (!s || !dev_ptr || !bytes) return DLP_ERR_ARG;
+    switch (which) {
+        case DLP_BUF_CAND_SEND: *dev_ptr = s->cand_send; *bytes = sizeof(dlp::Cand); break;
+        case DLP_BUF_CAND_RECV: *dev_ptr = s->cand_recv; *bytes = sizeof(dlp::Cand) * s->nranks; break;
+        case DLP_BUF_PROW_SEND: *dev_ptr = s->prow_send; *bytes = sizeof(int64_t) * s->ld; break;
+        case DLP_BUF_PROW_RECV: *dev_ptr = s->prow_recv; *bytes = sizeof(int64_t) * s->ld; break;
+        default: return DLP_ERR_ARG;
+    }
+    return DLP_OK;
+}
+
+int dlp_session_read_buffer(dlp_session* s, int which, void* host, size_t bytes) {
+    void* dev = nullptr;
+    size_t cap = 0;
+    CALL_TRY(dlp_session_buffer(s, which, &dev, &cap));
+    if (!host || bytes > cap) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return DLP_OK;
+}
+
+int dlp_session_write_buffer(dlp_session* s, int which, const void* host, size_t bytes) {
+    void* dev = nullptr;
+    size_t cap = 0;
+    CALL_TRY(dlp_session_buffer(s, which, &dev, &cap));
+    if (!host || bytes > cap) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return DLP_OK;
+}
+
+int dlp_session_sync(dlp_session* s) {
+    if (!s) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    return poll(s);
+}
+
+int dlp_session_status(dlp_session* s, int* status, int64_t* npivots) {
+    if (!s) return DLP_ERR_ARG;
+    CALL_TRY(dlp_session_sync(s));
+    if (status) *status = s->status;
+    if (npivots) *npivots = s->npivots;
+    return DLP_OK;
+}
+
+int dlp_session_timings(dlp_session* s, double* ms_out, int64_t* nsamples) {
+    if (!s || !ms_out) return DLP_ERR_ARG;
+    for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) ms_out[ph] = s->timings[ph];
+    if (nsamples) *nsamples = s->nsamples;
+    return DLP_OK;
+}
+
+int dlp_session_reset_timings(dlp_session* s) {
+    if (!s) return DLP_ERR_ARG;
+    for (double& t : s->timings) t = 0.0;
+    s->nsamples = 0;
+    return DLP_OK;
+}
+
+int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,
+                     int64_t* ncols) {
+    if (!s) return DLP_ERR_ARG;
+    if (rows_local) *rows_local = s->rows;
+    if (row_first) *row_first = s->row_first;
+    if (ld) *ld = s->ld;
+    if (ncols) *ncols = s->N;
+    return DLP_OK;
+}
+
+int dlp_session_tableau(dlp_session* s, double* host) {
+    if (!s || !host) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemcpyAsync(host, s->T, sizeof(double) * (s->rows + 1) * s->ld,
+                           hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return DLP_OK;
+}
+
+int dlp_session_read_rows(dlp_session* s, int64_t first, int64_t count, double* host) {
+    if (!s || !host || first < 0 || count < 0 || first + count > s->rows + 1) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemcpyAsync(host, s->T + first * s->ld, sizeof(double) * count * s->ld,
+                           hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return DLP_OK;
+}
+
+int dlp_session_result(dlp_session* s, dlp_result** out) {
+    if (!s || !out) return DLP_ERR_ARG;
+    auto* r = new (std::nothrow) dlp_result();
+    if (!r) return DLP_ERR_OOM;
+    int rc = extract_result(s, r);
+    if (rc != DLP_OK) {
+        delete r;
+        return rc;
+    }
+    *out = r;
+    return DLP_OK;
+}
+
+void dlp_session_free(dlp_session* s) { free_session(s); }
+
+int dlp_solve(const dlp_problem* prob, const dlp_options* opt, dlp_result** out) {
+    dlp_options o;
+    if (opt)
+        o = *opt;
+    else
+        dlp_options_default(&o);
+    dlp_session* s = nullptr;
+    CALL_TRY(dlp_session_create(prob, &o, &s));
+    int64_t done = 0;
+    int rc = dlp_session_run(s, o.max_pivots, &done);
+    if (rc < 0) {
+        dlp_session_free(s);
+        return rc;
+    }
+    rc = dlp_session_result(s, out);
+    dlp_session_free(s);
+    return rc;
+}
+
+int dlp_result_status(const dlp_result* r) { return r ? r->status : DLP_ERR_ARG; }
+double dlp_result_objective(const dlp_result* r) { return r ? r->objective : NAN; }
+int64_t dlp_result_num_pivots(const dlp_result* r) { return r ? r->npivots : -1; }
+
+int dlp_result_x(const dlp_result* r, double* x, int64_t n) {
+    if (!r || !x || n != r->n) return DLP_ERR_ARG;
+    std::memcpy(x, r->x.data(), sizeof(double) * n);
+    return DLP_OK;
+}
+int dlp_result_y(const dlp_result* r, double* y, int64_t m) {
+    if (!r || !y || m != r->m) return DLP_ERR_ARG;
+    std::memcpy(y, r->y.data(), sizeof(double) * m);
+    return DLP_OK;
+}
+int dlp_result_basis(const dlp_result* r, int32_t* basis, int64_t m) {
+    if (!r || !basis || m != r->m) return DLP_ERR_ARG;
+    std::memcpy(basis, r->basis.data(), sizeof(int32_t) * m);
+    return DLP_OK;
+}
+int dlp_result_pivot_log(const dlp_result* r, dlp_pivot* log, int64_t cap, int64_t* count) {
+    if (!r) return DLP_ERR_ARG;
+    const int64_t n = (int64_t)r->log.size();
+    if (count) *count = n;
+    if (log && cap > 0) std::memcpy(log, r->log.data(), sizeof(dlp_pivot) * std::min(cap, n));
+    return DLP_OK;
+}
+int dlp_result_timings(const dlp_result* r, double* ms_out) {
+    if (!r || !ms_out) return DLP_ERR_ARG;
+    for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) ms_out[ph] = r->timings[ph];
+    return DLP_OK;
+}
+void dlp_result_free(dlp_result* r) { delete r; }
+
+}  // extern "C"

@@ -1,0 +1,313 @@
+"""Python host API over the C ABI (include/dlp.h).
+
+Mirrors the reference's problem-loading / solver-entry / result surface
+(R/instance.h:41-57): ``Problem.adalloc`` regenerates the reference instance
+(``Instance(...)`` + ``GenerateInstance()``), ``solve`` replaces
+``RunMultiplicativeWeights`` with the exact GPU simplex, and ``Result`` exposes
+what the reference keeps in the private ``solution_`` (R/instance.h:34) and
+prints as "Dual Value" (R/global_problem.cpp:320-322).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+STATUS_NAMES = {L.OK: "optimal", L.INFEASIBLE: "infeasible", L.UNBOUNDED: "unbounded",
+                L.PIVOT_LIMIT: "pivot limit", L.RUNNING: "running"}
+
+PIVOT_DTYPE = np.dtype([("q", "<i4"), ("p", "<i4"), ("leaving", "<i4"), ("pad", "<i4"),
+                        ("ratio", "<f8"), ("objective", "<f8")])
+CAND_DTYPE = np.dtype([("ratio", "<f8"), ("basis_var", "<i4"), ("row", "<i4"), ("valid", "<i4"),
+                       ("pad0", "<i4"), ("pivot", "<f8")])
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Problem:
+    """An LP  max c^T x  s.t.  A x <= b, x >= 0 (b >= 0), owned by libdlp."""
+
+    def __init__(self, handle: int, kind: str):
+        self._h = C.c_void_p(handle)
+        self.kind = kind
+        m, n = C.c_int64(), C.c_int64()
+        L.check(L.lib().dlp_problem_dims(self._h, C.byref(m), C.byref(n)), "dlp_problem_dims")
+        self.m, self.n = m.value, n.value
+
+    @classmethod
+    def dense(cls, A, b, c) -> "Problem":
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        m, n = A.shape
+        if b.shape != (m,) or c.shape != (n,):
+            raise ValueError("shape mismatch: A (m,n), b (m,), c (n,)")
+        h = C.c_void_p()
+        L.check(L.lib().dlp_problem_create_dense(m, n, _dptr(A), _dptr(b), _dptr(c), C.byref(h)),
+                "dlp_problem_create_dense")
+        return cls(h.value, "dense")
+
+    @classmethod
+    def random(cls, m: int, n: int, seed: int, degenerate: bool = False) -> "Problem":
+        h = C.c_void_p()
+        kind = L.GEN_DEGENERATE if degenerate else L.GEN_DENSE
+        L.check(L.lib().dlp_problem_create_random(kind, m, n, seed, C.byref(h)),
+                "dlp_problem_create_random")
+        return cls(h.value, "random")
+
+    @classmethod
+    def adalloc(cls, num_advertisers: int, num_impressions: int, num_slots: int = 1,
+                bid_sparsity: float = 0.1, scaling_factor: float = 0.25) -> "Problem":
+        """The reference's generated instance (R/instance.cpp:32-57), as an exact LP."""
+        h = C.c_void_p()
+        L.check(L.lib().dlp_problem_create_adalloc(num_advertisers, num_impressions, num_slots,
+                                                   bid_sparsity, scaling_factor, C.byref(h)),
+                "dlp_problem_create_adalloc")
+        return cls(h.value, "adalloc")
+
+    def to_dense(self):
+        A = np.zeros((self.m, self.n))
+        b = np.zeros(self.m)
+        c = np.zeros(self.n)
+        L.check(L.lib().dlp_problem_get_dense(self._h, _dptr(A), _dptr(b), _dptr(c)),
+                "dlp_problem_get_dense")
+        return A, b, c
+
+    def adalloc_bids(self):
+        nnz = C.c_int64()
+        L.check(L.lib().dlp_problem_adalloc_bids(self._h, C.byref(nnz), None, None, None),
+                "dlp_problem_adalloc_bids")
+        adv = np.zeros(nnz.value, np.int32)
+        imp = np.zeros(nnz.value, np.int32)
+        bid = np.zeros(nnz.value)
+        L.check(L.lib().dlp_problem_adalloc_bids(
+            self._h, C.byref(nnz), adv.ctypes.data_as(C.POINTER(C.c_int32)),
+            imp.ctypes.data_as(C.POINTER(C.c_int32)), _dptr(bid)), "dlp_problem_adalloc_bids")
+        return adv, imp, bid
+
+    def close(self):
+        if self._h:
+            L.lib().dlp_problem_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class Result:
+    status: int
+    objective: float
+    num_pivots: int
+    x: np.ndarray
+    y: np.ndarray
+    basis: np.ndarray
+    pivot_log: np.ndarray
+    timings_ms: np.ndarray = field(default_factory=lambda: np.zeros(4))
+
+    @property
+    def status_name(self) -> str:
+        return STATUS_NAMES.get(self.status, str(self.status))
+
+
+def _result_from_handle(h: C.c_void_p, m: int, n: int) -> Result:
+    lib = L.lib()
+    try:
+        x = np.zeros(n)
+        y = np.zeros(m)
+        basis = np.zeros(m, np.int32)
+        L.check(lib.dlp_result_x(h, _dptr(x), n), "dlp_result_x")
+        L.check(lib.dlp_result_y(h, _dptr(y), m), "dlp_result_y")
+        L.check(lib.dlp_result_basis(h, basis.ctypes.data_as(C.POINTER(C.c_int32)), m),
+                "dlp_result_basis")
+        cnt = C.c_int64()
+        L.check(lib.dlp_result_pivot_log(h, None, 0, C.byref(cnt)), "dlp_result_pivot_log")
+        log = np.zeros(cnt.value, PIVOT_DTYPE)
+        if cnt.value:
+            L.check(lib.dlp_result_pivot_log(h, log.ctypes.data_as(C.POINTER(L.Pivot)), cnt.value,
+                                             C.byref(cnt)), "dlp_result_pivot_log")
+        tm = np.zeros(L.NUM_PHASES)
+        L.check(lib.dlp_result_timings(h, _dptr(tm)), "dlp_result_timings")
+        return Result(status=lib.dlp_result_status(h), objective=lib.dlp_result_objective(h),
+                      num_pivots=lib.dlp_result_num_pivots(h), x=x, y=y, basis=basis,
+                      pivot_log=log, timings_ms=tm)
+    finally:
+        lib.dlp_result_free(h)
+
+
+def options(**kw) -> L.Options:
+    return L.default_options(**kw)
+
+
+def solve(problem: Problem, **opts) -> Result:
+    """One-shot single-GPU solve (dlp_solve)."""
+    o = options(**opts)
+    h = C.c_void_p()
+    L.check(L.lib().dlp_solve(problem._h, C.byref(o), C.byref(h)), "dlp_solve")
+    return _result_from_handle(h, problem.m, problem.n)
+
+
+class Session:
+    """HBM-resident tableau (dlp_session_*): single GPU, or one row-block rank."""
+
+    def __init__(self, problem: Problem, rank: int = 0, nranks: int = 1, rccl_id: bytes | None = None,
+                 **opts):
+        self.problem = problem
+        self.rank, self.nranks = rank, nranks
+        self.exchange = nranks > 1 or rccl_id is not None
+        self.opts = options(**opts)
+        h = C.c_void_p()
+        uid = C.create_string_buffer(rccl_id, 128) if rccl_id is not None else None
+        L.check(L.lib().dlp_session_create_rank(problem._h, C.byref(self.opts), rank, nranks, uid,
+                                                C.byref(h)), "dlp_session_create_rank")
+        self._h = h
+        rows, first, ld, ncols = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        L.check(L.lib().dlp_session_info(h, C.byref(rows), C.byref(first), C.byref(ld),
+                                         C.byref(ncols)), "dlp_session_info")
+        self.rows, self.row_first, self.ld, self.ncols = rows.value, first.value, ld.value, ncols.value
+
+    def run(self, max_pivots: int) -> tuple[int, int]:
+        done = C.c_int64()
+        st = L.lib().dlp_session_run(self._h, max_pivots, C.byref(done))
+        L.check(st, "dlp_session_run", ok=(L.OK, L.UNBOUNDED, L.PIVOT_LIMIT, L.RUNNING))
+        return st, done.value
+
+    # caller-driven exchange (host-side communicators, see rowblock.py)
+    def step_candidate(self) -> np.ndarray:
+        L.check(L.lib().dlp_session_step_candidate(self._h), "dlp_session_step_candidate")
+        out = np.zeros(1, CAND_DTYPE)
+        L.check(L.lib().dlp_session_read_buffer(self._h, L.BUF_CAND_SEND, out.ctypes.data, 32),
+                "dlp_session_read_buffer")
+        return out
+
+    def step_select(self, gathered: np.ndarray) -> np.ndarray:
+        g = np.ascontiguousarray(gathered, dtype=CAND_DTYPE)
+        if self.exchange:
+            L.check(L.lib().dlp_session_write_buffer(self._h, L.BUF_CAND_RECV, g.ctypes.data,
+                                                     g.nbytes), "dlp_session_write_buffer")
+        L.check(L.lib().dlp_session_step_select(self._h), "dlp_session_step_select")
+        out = np.zeros(self.ld, np.int64)
+        L.check(L.lib().dlp_session_read_buffer(self._h, L.BUF_PROW_SEND, out.ctypes.data,
+                                                out.nbytes), "dlp_session_read_buffer")
+        return out
+
+    def step_update(self, prow_bits: np.ndarray) -> None:
+        p = np.ascontiguousarray(prow_bits, dtype=np.int64)
+        if self.exchange:
+            L.check(L.lib().dlp_session_write_buffer(self._h, L.BUF_PROW_RECV, p.ctypes.data,
+                                                     p.nbytes), "dlp_session_write_buffer")
+        L.check(L.lib().dlp_session_step_update(self._h), "dlp_session_step_update")
+
+    def status(self) -> tuple[int, int]:
+        st, n = C.c_int(), C.c_int64()
+        L.check(L.lib().dlp_session_status(self._h, C.byref(st), C.byref(n)), "dlp_session_status")
+        return st.value, n.value
+
+    def timings(self) -> tuple[np.ndarray, int]:
+        tm = np.zeros(L.NUM_PHASES)
+        ns = C.c_int64()
+        L.check(L.lib().dlp_session_timings(self._h, _dptr(tm), C.byref(ns)), "dlp_session_timings")
+        return tm, ns.value
+
+    def reset_timings(self):
+        L.check(L.lib().dlp_session_reset_timings(self._h), "dlp_session_reset_timings")
+
+    def tableau(self) -> np.ndarray:
+        T = np.zeros((self.rows + 1, self.ld))
+        L.check(L.lib().dlp_session_tableau(self._h, _dptr(T)), "dlp_session_tableau")
+        return T
+
+    def read_rows(self, first: int, count: int) -> np.ndarray:
+        T = np.zeros((count, self.ld))
+        L.check(L.lib().dlp_session_read_rows(self._h, first, count, _dptr(T)),
+                "dlp_session_read_rows")
+        return T
+
+    def result(self) -> Result:
+        h = C.c_void_p()
+        L.check(L.lib().dlp_session_result(self._h, C.byref(h)), "dlp_session_result")
+        return _result_from_handle(h, self.problem.m, self.problem.n)
+
+    def close(self):
+        if self._h:
+            L.lib().dlp_session_free(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class BatchResult:
+    objective: np.ndarray
+    status: np.ndarray
+    num_pivots: np.ndarray
+    basis: np.ndarray | None
+    logs: np.ndarray | None
+    kernel_ms: float
+
+
+def batched_solve(nlp: int, m: int, n: int, seed: int, degenerate: bool = False,
+                  want_basis: bool = False, log_cap: int = 0, **opts) -> BatchResult:
+    """C5: nlp independent generated LPs, one LDS-resident workgroup each."""
+    o = options(**opts)
+    obj = np.zeros(nlp)
+    st = np.zeros(nlp, np.int32)
+    npv = np.zeros(nlp, np.int64)
+    basis = np.zeros((nlp, m), np.int32) if want_basis else None
+    logs = np.zeros((nlp, log_cap), PIVOT_DTYPE) if log_cap > 0 else None
+    ms = C.c_double()
+    L.check(L.lib().dlp_batched_solve(
+        L.GEN_DEGENERATE if degenerate else L.GEN_DENSE, nlp, m, n, seed, C.byref(o), _dptr(obj),
+        st.ctypes.data_as(C.POINTER(C.c_int32)), npv.ctypes.data_as(C.POINTER(C.c_int64)),
+        basis.ctypes.data_as(C.POINTER(C.c_int32)) if basis is not None else None,
+        logs.ctypes.data_as(C.POINTER(L.Pivot)) if logs is not None else None, log_cap,
+        C.byref(ms)), "dlp_batched_solve")
+    return BatchResult(obj, st, npv, basis, logs, ms.value)
+
+
+def rank_rows(m: int, rank: int, nranks: int) -> tuple[int, int]:
+    first, count = C.c_int64(), C.c_int64()
+    L.check(L.lib().dlp_rank_rows(m, rank, nranks, C.byref(first), C.byref(count)), "dlp_rank_rows")
+    return first.value, count.value
+
+
+def candidate_select(cands: np.ndarray) -> int:
+    c = np.ascontiguousarray(cands, dtype=CAND_DTYPE)
+    w = C.c_int()
+    L.check(L.lib().dlp_candidate_select(c.ctypes.data_as(C.POINTER(L.Candidate)), len(c),
+                                         C.byref(w)), "dlp_candidate_select")
+    return w.value
+
+
+def tableau_ld(m: int, n: int) -> int:
+    return int(L.lib().dlp_tableau_ld(m, n))
+
+
+def device_count() -> int:
+    n = C.c_int()
+    L.check(L.lib().dlp_device_count(C.byref(n)), "dlp_device_count")
+    return n.value
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    L.check(L.lib().dlp_comm_unique_id(buf), "dlp_comm_unique_id")
+    return buf.raw

@@ -1,0 +1,233 @@
+/*
+ * dlp.h — C ABI of the MI355X-native dense-tableau fp64 simplex (libdlp.so).
+ *
+ * This is the drop-in boundary for the per-iteration solver core of
+ * shidanxu/DistributedLPSolver.  The reference has no FFI:
+ * its surface is in-process C++ (namespace distributed_solver).  Each entry
+ * point below names the reference interface it replaces; R/ is
+ * /root/reference/DistributedLPSolver/DistributedLPSolver/.
+ *
+ *   reference                                         this ABI
+ *   ------------------------------------------------  ---------------------------------
+ *   Instance::Instance(A, I, slots, sparsity, ...)     dlp_problem_create_adalloc
+ *     R/instance.h:41-42, R/instance.cpp:15-30
+ *   Instance::GenerateInstance()  R/instance.h:46      dlp_problem_create_adalloc (bids
+ *     R/instance.cpp:32-57                             regenerated bit-exactly, glibc rand)
+ *   (no reference: dense LP input)                     dlp_problem_create_dense / _random
+ *   Instance::RunMultiplicativeWeights(...)            dlp_solve  (exact simplex instead of
+ *     R/instance.h:52-53, R/instance.cpp:117-134       the epsilon-approximate MW loop)
+ *   GlobalProblem::ConstructPrimal per-iteration core  dlp_session_step_* (one pivot)
+ *     R/global_problem.cpp:257-323                     dlp_session_run   (K pivots)
+ *   Instance::solution_ (private, no getter)           dlp_result_x / dlp_result_y
+ *     R/instance.h:34
+ *   "Dual Value" stdout  R/global_problem.cpp:320-322  dlp_result_objective
+ *
+ * Conventions (build conventions):
+ *   - every function returns int status: DLP_OK (0) or a code below; no C++
+ *     exception ever crosses this boundary;
+ *   - the library owns problems, sessions and results; the caller frees them
+ *     with the matching *_free;
+ *   - a handle is not thread-safe; concurrent solves on distinct handles are;
+ *   - all arrays are plain host pointers unless the name says "dev";
+ *   - fp64 everywhere (the reference computes in x87 long double; see DESIGN.md
+ *     for what "parity" therefore means).
+ *
+ * Pivot rule (identical in oracle/ and on the GPU):
+ *   maximise c^T x  s.t.  A x <= b, x >= 0, b >= 0, slack starting basis.
+ *   Tableau T is (m+1) x (N+1), N = n + m, row-major, leading dimension
+ *   ld = roundup(N+1, 16); row m is the objective (z_j, initially -c_j).
+ *   price   : Dantzig q = argmin_{j<N} z_j (ties -> smallest j), optimal when
+ *             z_q >= -tol_dj; in Bland mode q = smallest j with z_j < -tol_dj.
+ *             Bland mode is entered after a degenerate pivot (r_p == 0) and
+ *             left after a non-degenerate one (DLP_PRICING_DANTZIG_BLAND), or
+ *             always on (DLP_PRICING_BLAND).
+ *   ratio   : rows i<m with T[i][q] > tol_piv; r_i = max(T[i][N],0) / T[i][q]
+ *             (IEEE division); p = argmin r_i, exact ties -> smallest basis[i];
+ *             unbounded when no row qualifies.
+ *   update  : prow_j = T[p][j] / T[p][q]; for i != p with T[i][q] != 0:
+ *             T[i][j] = fma(-T[i][q], prow_j, T[i][j]); row p := prow; rows with
+ *             T[i][q] == 0 are left untouched.
+ */
+#ifndef DLP_H
+#define DLP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define DLP_OK              0   /* optimal (or the step/run completed) */
+#define DLP_INFEASIBLE      1
+#define DLP_UNBOUNDED       2
+#define DLP_PIVOT_LIMIT     3
+#define DLP_RUNNING         4   /* session has pivots left to do */
+#define DLP_ERR_ARG        -1
+#define DLP_ERR_OOM        -2
+#define DLP_ERR_HIP        -3
+#define DLP_ERR_RCCL       -4
+#define DLP_ERR_NODEVICE   -5
+#define DLP_ERR_STATE      -6
+#define DLP_ERR_UNSUPPORTED -7
+
+/* ---- enums ------------------------------------------------------------ */
+#define DLP_PRICING_DANTZIG_BLAND 0
+#define DLP_PRICING_BLAND         1
+
+/* Synthetic instance families. */
+#define DLP_GEN_DENSE       0   /* A,x0,c ~ U[0,1); b = A x0 + U[0,1)          */
+#define DLP_GEN_DEGENERATE  1   /* as DENSE, b_i = 0 on ~50% of the rows       */
+
+/* Exchange buffers of a rank session (dlp_session_buffer). */
+#define DLP_BUF_CAND_SEND   0   /* 1 x dlp_candidate, device                   */
+#define DLP_BUF_CAND_RECV   1   /* nranks x dlp_candidate, device              */
+#define DLP_BUF_PROW_SEND   2   /* ld x int64 (fp64 bits or INT64_MIN), device */
+#define DLP_BUF_PROW_RECV   3   /* ld x int64, device                          */
+
+/* Timing phases (dlp_session_timings, milliseconds, HIP events). */
+#define DLP_PHASE_RATIO     0   /* pricing reduce + ratio test kernel          */
+#define DLP_PHASE_EXCHANGE  1   /* candidate all-gather + select (nranks > 1)  */
+#define DLP_PHASE_PROW      2   /* pivot-row normalise (+ all-reduce)          */
+#define DLP_PHASE_UPDATE    3   /* rank-1 elimination kernel                   */
+#define DLP_NUM_PHASES      4
+
+typedef struct dlp_problem dlp_problem;
+typedef struct dlp_session dlp_session;
+typedef struct dlp_result  dlp_result;
+
+/* 32-byte ratio-test candidate exchanged between ranks (all-gather). */
+typedef struct dlp_candidate {
+    double  ratio;      /* r_i */
+    int32_t basis_var;  /* basis[i] (tie-break) */
+    int32_t row;        /* global row index */
+    int32_t valid;      /* 0 = no eligible row on that rank */
+    int32_t pad0;
+    double  pivot;      /* T[row][q], the pivot element if this row wins */
+} dlp_candidate;
+
+/* 32-byte pivot-log entry: the parity artifact. */
+typedef struct dlp_pivot {
+    int32_t q;          /* entering column */
+    int32_t p;          /* pivot row (global) */
+    int32_t leaving;    /* basis[p] before the pivot */
+    int32_t pad;
+    double  ratio;      /* r_p */
+    double  objective;  /* T[m][N] after the pivot */
+} dlp_pivot;
+
+typedef struct dlp_options {
+    int32_t device;          /* HIP device ordinal (default 0) */
+    int32_t pricing;         /* DLP_PRICING_* */
+    double  tol_dj;          /* reduced-cost tolerance (default 1e-9) */
+    double  tol_piv;         /* pivot-element tolerance (default 1e-9) */
+    int64_t max_pivots;      /* pivot limit (default 1000000) */
+    int32_t log_pivots;      /* keep the pivot log (default 1) */
+    int32_t check_interval;  /* pivots between host status polls (default 64) */
+    int32_t timing;          /* 0 none, 1 update kernel, 2 every phase */
+    int32_t nontemporal;     /* update kernel uses nt loads/stores (default 1) */
+    int32_t rows_per_block;  /* update-kernel rows per workgroup (0 = auto) */
+    int32_t use_graph;       /* replay each poll window as a hipGraph (default 1) */
+} dlp_options;
+
+/* ---- library ---------------------------------------------------------- */
+void        dlp_options_default(dlp_options* opt);
+const char* dlp_status_string(int status);
+const char* dlp_last_error(void);          /* thread-local message of the last failure */
+int         dlp_device_count(int* count);
+/* Row partition of m constraint rows over nranks: [first, first+count). */
+int         dlp_rank_rows(int64_t m, int rank, int nranks, int64_t* first, int64_t* count);
+/* Deterministic winner of nranks candidates (same rule as the device select). */
+int         dlp_candidate_select(const dlp_candidate* cands, int n, int* winner);
+int64_t     dlp_tableau_ld(int64_t m, int64_t n);
+
+/* ---- problems ------------------------------------------------------------ */
+/* Dense LP: A is m x n row-major; inputs are copied. Requires b >= 0. */
+int dlp_problem_create_dense(int64_t m, int64_t n, const double* A, const double* b,
+                             const double* c, dlp_problem** out);
+/* Synthetic LP generated on the device (no host copy of A). */
+int dlp_problem_create_random(int kind, int64_t m, int64_t n, uint64_t seed, dlp_problem** out);
+/* The reference's ad-allocation LP (R/instance.cpp:32-57, R/allocation_mw.cpp:163-171):
+ * max sum b_ai x_ai  s.t.  sum_i b_ai x_ai <= B_a (A rows),  sum_a x_ai <= 1 (I rows). */
+int dlp_problem_create_adalloc(int num_advertisers, int num_impressions, int num_slots,
+                               double bid_sparsity, double scaling_factor, dlp_problem** out);
+int dlp_problem_dims(const dlp_problem* prob, int64_t* m, int64_t* n);
+/* Dense copy of the problem data (A m x n row-major, b, c); NULL pointers skipped. */
+int dlp_problem_get_dense(const dlp_problem* prob, double* A, double* b, double* c);
+/* Ad-allocation bid list in variable order: (advertiser, impression, bid) triples. */
+int dlp_problem_adalloc_bids(const dlp_problem* prob, int64_t* nnz, int32_t* adv,
+                             int32_t* imp, double* bid);
+void dlp_problem_free(dlp_problem* prob);
+
+/* ---- one-shot solve (single GPU) ---------------------------------------- */
+int dlp_solve(const dlp_problem* prob, const dlp_options* opt, dlp_result** out);
+
+/* ---- sessions: tableau resident in HBM ---------------------------------- */
+/* Single GPU (rank 0 of 1). */
+int dlp_session_create(const dlp_problem* prob, const dlp_options* opt, dlp_session** out);
+/* Row-block rank of a multi-GPU solve; exchange through RCCL when
+ * rccl_unique_id != NULL (128 bytes from dlp_comm_unique_id, identical on every
+ * rank), or through caller-driven dlp_session_step_* when it is NULL.  With
+ * nranks == 1 and an id, the RCCL exchange path runs on a 1-rank communicator
+ * (same results; used to exercise that path on one GPU). */
+int dlp_session_create_rank(const dlp_problem* prob, const dlp_options* opt, int rank,
+                            int nranks, const void* rccl_unique_id, dlp_session** out);
+int dlp_comm_unique_id(void* out128);
+/* Launch up to max_pivots more pivots; returns DLP_OK / DLP_UNBOUNDED /
+ * DLP_PIVOT_LIMIT / DLP_RUNNING (pivot budget of this call spent). */
+int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done);
+/* Caller-driven pivot (external communicator), in this order per pivot:
+ *   step_candidate -> all-gather CAND_SEND into CAND_RECV (nranks x 32 B)
+ *   step_select    -> all-reduce(MAX, int64) PROW_SEND into PROW_RECV (ld x 8 B)
+ *   step_update.   With nranks == 1 no exchange is needed. */
+int dlp_session_step_candidate(dlp_session* s);
+int dlp_session_step_select(dlp_session* s);
+int dlp_session_step_update(dlp_session* s);
+int dlp_session_buffer(dlp_session* s, int which, void** dev_ptr, size_t* bytes);
+/* Synchronous host copies of an exchange buffer (for host-side communicators). */
+int dlp_session_read_buffer(dlp_session* s, int which, void* host, size_t bytes);
+int dlp_session_write_buffer(dlp_session* s, int which, const void* host, size_t bytes);
+int dlp_session_sync(dlp_session* s);
+int dlp_session_status(dlp_session* s, int* status, int64_t* npivots);
+int dlp_session_timings(dlp_session* s, double* ms_out /* DLP_NUM_PHASES */, int64_t* nsamples);
+int dlp_session_reset_timings(dlp_session* s);
+int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,
+                     int64_t* ncols);
+/* Copy the local tableau (rows_local+1 rows x ld, objective last) to the host. */
+int dlp_session_tableau(dlp_session* s, double* host);
+/* Copy local rows [first, first+count) (row rows_local = objective) to the host. */
+int dlp_session_read_rows(dlp_session* s, int64_t first, int64_t count, double* host);
+int dlp_session_result(dlp_session* s, dlp_result** out);
+void dlp_session_free(dlp_session* s);
+
+/* ---- batched small LPs ------------------
+ * nlp independent LPs of size m x n, LP k generated on the device with seed
+ * (seed + k) by the DLP_GEN_* family `kind`; one workgroup per LP solves it
+ * with its whole tableau resident in LDS (rule as above, bit-identical to a
+ * single-LP solve).  Per-LP outputs (NULL to skip): objective[nlp],
+ * status[nlp], npivots[nlp], basis[nlp*m], logs[nlp*log_cap] (first log_cap
+ * pivots of each LP).  *kernel_ms gets the solve kernel's device time.
+ * Reference analog: the independent per-impression subproblems solved in a
+ * loop, R/global_problem.cpp:270-274. */
+int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, uint64_t seed,
+                      const dlp_options* opt, double* objective, int32_t* status,
+                      int64_t* npivots, int32_t* basis, dlp_pivot* logs, int64_t log_cap,
+                      double* kernel_ms);
+
+/* ---- results ------------------------------------------------------------- */
+int     dlp_result_status(const dlp_result* r);
+double  dlp_result_objective(const dlp_result* r);
+int64_t dlp_result_num_pivots(const dlp_result* r);
+/* x (n, this rank's basic rows only when nranks > 1), y (m, duals), basis (m). */
+int dlp_result_x(const dlp_result* r, double* x, int64_t n);
+int dlp_result_y(const dlp_result* r, double* y, int64_t m);
+int dlp_result_basis(const dlp_result* r, int32_t* basis, int64_t m);
+int dlp_result_pivot_log(const dlp_result* r, dlp_pivot* log, int64_t cap, int64_t* count);
+int dlp_result_timings(const dlp_result* r, double* ms_out /* DLP_NUM_PHASES */);
+void dlp_result_free(dlp_result* r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLP_H */

@@ -1,0 +1,228 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of oracle/liboracle.so (the CPU
+restatement of the pivot rule, oracle/oracle.h).  Imported by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg only — never by the
+product package."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+PIVOT_DTYPE = np.dtype([("q", "<i4"), ("p", "<i4"), ("leaving", "<i4"), ("pad", "<i4"),
+                        ("ratio", "<f8"), ("objective", "<f8")])
+CAND_DTYPE = np.dtype([("ratio", "<f8"), ("basis_var", "<i4"), ("row", "<i4"), ("valid", "<i4"),
+                       ("pad0", "<i4"), ("pivot", "<f8")])
+
+
+class Opts(C.Structure):
+    _fields_ = [("pricing", C.c_int32), ("tol_dj", C.c_double), ("tol_piv", C.c_double),
+                ("max_pivots", C.c_int64), ("nthreads", C.c_int32)]
+
+
+_lib = None
+_D = C.POINTER(C.c_double)
+_I32 = C.POINTER(C.c_int32)
+_I64 = C.POINTER(C.c_int64)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_PATH):
+            raise RuntimeError(f"{ORACLE_PATH} missing: run `make -C oracle`")
+        L = C.CDLL(ORACLE_PATH)
+        L.oracle_gen_dense.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_uint64, _D, _D, _D]
+        L.oracle_gen_tableau.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_uint64, C.c_int64,
+                                         C.c_int64, C.c_int64, _D, C.c_int32]
+        L.oracle_ld.restype = C.c_int64
+        L.oracle_ld.argtypes = [C.c_int64, C.c_int64]
+        L.oracle_gen_adalloc.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, _I64, _I32,
+                                         _I32, _D, _D, _I32, _D]
+        L.oracle_solve_dense.argtypes = [C.c_int64, C.c_int64, _D, _D, _D, C.POINTER(Opts), _D, _D,
+                                         _D, _I32, C.c_void_p, C.c_int64, _I64, C.POINTER(C.c_int)]
+        L.oracle_slice_create.argtypes = [C.c_int64, C.c_int64, _D, _D, _D, C.c_int64, C.c_int64,
+                                          C.POINTER(Opts), C.POINTER(C.c_void_p)]
+        L.oracle_slice_candidate.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+        L.oracle_slice_select.argtypes = [C.c_void_p, C.c_void_p, C.c_int, _I64, C.POINTER(C.c_int)]
+        L.oracle_slice_update.argtypes = [C.c_void_p, _I64]
+        L.oracle_slice_ld.restype = C.c_int64
+        L.oracle_slice_ld.argtypes = [C.c_void_p]
+        L.oracle_slice_npivots.restype = C.c_int64
+        L.oracle_slice_npivots.argtypes = [C.c_void_p]
+        L.oracle_slice_log.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_slice_tableau.argtypes = [C.c_void_p, _D]
+        L.oracle_slice_free.argtypes = [C.c_void_p]
+        L.oracle_bench_pivots.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_uint64, C.c_int64,
+                                          C.c_int64, C.c_int32, _D, _I64, _D]
+        L.oracle_run_generated.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_uint64, C.c_int64,
+                                           C.c_int32, C.c_void_p, _I64, _I64, C.c_int64, _D, _I32]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(_D)
+
+
+def gen_dense(m, n, seed, degenerate=False):
+    A = np.zeros((m, n))
+    b = np.zeros(m)
+    c = np.zeros(n)
+    rc = lib().oracle_gen_dense(1 if degenerate else 0, m, n, seed, _d(A), _d(b), _d(c))
+    assert rc == 0
+    return A, b, c
+
+
+def ld(m, n):
+    return int(lib().oracle_ld(m, n))
+
+
+def gen_tableau(m, n, seed, degenerate=False, row_first=0, row_count=None, nthreads=4):
+    row_count = m - row_first if row_count is None else row_count
+    L_ = ld(m, n)
+    T = np.zeros((row_count + 1, L_))
+    rc = lib().oracle_gen_tableau(1 if degenerate else 0, m, n, seed, row_first, row_count, L_,
+                                  _d(T), nthreads)
+    assert rc == 0
+    return T
+
+
+def gen_adalloc(A, I, sparsity=0.1, scaling=0.25):
+    nnz = C.c_int64()
+    rc = lib().oracle_gen_adalloc(A, I, sparsity, scaling, C.byref(nnz), None, None, None, None,
+                                  None, None)
+    assert rc == 0
+    adv = np.zeros(nnz.value, np.int32)
+    imp = np.zeros(nnz.value, np.int32)
+    bid = np.zeros(nnz.value)
+    budgets = np.zeros(A)
+    draws = np.zeros(A, np.int32)
+    mb = C.c_double()
+    rc = lib().oracle_gen_adalloc(A, I, sparsity, scaling, C.byref(nnz),
+                                  adv.ctypes.data_as(_I32), imp.ctypes.data_as(_I32), _d(bid),
+                                  _d(budgets), draws.ctypes.data_as(_I32), C.byref(mb))
+    assert rc == 0
+    return dict(adv=adv, imp=imp, bid=bid, budgets=budgets, draws=draws, max_bid=mb.value)
+
+
+def adalloc_lp(A, I, sparsity=0.1, scaling=0.25):
+    """Dense LP of the ad-allocation instance: rows [0,A) budgets, [A,A+I) assignment."""
+    g = gen_adalloc(A, I, sparsity, scaling)
+    nnz = len(g["bid"])
+    M = np.zeros((A + I, nnz))
+    M[g["adv"], np.arange(nnz)] = g["bid"]
+    M[A + g["imp"], np.arange(nnz)] = 1.0
+    b = np.concatenate([g["budgets"], np.ones(I)])
+    return M, b, g["bid"].copy()
+
+
+class Solution:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def solve_dense(A, b, c, pricing=0, tol_dj=1e-9, tol_piv=1e-9, max_pivots=1_000_000, nthreads=4,
+                log_cap=None):
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    m, n = A.shape
+    o = Opts(pricing, tol_dj, tol_piv, max_pivots, nthreads)
+    x = np.zeros(n)
+    y = np.zeros(m)
+    obj = C.c_double()
+    basis = np.zeros(m, np.int32)
+    cap = max_pivots if log_cap is None else log_cap
+    cap = min(cap, 2_000_000)
+    log = np.zeros(cap, PIVOT_DTYPE)
+    npiv = C.c_int64()
+    st = C.c_int()
+    rc = lib().oracle_solve_dense(m, n, _d(A), _d(b), _d(c), C.byref(o), _d(x), _d(y), C.byref(obj),
+                                  basis.ctypes.data_as(_I32), log.ctypes.data, cap, C.byref(npiv),
+                                  C.byref(st))
+    assert rc == 0, "oracle_solve_dense rejected the problem"
+    return Solution(status=st.value, objective=obj.value, x=x, y=y, basis=basis,
+                    pivot_log=log[:min(npiv.value, cap)], num_pivots=npiv.value)
+
+
+class OracleEngine:
+    """A simulated rank (oracle row slice) with the rowblock engine interface."""
+
+    def __init__(self, A, b, c, rank, nranks, row_first, row_count, pricing=0, tol_dj=1e-9,
+                 tol_piv=1e-9):
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        m, n = A.shape
+        self._keep = (A, np.ascontiguousarray(b, float), np.ascontiguousarray(c, float))
+        o = Opts(pricing, tol_dj, tol_piv, 1 << 40, 1)
+        h = C.c_void_p()
+        rc = lib().oracle_slice_create(m, n, _d(self._keep[0]), _d(self._keep[1]),
+                                       _d(self._keep[2]), row_first, row_count, C.byref(o),
+                                       C.byref(h))
+        assert rc == 0
+        self.h = h
+        self.ld = int(lib().oracle_slice_ld(h))
+        self.state = 4  # running
+
+    def step_candidate(self):
+        cand = np.zeros(1, CAND_DTYPE)
+        opt = C.c_int()
+        lib().oracle_slice_candidate(self.h, cand.ctypes.data, C.byref(opt))
+        if opt.value:
+            self.state = 0
+        return cand
+
+    def step_select(self, gathered):
+        g = np.ascontiguousarray(gathered, dtype=CAND_DTYPE)
+        out = np.zeros(self.ld, np.int64)
+        unb = C.c_int()
+        lib().oracle_slice_select(self.h, g.ctypes.data, len(g), out.ctypes.data_as(_I64),
+                                  C.byref(unb))
+        if unb.value:
+            self.state = 2
+        return out
+
+    def step_update(self, prow_bits):
+        p = np.ascontiguousarray(prow_bits, dtype=np.int64)
+        lib().oracle_slice_update(self.h, p.ctypes.data_as(_I64))
+
+    def status(self):
+        return self.state, int(lib().oracle_slice_npivots(self.h))
+
+    def log(self):
+        n = int(lib().oracle_slice_npivots(self.h))
+        out = np.zeros(n, PIVOT_DTYPE)
+        lib().oracle_slice_log(self.h, out.ctypes.data, n)
+        return out
+
+    def close(self):
+        if self.h:
+            lib().oracle_slice_free(self.h)
+            self.h = None
+
+
+def bench_pivots(m, n, seed, warmup, k, nthreads, degenerate=False):
+    secs = C.c_double()
+    gen = C.c_double()
+    done = C.c_int64()
+    rc = lib().oracle_bench_pivots(1 if degenerate else 0, m, n, seed, warmup, k, nthreads,
+                                   C.byref(secs), C.byref(done), C.byref(gen))
+    assert rc == 0, f"oracle_bench_pivots rc={rc}"
+    return secs.value, done.value, gen.value
+
+
+def run_generated(m, n, seed, k, rows, degenerate=False, nthreads=8):
+    """k oracle pivots on the generated tableau; returns (log, sampled rows, basis)."""
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    log = np.zeros(k, PIVOT_DTYPE)
+    npiv = C.c_int64()
+    out = np.zeros((len(rows), ld(m, n)))
+    basis = np.zeros(m, np.int32)
+    rc = lib().oracle_run_generated(1 if degenerate else 0, m, n, seed, k, nthreads, log.ctypes.data,
+                                    C.byref(npiv), rows.ctypes.data_as(_I64), len(rows), _d(out),
+                                    basis.ctypes.data_as(_I32))
+    assert rc == 0
+    return log[:npiv.value], out, basis
