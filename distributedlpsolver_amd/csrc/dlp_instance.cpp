@@ -1,0 +1,157 @@
+// dlp_instance.cpp — the reference-signature facade (include/distributed_solver/
+// instance.h) over the C ABI.  Reference: R/instance.{h,cpp}.
+#include "distributed_solver/instance.h"
+
+#include <algorithm>
+#include <iostream>
+#include <stdexcept>
+#include <vector>
+
+namespace distributed_solver {
+
+Instance::Instance(int num_advertisers, int num_impressions, int num_slots,
+                   long double bid_sparsity, long double epsilon, long double scaling_factor,
+                   long double numerical_accuracy_tolerance)
+    : num_advertisers_(num_advertisers),
+      num_impressions_(num_impressions),
+      num_slots_(num_slots),
+      bid_sparsity_(bid_sparsity),
+      epsilon_(epsilon),
+      scaling_factor_(scaling_factor),
+      numerical_accuracy_tolerance_(numerical_accuracy_tolerance) {
+    budgets_.assign(num_advertisers_ > 0 ? num_advertisers_ : 0, 0.0L);
+    SetBudgets();
+}
+
+Instance::~Instance() {
+    if (problem_) dlp_problem_free(problem_);
+}
+
+Instance::Instance(Instance&& o) noexcept
+    : max_bid_(o.max_bid_),
+      verbose(o.verbose),
+      num_advertisers_(o.num_advertisers_),
+      num_impressions_(o.num_impressions_),
+      num_slots_(o.num_slots_),
+      bid_sparsity_(o.bid_sparsity_),
+      epsilon_(o.epsilon_),
+      scaling_factor_(o.scaling_factor_),
+      numerical_accuracy_tolerance_(o.numerical_accuracy_tolerance_),
+      budgets_(std::move(o.budgets_)),
+      bids_matrix_(std::move(o.bids_matrix_)),
+      transpose_bids_matrix_(std::move(o.transpose_bids_matrix_)),
+      solution_(std::move(o.solution_)),
+      problem_(o.problem_),
+      dual_value_(o.dual_value_),
+      num_pivots_(o.num_pivots_),
+      status_(o.status_) {
+    o.problem_ = nullptr;
+}
+
+// R/instance.cpp:136-141 (average bid 0.5, integer I/A, scaling factor).
+void Instance::SetBudgets() {
+    const long double average_bid = 0.5;
+    for (int a = 0; a < num_advertisers_; ++a)
+        budgets_[a] = average_bid * (num_impressions_ / num_advertisers_) * scaling_factor_;
+}
+
+// R/instance.cpp:32-57; the bids come from libdlp's bit-exact restatement.
+void Instance::GenerateInstance() {
+    if (problem_) dlp_problem_free(problem_);
+    problem_ = nullptr;
+    int rc = dlp_problem_create_adalloc(num_advertisers_, num_impressions_, num_slots_,
+                                        (double)bid_sparsity_, (double)scaling_factor_, &problem_);
+    if (rc != DLP_OK) throw std::runtime_error(std::string("GenerateInstance: ") + dlp_last_error());
+    int64_t nnz = 0;
+    dlp_problem_adalloc_bids(problem_, &nnz, nullptr, nullptr, nullptr);
+    std::vector<int32_t> adv(nnz), imp(nnz);
+    std::vector<double> bid(nnz);
+    dlp_problem_adalloc_bids(problem_, &nnz, adv.data(), imp.data(), bid.data());
+    bids_matrix_.assign(num_advertisers_, {});
+    transpose_bids_matrix_.assign(num_impressions_, {});
+    max_bid_ = 0;
+    for (int64_t k = 0; k < nnz; ++k) {
+        bids_matrix_[adv[k]][imp[k]] = bid[k];
+        transpose_bids_matrix_[imp[k]][adv[k]] = bid[k];
+        max_bid_ = std::max<long double>(max_bid_, bid[k]);
+    }
+    if (verbose) {
+        std::cout << "Generated instance \n";
+        ReportGraphTopology();
+    }
+}
+
+// R/instance.cpp:178-185.
+void Instance::ReportGraphTopology() {
+    for (int a = 0; a < (int)bids_matrix_.size(); ++a)
+        std::cout << "Advertiser " << a << " degree is " << bids_matrix_[a].size() << "\n";
+    for (int i = 0; i < (int)transpose_bids_matrix_.size(); ++i)
+        std::cout << "Impression " << i << " degree is " << transpose_bids_matrix_[i].size() << "\n";
+}
+
+// R/instance.cpp:154-165: one (current, average) pair per bid.
+void Instance::BuildPrimals() {
+    solution_.assign(num_advertisers_, {});
+    for (int a = 0; a < num_advertisers_; ++a)
+        for (const auto& kv : bids_matrix_[a]) solution_[a][kv.first] = {0.0L, 0.0L};
+}
+
+int Instance::RunSimplex(const dlp_options& options) {
+    if (!problem_) GenerateInstance();
+    BuildPrimals();
+    dlp_result* r = nullptr;
+    status_ = dlp_solve(problem_, &options, &r);
+    if (status_ < 0) return status_;
+    status_ = dlp_result_status(r);
+    int64_t m = 0, n = 0;
+    dlp_problem_dims(problem_, &m, &n);
+    std::vector<double> x(n);
+    dlp_result_x(r, x.data(), n);
+    dual_value_ = dlp_result_objective(r);
+    num_pivots_ = dlp_result_num_pivots(r);
+    dlp_result_free(r);
+    std::vector<int32_t> adv(n), imp(n);
+    int64_t nnz = n;
+    dlp_problem_adalloc_bids(problem_, &nnz, adv.data(), imp.data(), nullptr);
+    for (int64_t k = 0; k < n; ++k) solution_[adv[k]][imp[k]] = {x[k], x[k]};
+    return status_;
+}
+
+void Instance::RunMultiplicativeWeights(long double num_iterations,
+                                        long double numerical_accuracy_tolerance, bool binary) {
+    (void)num_iterations;
+    (void)numerical_accuracy_tolerance;
+    (void)binary;
+    dlp_options o;
+    dlp_options_default(&o);
+    const int rc = RunSimplex(o);
+    if (rc < 0) throw std::runtime_error(std::string("RunMultiplicativeWeights: ") + dlp_last_error());
+    if (verbose) std::cout << "Dual Value = " << dual_value_ << "\n";
+}
+
+void Instance::RunMultiplicativeWeights(long double num_iterations,
+                                        long double numerical_accuracy_tolerance, bool binary,
+                                        long double scale, int intervals) {
+    (void)scale;
+    (void)intervals;
+    RunMultiplicativeWeights(num_iterations, numerical_accuracy_tolerance, binary);
+}
+
+long double Instance::MaxInfeasibility() const {
+    long double worst = 0;
+    for (int a = 0; a < num_advertisers_ && a < (int)solution_.size(); ++a) {
+        long double spend = 0;
+        for (const auto& kv : solution_[a]) spend += kv.second.first * bids_matrix_[a].at(kv.first);
+        worst = std::max(worst, (spend - budgets_[a]) / budgets_[a]);
+    }
+    return worst;
+}
+
+long double Instance::Revenue() const {
+    long double rev = 0;
+    for (int a = 0; a < (int)solution_.size(); ++a)
+        for (const auto& kv : solution_[a]) rev += kv.second.first * bids_matrix_[a].at(kv.first);
+    return rev;
+}
+
+}  // namespace distributed_solver

@@ -1,0 +1,85 @@
+// instance.h — C++ facade with the reference's problem-loading / solver-entry
+// / result surface, over the C ABI of include/dlp.h.
+//
+// Same constructor, GenerateInstance and RunMultiplicativeWeights signatures
+// as R/instance.h:41-53 (R/ = /root/reference/DistributedLPSolver/
+// DistributedLPSolver/), so a reference caller (R/main.cpp:44-64) compiles
+// unchanged against it.  What changes underneath: the instance is solved
+// EXACTLY by the MI355X dense-tableau simplex instead of the epsilon-approximate
+// multiplicative-weights loop; the result the reference keeps private
+// (solution_, R/instance.h:34) and prints ("Dual Value", R/global_problem.cpp:
+// 320-322) is available through Solution() / DualValue().
+#pragma once
+
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "dlp.h"
+
+namespace distributed_solver {
+
+class Instance {
+  public:
+    // R/instance.h:41-42.  num_slots must be 1 (every reference scenario).
+    Instance(int num_advertisers, int num_impressions, int num_slots, long double bid_sparsity,
+             long double epsilon, long double scaling_factor,
+             long double numerical_accuracy_tolerance);
+    ~Instance();
+    Instance(const Instance&) = delete;
+    Instance& operator=(const Instance&) = delete;
+    Instance(Instance&& o) noexcept;
+
+    // R/instance.h:46: srand(1) bid generation (R/instance.cpp:32-57), printed
+    // topology as the reference prints it (R/instance.cpp:178-185).
+    void GenerateInstance();
+    // R/instance.cpp:136-141 (called by the constructor, as in the reference).
+    void SetBudgets();
+
+    // R/instance.h:52-53.  Solve the instance's LP exactly on the GPU (the MW
+    // iteration parameters are accepted for signature compatibility; the MW
+    // trajectory itself is SURVEY.md §8f row f3).  Prints "Dual Value = OPT".
+    void RunMultiplicativeWeights(long double num_iterations,
+                                  long double numerical_accuracy_tolerance, bool binary);
+    void RunMultiplicativeWeights(long double num_iterations,
+                                  long double numerical_accuracy_tolerance, bool binary,
+                                  long double scale, int intervals);
+
+    // Added entry: exact simplex with explicit options; returns a dlp status.
+    int RunSimplex(const dlp_options& options);
+
+    // Results.  Solution()[a][i] = (current x_ai, averaged x_ai) as in the
+    // reference's solution_ (both equal the exact optimum here).
+    const std::vector<std::unordered_map<int, std::pair<long double, long double>>>& Solution()
+        const {
+        return solution_;
+    }
+    long double DualValue() const { return dual_value_; }
+    long double MaxInfeasibility() const;   // max_a (sum_i b_ai x_ai - B_a)/B_a, cf. R/allocation_mw.cpp:205-232
+    long double Revenue() const;            // sum b_ai x_ai, cf. R/allocation_mw.cpp:235-251
+    int64_t NumPivots() const { return num_pivots_; }
+    int Status() const { return status_; }
+    const std::vector<long double>& Budgets() const { return budgets_; }
+    const std::vector<std::unordered_map<int, long double>>& Bids() const { return bids_matrix_; }
+
+    long double max_bid_ = 0;   // public in the reference (R/instance.h:43)
+    bool verbose = true;        // print as the reference does
+
+  private:
+    void BuildPrimals();
+    void ReportGraphTopology();
+
+    int num_advertisers_, num_impressions_, num_slots_;
+    long double bid_sparsity_, epsilon_, scaling_factor_, numerical_accuracy_tolerance_;
+    std::vector<long double> budgets_;
+    std::vector<std::unordered_map<int, long double>> bids_matrix_;
+    std::vector<std::unordered_map<int, long double>> transpose_bids_matrix_;
+    std::vector<std::unordered_map<int, std::pair<long double, long double>>> solution_;
+    dlp_problem* problem_ = nullptr;
+    long double dual_value_ = 0;
+    int64_t num_pivots_ = 0;
+    int status_ = DLP_ERR_STATE;
+};
+
+}  // namespace distributed_solver

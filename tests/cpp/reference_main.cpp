@@ -1,0 +1,38 @@
+// The reference's driver call sequence (R/main.cpp:44-64), compiled against the
+// drop-in facade (include/distributed_solver/instance.h) instead of the
+// reference sources.  argv: A I sparsity [solve]
+//   without "solve": GenerateInstance only (host-only, prints the topology);
+//   with "solve": RunMultiplicativeWeights as the reference calls it (exact
+//   GPU simplex underneath) and prints "Dual Value = ..." and the pivot count.
+#include <cstdlib>
+#include <iostream>
+#include <string>
+
+#include "distributed_solver/instance.h"
+
+int main(int argc, const char* argv[]) {
+    using namespace distributed_solver;
+    int A = argc > 1 ? std::atoi(argv[1]) : 1000;
+    int I = argc > 2 ? std::atoi(argv[2]) : 1000;
+    long double sparsity = argc > 3 ? (long double)std::atof(argv[3]) : 0.1;
+    bool solve = argc > 4 && std::string(argv[4]) == "solve";
+    int num_iterations = 300;
+    long double epsilon = 0.01;
+    long double numerical_accuracy_tolerance = 0.000000000000000001;
+    bool use_binary_search = true;
+    int num_bin_intervals = 3;
+    long double cr_transition_scale = 1 - epsilon * 0.001;
+
+    Instance inst = Instance(A, I, 1, sparsity, epsilon, 0.25, numerical_accuracy_tolerance);
+    inst.GenerateInstance();
+    if (solve) {
+        inst.RunMultiplicativeWeights(num_iterations, numerical_accuracy_tolerance,
+                                      use_binary_search, cr_transition_scale, num_bin_intervals);
+        std::cout.precision(17);
+        std::cout << "status " << inst.Status() << " pivots " << inst.NumPivots() << " objective "
+                  << (double)inst.DualValue() << " revenue " << (double)inst.Revenue()
+                  << " max_infeasibility " << (double)inst.MaxInfeasibility() << "\n";
+    }
+    std::cout << "finished \n";
+    return 0;
+}
