@@ -45,6 +45,7 @@ class Options(C.Structure):
         ("nontemporal", C.c_int32),
         ("rows_per_block", C.c_int32),
         ("use_graph", C.c_int32),
+        ("update_variant", C.c_int32),
     ]
 
 
@@ -111,6 +112,9 @@ SIGNATURES = [
     ("dlp_session_status", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(_I64)]),
     ("dlp_session_timings", C.c_int, [_P, _DP, C.POINTER(_I64)]),
     ("dlp_session_reset_timings", C.c_int, [_P]),
+    ("dlp_session_set_tuning", C.c_int, [_P, C.c_int, C.c_int, C.c_int]),
+    ("dlp_session_get_tuning", C.c_int,
+     [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dlp_session_info", C.c_int,
      [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64)]),
     ("dlp_session_tableau", C.c_int, [_P, _DP]),

@@ -73,7 +73,13 @@ struct Geometry {
     int rows_per_block;   // update kernel
 };
 
-hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, hipStream_t s);
+// Update-kernel variants (tuning): 0 U4/2dbl/scalar-colq (default), 1 U8, 2 U4/LDS-colq,
+// 3 U8/LDS, 4 U4/4dbl, 5 U2/4dbl, 6 U4/4dbl/LDS, 7 U16/LDS.  Column tile = update_tile().
+int update_tile(int variant);
+int update_variants();
+constexpr int kMaxBandLdsHost = 256;   // LDS-colq variants need rows_per_block <= this
+hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, int variant,
+                             hipStream_t s);
 hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* basis_out,
                         const PricePart* pp, DevState* st, double* colq, Cand* partials,
                         int nblocks, Cand* cand_out, int nranks, double tol_dj, double tol_piv,
@@ -86,7 +92,7 @@ hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits
                        hipStream_t s);
 hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,
                          const DevState* st, PricePart* pp, double tol_dj, dlp_pivot* log,
-                         int64_t log_cap, bool nontemporal, hipStream_t s);
+                         int64_t log_cap, bool nontemporal, int variant, hipStream_t s);
 // Synthetic tableau rows [row_first, row_first+rows) + objective row, on device.
 hipError_t launch_generate(const Geometry& g, int kind, int64_t m, int64_t n, uint64_t seed,
                            hipStream_t s);

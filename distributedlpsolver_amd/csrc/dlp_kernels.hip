@@ -154,16 +154,18 @@ __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* ba
 // a1 at start-up: pricing partials of the initial objective row, one per
 // 512-column tile (the same tiling the update kernel's fused epilogue uses).
 __global__ __launch_bounds__(kUpdThreads) void price_init_kernel(const double* __restrict__ zrow,
-                                                                 int64_t ncols, PricePart* pp,
-                                                                 double tol_dj) {
+                                                                 int64_t ncols, int tile,
+                                                                 PricePart* pp, double tol_dj) {
     __shared__ PricePart lds[4];
-    const int64_t j = (int64_t)blockIdx.x * kUpdTile + threadIdx.x * kUpdVec;
     PricePart acc = pp_empty();
-    if (j < ncols) {
-        const double z0 = zrow[j];
-        const double z1 = (j + 1 < ncols) ? zrow[j + 1] : 0.0;
-        price_pair(acc, z0, z1, j, ncols, tol_dj);
-    }
+    const int per_lane = tile / kUpdThreads;   // 2 or 4 columns per lane, ascending
+    const int64_t j = (int64_t)blockIdx.x * tile + (int64_t)threadIdx.x * per_lane;
+    for (int k = 0; k < per_lane; k += 2)
+        if (j + k < ncols) {
+            const double z0 = zrow[j + k];
+            const double z1 = (j + k + 1 < ncols) ? zrow[j + k + 1] : 0.0;
+            price_pair(acc, z0, z1, j + k, ncols, tol_dj);
+        }
     acc = block_price(acc, lds);
     if (threadIdx.x == 0) pp[blockIdx.x] = acc;
 }
@@ -306,34 +308,54 @@ __device__ inline void st2(double* p, d2 v) {
 }
 
 // a3 (second half): the rank-1 elimination, the HBM-bound ~100% of a pivot.
-// Workgroup (tile, band) owns columns [tile*512, +512) of rows
-// [band*rb, +rb): each lane keeps its 2 prow values in registers for the whole
-// band, colq[i] is a wave-uniform scalar load, and U rows are loaded before
-// any is stored so every lane has U x 16 B in flight.  Rows with colq == 0
-// are skipped (no traffic); row p becomes prow.  The band holding the
-// objective row also emits the next pivot's pricing partial for its tile and
-// the objective value into the pivot log.
+// Workgroup (tile, band) owns columns [tile*TILE, +TILE) of rows
+// [band*rb, +rb), TILE = 256 lanes x VEC doubles: each lane keeps its VEC prow
+// values in registers for the whole band; colq[i] is wave-uniform (scalar
+// load, or staged once per band in LDS when LDSQ); U rows are loaded before
+// any is stored so every lane has U x VEC x 8 B in flight.  Rows with
+// colq == 0 are skipped (no traffic); row p becomes prow.  The band holding
+// the objective row also emits the next pivot's pricing partial for its tile
+// and the objective value into the pivot log.
 // Nearest reference analog: the 2x2 basis solve R/global_problem.cpp:393-405.
-template <bool NT, int U>
+constexpr int kMaxBandLds = 256;
+
+template <int VEC>
+__device__ inline void price_lane(PricePart& acc, const d2* z, int64_t j, int64_t ncols,
+                                  double tol_dj) {
+#pragma unroll
+    for (int v = 0; v < VEC / 2; ++v) price_pair(acc, z[v].x, z[v].y, j + 2 * v, ncols, tol_dj);
+}
+
+template <bool NT, int U, int VEC, bool LDSQ>
 __global__ __launch_bounds__(kUpdThreads) void update_kernel(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
     const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
     PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
+    constexpr int TILE = kUpdThreads * VEC;
+    constexpr int NV = VEC / 2;
     __shared__ PricePart lds_pp[4];
+    __shared__ double lds_q[LDSQ ? kMaxBandLds + 16 : 1];
     if (st->status != DLP_RUNNING) return;
     const int tile = blockIdx.x;
-    const int64_t j = (int64_t)tile * kUpdTile + threadIdx.x * kUpdVec;
-    const bool colok = j < ld;
+    const int64_t j = (int64_t)tile * TILE + threadIdx.x * VEC;
+    const bool colok = j < ld;   // ld % 16 == 0 and j % VEC == 0: the whole vector is in range
     // Lanes past ld (last, partial tile only) read a valid in-row address and
     // never store, so every load below is issued without a branch.
-    const int64_t jc = colok ? j : ld - kUpdVec;
-    const d2 pr = *(const d2*)(prow + jc);
+    const int64_t jc = colok ? j : ld - VEC;
+    d2 pr[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) pr[v] = *(const d2*)(prow + jc + 2 * v);
     const int64_t pl = st->p_local;
     const int64_t i0 = (int64_t)blockIdx.y * rb;
     const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;   // constraint rows only
+    if constexpr (LDSQ) {
+        for (int k = threadIdx.x; k < rb + U; k += blockDim.x)
+            lds_q[k] = (i0 + k <= rows) ? colq[i0 + k] : 0.0;
+        __syncthreads();
+    }
 
     for (int64_t i = i0; i < iend; i += U) {
-        d2 t[U];
+        d2 t[U][NV];
         double f[U];
         // All U loads in flight before the first use; a row that needs no
         // load (out of band, colq == 0, or the pivot row) reads the L2-hot
@@ -341,20 +363,27 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t ii = i + u;
-            f[u] = colq[ii];   // colq is padded by kColqPad: always a valid read
+            if constexpr (LDSQ)
+                f[u] = lds_q[ii - i0];
+            else
+                f[u] = colq[ii];   // colq is padded by kColqPad: always a valid read
             const bool need = (ii < iend) && (ii != pl) && (f[u] != 0.0);
             const double* src = need ? (T + ii * ld + jc) : (prow + jc);
-            t[u] = ld2<NT>(src);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) t[u][v] = ld2<NT>(src + 2 * v);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t ii = i + u;
             if ((ii < iend) && (ii == pl || f[u] != 0.0)) {   // wave-uniform
-                d2 o;
-                o.x = __builtin_fma(-f[u], pr.x, t[u].x);
-                o.y = __builtin_fma(-f[u], pr.y, t[u].y);
-                if (ii == pl) o = pr;
-                if (colok) st2<NT>(T + ii * ld + j, o);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    d2 o;
+                    o.x = __builtin_fma(-f[u], pr[v].x, t[u][v].x);
+                    o.y = __builtin_fma(-f[u], pr[v].y, t[u][v].y);
+                    if (ii == pl) o = pr[v];
+                    if (colok) st2<NT>(T + ii * ld + j + 2 * v, o);
+                }
             }
         }
     }
@@ -362,19 +391,24 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(
     if (i0 + rb > rows) {   // this band holds the objective row (local index `rows`)
         const double f = colq[rows];
         double* zp = T + rows * ld + jc;
-        d2 z = *(const d2*)zp;
-        if (f != 0.0 && colok) {
-            z.x = __builtin_fma(-f, pr.x, z.x);
-            z.y = __builtin_fma(-f, pr.y, z.y);
-            *(d2*)zp = z;
+        d2 z[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            z[v] = *(const d2*)(zp + 2 * v);
+            if (f != 0.0 && colok) {
+                z[v].x = __builtin_fma(-f, pr[v].x, z[v].x);
+                z[v].y = __builtin_fma(-f, pr[v].y, z[v].y);
+                *(d2*)(zp + 2 * v) = z[v];
+            }
         }
         PricePart acc = pp_empty();
-        if (colok) price_pair(acc, z.x, z.y, j, ncols, tol_dj);
+        if (colok) price_lane<VEC>(acc, z, j, ncols, tol_dj);
         acc = block_price(acc, lds_pp);
         if (threadIdx.x == 0) pp[tile] = acc;
-        if (log && colok && j <= ncols && ncols < j + 2) {
+        if (log && colok && j <= ncols && ncols < j + VEC) {
             const int64_t k = st->npivots - 1;
-            if (k >= 0 && k < log_cap) log[k].objective = (ncols == j) ? z.x : z.y;
+            const int64_t o = ncols - j;
+            if (k >= 0 && k < log_cap) log[k].objective = (o & 1) ? z[o >> 1].y : z[o >> 1].x;
         }
     }
 }
@@ -448,9 +482,15 @@ int ratio_blocks(const Geometry& g) {
     return (int)((g.rows + 1 + kRatioThreads - 1) / kRatioThreads);
 }
 
-hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, hipStream_t s) {
+int update_tile(int variant) { return kUpdThreads * ((variant >= 4 && variant <= 6) ? 4 : 2); }
+int update_variants() { return 8; }
+
+hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, int variant,
+                             hipStream_t s) {
     const double* z = g.T + g.rows * g.ld;
-    price_init_kernel<<<g.ntiles, kUpdThreads, 0, s>>>(z, g.ncols, pp, tol_dj);
+    const int tile = update_tile(variant);
+    const int ntiles = (int)((g.ld + tile - 1) / tile);
+    price_init_kernel<<<ntiles, kUpdThreads, 0, s>>>(z, g.ncols, tile, pp, tol_dj);
     return hipGetLastError();
 }
 
@@ -482,19 +522,41 @@ hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits
     return hipGetLastError();
 }
 
+template <bool NT, int U, int VEC, bool LDSQ>
+static void upd(const Geometry& g, const double* colq, const double* prow, const DevState* st,
+                PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+    constexpr int TILE = kUpdThreads * VEC;
+    const int ntiles = (int)((g.ld + TILE - 1) / TILE);
+    const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
+    dim3 grid(ntiles, (unsigned)bands);
+    update_kernel<NT, U, VEC, LDSQ><<<grid, kUpdThreads, 0, s>>>(
+        g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
+}
+
+template <bool NT>
+static void upd_variant(int variant, const Geometry& g, const double* colq, const double* prow,
+                        const DevState* st, PricePart* pp, double tol_dj, dlp_pivot* log,
+                        int64_t log_cap, hipStream_t s) {
+    switch (variant) {
+        default:
+        case 0: upd<NT, 4, 2, false>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 1: upd<NT, 8, 2, false>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 2: upd<NT, 4, 2, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 3: upd<NT, 8, 2, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 4: upd<NT, 4, 4, false>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 5: upd<NT, 2, 4, false>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 6: upd<NT, 4, 4, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 7: upd<NT, 16, 2, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+    }
+}
+
 hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,
                          const DevState* st, PricePart* pp, double tol_dj, dlp_pivot* log,
-                         int64_t log_cap, bool nontemporal, hipStream_t s) {
-    const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
-    dim3 grid(g.ntiles, (unsigned)bands);
+                         int64_t log_cap, bool nontemporal, int variant, hipStream_t s) {
     if (nontemporal)
-        update_kernel<true, 4><<<grid, kUpdThreads, 0, s>>>(g.T, g.ld, g.rows, g.ncols, colq,
-                                                            prow, st, pp, g.rows_per_block,
-                                                            tol_dj, log, log_cap);
+        upd_variant<true>(variant, g, colq, prow, st, pp, tol_dj, log, log_cap, s);
     else
-        update_kernel<false, 4><<<grid, kUpdThreads, 0, s>>>(g.T, g.ld, g.rows, g.ncols, colq,
-                                                             prow, st, pp, g.rows_per_block,
-                                                             tol_dj, log, log_cap);
+        upd_variant<false>(variant, g, colq, prow, st, pp, tol_dj, log, log_cap, s);
     return hipGetLastError();
 }
 

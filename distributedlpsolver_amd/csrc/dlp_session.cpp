@@ -197,9 +197,15 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     g.rows = s->rows;
     g.row_first = s->row_first;
     g.ncols = s->N;
-    g.ntiles = (int)((s->ld + dlp::kUpdTile - 1) / dlp::kUpdTile);
+    if (opt->update_variant < 0 || opt->update_variant >= dlp::update_variants()) {
+        set_error("update_variant out of range");
+        return DLP_ERR_ARG;
+    }
+    const int tile = dlp::update_tile(opt->update_variant);
+    g.ntiles = (int)((s->ld + tile - 1) / tile);
     g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block
                                                : auto_rows_per_block(rows_total, g.ntiles);
+    g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
     const size_t tbytes = (size_t)rows_total * s->ld * sizeof(double);
     if (hipMalloc(&s->T, tbytes) != hipSuccess) {
         set_error("hipMalloc of the tableau failed (" + std::to_string(tbytes) + " bytes)");
@@ -218,7 +224,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     HIP_TRY(hipMalloc(&s->partials, sizeof(dlp::Cand) * s->ratio_blocks));
     HIP_TRY(hipMalloc(&s->cand_send, sizeof(dlp::Cand)));
     HIP_TRY(hipMalloc(&s->cand_recv, sizeof(dlp::Cand) * nranks));
-    HIP_TRY(hipMalloc(&s->pp, sizeof(dlp::PricePart) * g.ntiles));
+    HIP_TRY(hipMalloc(&s->pp, sizeof(dlp::PricePart) * ((s->ld + 511) / 512)));
     HIP_TRY(hipMalloc(&s->basis, sizeof(int32_t) * s->m));
     HIP_TRY(hipMalloc(&s->st, sizeof(dlp::DevState)));
     s->log_cap = opt->log_pivots ? std::max<int64_t>(1, opt->max_pivots) : 0;
@@ -248,7 +254,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     st0.bland = opt->pricing == DLP_PRICING_BLAND ? 1 : 0;
     *s->host_st = st0;
     HIP_TRY(hipMemcpyAsync(s->st, s->host_st, sizeof(st0), hipMemcpyHostToDevice, s->stream));
-    HIP_TRY(dlp::launch_price_init(g, s->pp, opt->tol_dj, s->stream));
+    HIP_TRY(dlp::launch_price_init(g, s->pp, opt->tol_dj, opt->update_variant, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
 
     if (uid) {
@@ -288,7 +294,8 @@ int enqueue_prow(dlp_session* s) {
 int enqueue_update(dlp_session* s) {
     const dlp_options& o = s->opt;
     HIP_TRY(dlp::launch_update(s->g, s->colq, (const double*)s->prow_recv, s->st, s->pp, o.tol_dj,
-                               s->log, s->log_cap, o.nontemporal != 0, s->stream));
+                               s->log, s->log_cap, o.nontemporal != 0, o.update_variant,
+                               s->stream));
     return DLP_OK;
 }
 
@@ -419,6 +426,7 @@ void dlp_options_default(dlp_options* o) {
     o->nontemporal = 1;
     o->rows_per_block = 0;
     o->use_graph = 1;
+    o->update_variant = 0;
 }
 
 const char* dlp_status_string(int st) {
@@ -713,6 +721,36 @@ int dlp_session_timings(dlp_session* s, double* ms_out, int64_t* nsamples) {
     if (!s || !ms_out) return DLP_ERR_ARG;
     for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) ms_out[ph] = s->timings[ph];
     if (nsamples) *nsamples = s->nsamples;
+    return DLP_OK;
+}
+
+int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_block,
+                           int nontemporal) {
+    if (!s || update_variant < 0 || update_variant >= dlp::update_variants() || rows_per_block < 0)
+        return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->opt.update_variant = update_variant;
+    s->opt.nontemporal = nontemporal;
+    const int tile = dlp::update_tile(update_variant);
+    s->g.ntiles = (int)((s->ld + tile - 1) / tile);
+    s->g.rows_per_block = rows_per_block > 0 ? rows_per_block
+                                             : auto_rows_per_block(s->rows + 1, s->g.ntiles);
+    s->g.rows_per_block = std::min(s->g.rows_per_block, dlp::kMaxBandLdsHost);
+    if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
+    if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
+    // pricing partials depend only on the current objective row: rebuild at the new tiling
+    HIP_TRY(dlp::launch_price_init(s->g, s->pp, s->opt.tol_dj, update_variant, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return DLP_OK;
+}
+
+int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_block,
+                           int* nontemporal) {
+    if (!s) return DLP_ERR_ARG;
+    if (update_variant) *update_variant = s->opt.update_variant;
+    if (rows_per_block) *rows_per_block = s->g.rows_per_block;
+    if (nontemporal) *nontemporal = s->opt.nontemporal;
     return DLP_OK;
 }
 

@@ -217,6 +217,16 @@ class Session:
         L.check(L.lib().dlp_session_timings(self._h, _dptr(tm), C.byref(ns)), "dlp_session_timings")
         return tm, ns.value
 
+    def set_tuning(self, update_variant: int, rows_per_block: int = 0, nontemporal: int = 1):
+        L.check(L.lib().dlp_session_set_tuning(self._h, update_variant, rows_per_block, nontemporal),
+                "dlp_session_set_tuning")
+
+    def get_tuning(self) -> tuple[int, int, int]:
+        v, rb, nt = C.c_int(), C.c_int(), C.c_int()
+        L.check(L.lib().dlp_session_get_tuning(self._h, C.byref(v), C.byref(rb), C.byref(nt)),
+                "dlp_session_get_tuning")
+        return v.value, rb.value, nt.value
+
     def reset_timings(self):
         L.check(L.lib().dlp_session_reset_timings(self._h), "dlp_session_reset_timings")
 

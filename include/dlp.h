@@ -78,7 +78,7 @@ extern "C" {
 
 /* Synthetic instance families. */
 #define DLP_GEN_DENSE       0   /* A,x0,c ~ U[0,1); b = A x0 + U[0,1)          */
-#define DLP_GEN_DEGENERATE  1   /* as DENSE, b_i = 0 on ~50% of the rows       */
+#define DLP_GEN_DEGENERATE  1   /* ~50% "cone" rows: A in [-1,1), b_i = 0      */
 
 /* Exchange buffers of a rank session (dlp_session_buffer). */
 #define DLP_BUF_CAND_SEND   0   /* 1 x dlp_candidate, device                   */
@@ -129,6 +129,7 @@ typedef struct dlp_options {
     int32_t nontemporal;     /* update kernel uses nt loads/stores (default 1) */
     int32_t rows_per_block;  /* update-kernel rows per workgroup (0 = auto) */
     int32_t use_graph;       /* replay each poll window as a hipGraph (default 1) */
+    int32_t update_variant;  /* rank-1 kernel variant (tuning; default 0), see dlp_session_set_tuning */
 } dlp_options;
 
 /* ---- library ---------------------------------------------------------- */
@@ -192,6 +193,11 @@ int dlp_session_sync(dlp_session* s);
 int dlp_session_status(dlp_session* s, int* status, int64_t* npivots);
 int dlp_session_timings(dlp_session* s, double* ms_out /* DLP_NUM_PHASES */, int64_t* nsamples);
 int dlp_session_reset_timings(dlp_session* s);
+/* Retune the rank-1 update between pivots (results are bit-identical for every
+ * setting): variant 0..7 (rows in flight x doubles per lane x colq staging),
+ * rows per workgroup band (0 = auto, <= 256), non-temporal loads/stores. */
+int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_block, int nontemporal);
+int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_block, int* nontemporal);
 int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,
                      int64_t* ncols);
 /* Copy the local tableau (rows_local+1 rows x ld, objective last) to the host. */

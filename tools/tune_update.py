@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of rank-1 update variants on one HBM-resident tableau.
+
+    python tools/tune_update.py [--workload c3|c2] [--rounds 3] [--pivots 10]
+
+Every (variant, rows_per_block, nontemporal) config runs `pivots` real pivots
+per round, configs shuffled per round, all in ONE process on ONE device
+(cdna_hip_programming.md §5.4 rule 24).  Reports median/min update-kernel ms
+(HIP events) and GB/s of algorithmic bytes 16 (m_local+1)(N+1)."""
+import argparse
+import json
+import os
+import random
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import distributedlpsolver_amd as dlp  # noqa: E402
+
+W = {"c3": (32768, 32768, 3), "c2": (4096, 4096, 2)}
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="c3", choices=sorted(W))
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--pivots", type=int, default=10)
+ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
+ap.add_argument("--rbs", default="0,16,64,256")
+ap.add_argument("--nts", default="1,0")
+ap.add_argument("--out", default=None)
+a = ap.parse_args()
+m, n, seed = W[a.workload]
+s = dlp.Session(dlp.Problem.random(m, n, seed), timing=1, check_interval=max(a.pivots, 1),
+                max_pivots=10 ** 7, log_pivots=0)
+s.run(3)
+cfgs = [(v, rb, nt) for v in map(int, a.variants.split(",")) for rb in map(int, a.rbs.split(","))
+        for nt in map(int, a.nts.split(","))]
+res = {c: [] for c in cfgs}
+bytes_launch = 16.0 * (s.rows + 1) * (s.ncols + 1)
+rng = random.Random(0)
+for r in range(a.rounds):
+    order = cfgs[:]
+    rng.shuffle(order)
+    for c in order:
+        s.set_tuning(*c)
+        s.run(1)            # first launch after a retune is not timed
+        s.reset_timings()
+        st, done = s.run(a.pivots)
+        tm, ns = s.timings()
+        res[c].append(tm[3] / max(ns, 1))
+    print(f"round {r} done", flush=True)
+rows = []
+for c, v in res.items():
+    med, mn = statistics.median(v), min(v)
+    rows.append(dict(variant=c[0], rows_per_block=c[1], nontemporal=c[2], median_ms=med, min_ms=mn,
+                     median_gbs=bytes_launch / med / 1e6, best_gbs=bytes_launch / mn / 1e6))
+rows.sort(key=lambda d: d["median_ms"])
+for d in rows:
+    print(f"v{d['variant']} rb={d['rows_per_block']:4d} nt={d['nontemporal']}  "
+          f"median {d['median_ms']:.4f} ms  {d['median_gbs']:.0f} GB/s  (best {d['best_gbs']:.0f})")
+if a.out:
+    json.dump(dict(workload=a.workload, m=m, n=n, bytes_per_launch=bytes_launch, rounds=a.rounds,
+                   pivots=a.pivots, results=rows), open(a.out, "w"), indent=1)
