@@ -44,10 +44,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-pivots", type=int, default=3)
+    ap.add_argument("--cpu-pivots", type=int, default=60)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--rows-per-block", type=int, default=0)
-    ap.add_argument("--nontemporal", type=int, default=1)
+    ap.add_argument("--nontemporal", type=int, default=-1, help="-1 = auto")
+    ap.add_argument("--variant", type=int, default=-1, help="update-kernel variant, -1 = auto")
+    ap.add_argument("--ld-align", type=int, default=0, help="row alignment (doubles), 0 = auto")
     ap.add_argument("--timing", type=int, default=2)
     ap.add_argument("--pmc-dir", default=None,
                     help="rocprofv3 --pmc output dir (FETCH_SIZE / WRITE_SIZE) to fill roofline.traffic")
@@ -74,6 +76,18 @@ def pmc_traffic(pmc_dir: str, kernel_substr: str = "update_kernel"):
     if not fetch or not write:
         return None
     return (2.0 * sum(fetch) / len(fetch) + sum(write) / len(write)) * 1024.0
+
+
+def committed_traffic(workload: str):
+    """Latest committed PMC summary for this workload (profiles/*/<workload>_update_pmc_traffic.json),
+    produced by tools/gpu_profile.sh on the same kernel; None when absent."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{workload}_update_pmc_traffic.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_launch"), os.path.relpath(paths[-1], ROOT)
 
 
 def cpu_baseline(m, n, seed, k, threads):
@@ -118,6 +132,7 @@ def main():
     sess = dlp.Session(dlp.Problem.random(m, n, seed), rank=rank, nranks=world, rccl_id=rccl_id,
                        device=local, check_interval=max(args.steps, args.warmup, 1),
                        timing=args.timing, nontemporal=args.nontemporal,
+                       update_variant=args.variant, ld_align=args.ld_align,
                        rows_per_block=args.rows_per_block, max_pivots=args.warmup + args.steps + 1,
                        log_pivots=1)
     st, done = sess.run(args.warmup)
@@ -134,6 +149,8 @@ def main():
         raise SystemExit(f"timed window ended early: status {st} after {done} pivots")
 
     tm, nsamp = sess.timings()
+    variant, rb_used, nt_used = sess.get_tuning()
+    ld_used = sess.ld
     rows_local, N1 = sess.rows, sess.ncols + 1
     upd_ms = tm[3] / max(nsamp, 1)
     bytes_launch = 16.0 * (rows_local + 1) * N1
@@ -148,7 +165,10 @@ def main():
     sess.close()
 
     if rank == 0:
-        traffic = pmc_traffic(args.pmc_dir) if args.pmc_dir else None
+        if args.pmc_dir:
+            traffic, traffic_src = pmc_traffic(args.pmc_dir), f"live: {args.pmc_dir}"
+        else:
+            traffic, traffic_src = committed_traffic(args.workload) if world == 1 else (None, None)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(m, n, seed, args.cpu_pivots, args.cpu_threads)
@@ -166,7 +186,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (device-generated splitmix64 dense LP, seed = config id)",
-            "config": {"workload": desc, "m": m, "n": n, "N": m + n, "ld": dlp.tableau_ld(m, n), "seed": seed, "rows_per_rank": rows_local,
+            "config": {"workload": desc, "m": m, "n": n, "N": m + n, "ld": ld_used, "seed": seed, "rows_per_rank": rows_local,
                        "parallelism": f"rowblock{world}", "pricing": "dantzig->bland on degeneracy"},
             "achieved_hbm_gbs": achieved,
             "phases_ms_per_pivot": {"ratio": tm[0] / max(nsamp, 1), "exchange": tm[1] / max(nsamp, 1),
@@ -174,8 +194,10 @@ def main():
             "objective_after_window": res.objective,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch,
-                         "kernel": "update_kernel<nt=1,U=4>", "launch_ms": upd_ms},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "kernel": f"rank-1 update variant {variant} (rows/band {rb_used}, "
+                                   f"nt {nt_used}, ld {ld_used})", "launch_ms": upd_ms},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

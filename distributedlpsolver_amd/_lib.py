@@ -46,6 +46,7 @@ class Options(C.Structure):
         ("rows_per_block", C.c_int32),
         ("use_graph", C.c_int32),
         ("update_variant", C.c_int32),
+        ("ld_align", C.c_int32),
     ]
 
 
@@ -87,6 +88,7 @@ SIGNATURES = [
     ("dlp_rank_rows", C.c_int, [_I64, C.c_int, C.c_int, C.POINTER(_I64), C.POINTER(_I64)]),
     ("dlp_candidate_select", C.c_int, [C.POINTER(Candidate), C.c_int, C.POINTER(C.c_int)]),
     ("dlp_tableau_ld", _I64, [_I64, _I64]),
+    ("dlp_update_variants", C.c_int, []),
     ("dlp_problem_create_dense", C.c_int, [_I64, _I64, _DP, _DP, _DP, C.POINTER(_P)]),
     ("dlp_problem_create_random", C.c_int, [C.c_int, _I64, _I64, C.c_uint64, C.POINTER(_P)]),
     ("dlp_problem_create_adalloc", C.c_int,

@@ -65,7 +65,8 @@ __host__ __device__ inline bool cand_better(const Cand& a, const Cand& b) {
 // Launchers (dlp_kernels.hip).  All asynchronous on `stream`.
 struct Geometry {
     double* T;            // (rows+1) x ld, objective row last
-    int64_t ld;
+    int64_t ld;           // row stride (>= width, multiple of ld_align)
+    int64_t width;        // round16(N+1): columns the kernels touch
     int64_t rows;         // local constraint rows
     int64_t row_first;    // global index of local row 0
     int64_t ncols;        // N = n + m (pricing columns; RHS column index)

@@ -338,10 +338,11 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(
     if (st->status != DLP_RUNNING) return;
     const int tile = blockIdx.x;
     const int64_t j = (int64_t)tile * TILE + threadIdx.x * VEC;
-    const bool colok = j < ld;   // ld % 16 == 0 and j % VEC == 0: the whole vector is in range
+    const int64_t width = (ncols + 16) & ~(int64_t)15;   // round16(N+1) <= ld: real columns
+    const bool colok = j < width;   // ld % 16 == 0 and j % VEC == 0: the whole vector is in range
     // Lanes past ld (last, partial tile only) read a valid in-row address and
     // never store, so every load below is issued without a branch.
-    const int64_t jc = colok ? j : ld - VEC;
+    const int64_t jc = colok ? j : width - VEC;
     d2 pr[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) pr[v] = *(const d2*)(prow + jc + 2 * v);
@@ -389,6 +390,252 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(
     }
 
     if (i0 + rb > rows) {   // this band holds the objective row (local index `rows`)
+        const double f = colq[rows];
+        double* zp = T + rows * ld + jc;
+        d2 z[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            z[v] = *(const d2*)(zp + 2 * v);
+            if (f != 0.0 && colok) {
+                z[v].x = __builtin_fma(-f, pr[v].x, z[v].x);
+                z[v].y = __builtin_fma(-f, pr[v].y, z[v].y);
+                *(d2*)(zp + 2 * v) = z[v];
+            }
+        }
+        PricePart acc = pp_empty();
+        if (colok) price_lane<VEC>(acc, z, j, ncols, tol_dj);
+        acc = block_price(acc, lds_pp);
+        if (threadIdx.x == 0) pp[tile] = acc;
+        if (log && colok && j <= ncols && ncols < j + VEC) {
+            const int64_t k = st->npivots - 1;
+            const int64_t o = ncols - j;
+            if (k >= 0 && k < log_cap) log[k].objective = (o & 1) ? z[o >> 1].y : z[o >> 1].x;
+        }
+    }
+}
+
+// Dense fast path of the same elimination.  The band's colq values are staged
+// in LDS once; when no row of the band has colq == 0 and the pivot row is not
+// in it (the common case on dense tableaus) every group of U rows is issued as
+// U unconditional 16-B loads per lane from one uniform row pointer, then U
+// fma pairs and U stores, with no per-row uniform state in scalar registers.
+// Otherwise the band takes the general per-row path.  Results are identical
+// to update_kernel (same fma per element, same skipped rows).
+template <bool NT, int U, int THREADS>
+__global__ __launch_bounds__(THREADS) void update_fast_kernel(
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+    const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
+    PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
+    constexpr int TILE = THREADS * 2;
+    __shared__ PricePart lds_pp[THREADS / 64];
+    __shared__ double lds_q[kMaxBandLds + 16];
+    if (st->status != DLP_RUNNING) return;
+    const int tile = blockIdx.x;
+    const int64_t j = (int64_t)tile * TILE + threadIdx.x * 2;
+    const int64_t width = (ncols + 16) & ~(int64_t)15;   // round16(N+1) <= ld: real columns
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 2;
+    const d2 pr = *(const d2*)(prow + jc);
+    const int64_t pl = st->p_local;
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    int sparse = 0;
+    for (int k = threadIdx.x; k < rb + U; k += THREADS) {
+        const double f = (i0 + k <= rows) ? colq[i0 + k] : 0.0;
+        lds_q[k] = f;
+        if (i0 + k < iend && f == 0.0) sparse = 1;
+    }
+    sparse = __syncthreads_or(sparse) || (pl >= i0 && pl < iend);
+
+    int64_t i = i0;
+    if (!sparse) {
+        for (; i + U <= iend; i += U) {
+            double* rp = T + i * ld + jc;
+            d2 t[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) t[u] = ld2<NT>(rp + u * ld);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double f = lds_q[i - i0 + u];
+                d2 o;
+                o.x = __builtin_fma(-f, pr.x, t[u].x);
+                o.y = __builtin_fma(-f, pr.y, t[u].y);
+                if (colok) st2<NT>(rp + u * ld, o);
+            }
+        }
+    }
+    for (; i < iend; ++i) {   // general path: remainder rows, or a sparse / pivot band
+        const double f = lds_q[i - i0];
+        if (i == pl) {
+            if (colok) st2<NT>(T + i * ld + j, pr);
+        } else if (f != 0.0) {
+            const d2 t = ld2<NT>(T + i * ld + jc);
+            d2 o;
+            o.x = __builtin_fma(-f, pr.x, t.x);
+            o.y = __builtin_fma(-f, pr.y, t.y);
+            if (colok) st2<NT>(T + i * ld + j, o);
+        }
+    }
+
+    if (i0 + rb > rows) {   // objective row: update + next pivot's pricing partial + log
+        const double f = colq[rows];
+        double* zp = T + rows * ld + jc;
+        d2 z = *(const d2*)zp;
+        if (f != 0.0 && colok) {
+            z.x = __builtin_fma(-f, pr.x, z.x);
+            z.y = __builtin_fma(-f, pr.y, z.y);
+            *(d2*)zp = z;
+        }
+        PricePart acc = pp_empty();
+        if (colok) price_pair(acc, z.x, z.y, j, ncols, tol_dj);
+        acc = block_price(acc, lds_pp);
+        if (threadIdx.x == 0) pp[tile] = acc;
+        if (log && colok && j <= ncols && ncols < j + 2) {
+            const int64_t k = st->npivots - 1;
+            if (k >= 0 && k < log_cap) log[k].objective = (ncols == j) ? z.x : z.y;
+        }
+    }
+}
+
+// Row-serial form: every lane handles one row at a time (load -> fma -> store),
+// so each wave has at most one 16-B load and one store in flight.  The number
+// of resident workgroups per CU (and with it the requests in flight per CU)
+// is capped by the launcher through a dynamic-LDS reservation: on this
+// streaming pattern fewer outstanding requests per CU measured FASTER
+// (tuning log).  Same arithmetic and skip rules as update_kernel.
+template <bool NT, int VEC>
+__global__ __launch_bounds__(kUpdThreads) void update_serial_kernel(
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+    const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
+    PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
+    constexpr int TILE = kUpdThreads * VEC;
+    constexpr int NV = VEC / 2;
+    __shared__ PricePart lds_pp[4];
+    __shared__ double lds_q[kMaxBandLds + 16];
+    if (st->status != DLP_RUNNING) return;
+    const int tile = blockIdx.x;
+    const int64_t j = (int64_t)tile * TILE + threadIdx.x * VEC;
+    const int64_t width = (ncols + 16) & ~(int64_t)15;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - VEC;
+    d2 pr[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) pr[v] = *(const d2*)(prow + jc + 2 * v);
+    const int64_t pl = st->p_local;
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    for (int k = threadIdx.x; k < rb; k += kUpdThreads)
+        lds_q[k] = (i0 + k <= rows) ? colq[i0 + k] : 0.0;
+    __syncthreads();
+    for (int64_t i = i0; i < iend; ++i) {
+        const double f = lds_q[i - i0];
+        if (i == pl) {
+            if (colok)
+#pragma unroll
+                for (int v = 0; v < NV; ++v) st2<NT>(T + i * ld + j + 2 * v, pr[v]);
+        } else if (f != 0.0) {
+            d2 t[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) t[v] = ld2<NT>(T + i * ld + jc + 2 * v);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                d2 o;
+                o.x = __builtin_fma(-f, pr[v].x, t[v].x);
+                o.y = __builtin_fma(-f, pr[v].y, t[v].y);
+                if (colok) st2<NT>(T + i * ld + j + 2 * v, o);
+            }
+        }
+    }
+
+    if (i0 + rb > rows) {   // objective row: update + next pivot's pricing partial + log
+        const double f = colq[rows];
+        double* zp = T + rows * ld + jc;
+        d2 z[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            z[v] = *(const d2*)(zp + 2 * v);
+            if (f != 0.0 && colok) {
+                z[v].x = __builtin_fma(-f, pr[v].x, z[v].x);
+                z[v].y = __builtin_fma(-f, pr[v].y, z[v].y);
+                *(d2*)(zp + 2 * v) = z[v];
+            }
+        }
+        PricePart acc = pp_empty();
+        if (colok) price_lane<VEC>(acc, z, j, ncols, tol_dj);
+        acc = block_price(acc, lds_pp);
+        if (threadIdx.x == 0) pp[tile] = acc;
+        if (log && colok && j <= ncols && ncols < j + VEC) {
+            const int64_t k = st->npivots - 1;
+            const int64_t o = ncols - j;
+            if (k >= 0 && k < log_cap) log[k].objective = (o & 1) ? z[o >> 1].y : z[o >> 1].x;
+        }
+    }
+}
+
+// Software-pipelined streaming form: each lane keeps DEPTH rows in flight
+// and, in steady state, retires one row (fma + store) per new load, so reads
+// and writes interleave at row granularity instead of in bursts of U.  Same
+// arithmetic and skip rules as update_kernel.
+template <bool NT, int DEPTH, int VEC>
+__global__ __launch_bounds__(kUpdThreads) void update_stream_kernel(
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+    const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
+    PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
+    constexpr int TILE = kUpdThreads * VEC;
+    constexpr int NV = VEC / 2;
+    __shared__ PricePart lds_pp[4];
+    __shared__ double lds_q[kMaxBandLds + 16];
+    if (st->status != DLP_RUNNING) return;
+    const int tile = blockIdx.x;
+    const int64_t j = (int64_t)tile * TILE + threadIdx.x * VEC;
+    const int64_t width = (ncols + 16) & ~(int64_t)15;   // round16(N+1) <= ld: real columns
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - VEC;
+    d2 pr[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) pr[v] = *(const d2*)(prow + jc + 2 * v);
+    const int64_t pl = st->p_local;
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    for (int k = threadIdx.x; k < rb + DEPTH; k += kUpdThreads)
+        lds_q[k] = (i0 + k <= rows) ? colq[i0 + k] : 0.0;
+    __syncthreads();
+
+    auto src_of = [&](int64_t ii) -> const double* {
+        const bool need = (ii < iend) && (ii != pl) && (lds_q[ii - i0] != 0.0);
+        return need ? (T + ii * ld + jc) : (prow + jc);
+    };
+    d2 t[DEPTH][NV];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+        const double* sp = src_of(i0 + d);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) t[d][v] = ld2<NT>(sp + 2 * v);
+    }
+    for (int64_t i = i0; i < iend; i += DEPTH) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const int64_t ii = i + d;
+            const double f = lds_q[ii - i0];
+            d2 o[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                o[v].x = __builtin_fma(-f, pr[v].x, t[d][v].x);
+                o[v].y = __builtin_fma(-f, pr[v].y, t[d][v].y);
+                if (ii == pl) o[v] = pr[v];
+            }
+            // refill this slot with row ii + DEPTH before storing row ii
+            const double* sp = src_of(ii + DEPTH);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) t[d][v] = ld2<NT>(sp + 2 * v);
+            if ((ii < iend) && (ii == pl || f != 0.0) && colok) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) st2<NT>(T + ii * ld + j + 2 * v, o[v]);
+            }
+        }
+    }
+
+    if (i0 + rb > rows) {   // objective row: update + next pivot's pricing partial + log
         const double f = colq[rows];
         double* zp = T + rows * ld + jc;
         d2 z[NV];
@@ -482,14 +729,19 @@ int ratio_blocks(const Geometry& g) {
     return (int)((g.rows + 1 + kRatioThreads - 1) / kRatioThreads);
 }
 
-int update_tile(int variant) { return kUpdThreads * ((variant >= 4 && variant <= 6) ? 4 : 2); }
-int update_variants() { return 8; }
+int update_tile(int variant) {
+    if (variant == 14) return 512 * 2;
+    const bool v4 = (variant >= 4 && variant <= 6) || variant == 10 || variant == 11 ||
+                    variant == 19 || variant == 20 || variant == 27 || variant == 28;
+    return kUpdThreads * (v4 ? 4 : 2);
+}
+int update_variants() { return 30; }
 
 hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, int variant,
                              hipStream_t s) {
     const double* z = g.T + g.rows * g.ld;
     const int tile = update_tile(variant);
-    const int ntiles = (int)((g.ld + tile - 1) / tile);
+    const int ntiles = (int)((g.width + tile - 1) / tile);
     price_init_kernel<<<ntiles, kUpdThreads, 0, s>>>(z, g.ncols, tile, pp, tol_dj);
     return hipGetLastError();
 }
@@ -526,10 +778,46 @@ template <bool NT, int U, int VEC, bool LDSQ>
 static void upd(const Geometry& g, const double* colq, const double* prow, const DevState* st,
                 PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
     constexpr int TILE = kUpdThreads * VEC;
-    const int ntiles = (int)((g.ld + TILE - 1) / TILE);
+    const int ntiles = (int)((g.width + TILE - 1) / TILE);
     const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
     dim3 grid(ntiles, (unsigned)bands);
     update_kernel<NT, U, VEC, LDSQ><<<grid, kUpdThreads, 0, s>>>(
+        g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
+}
+
+template <bool NT, int U, int THREADS>
+static void updf(const Geometry& g, const double* colq, const double* prow, const DevState* st,
+                 PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+    constexpr int TILE = THREADS * 2;
+    const int ntiles = (int)((g.width + TILE - 1) / TILE);
+    const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
+    dim3 grid(ntiles, (unsigned)bands);
+    update_fast_kernel<NT, U, THREADS><<<grid, THREADS, 0, s>>>(
+        g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
+}
+
+template <bool NT, int DEPTH, int VEC>
+static void upds(const Geometry& g, const double* colq, const double* prow, const DevState* st,
+                 PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+    constexpr int TILE = kUpdThreads * VEC;
+    const int ntiles = (int)((g.width + TILE - 1) / TILE);
+    const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
+    dim3 grid(ntiles, (unsigned)bands);
+    update_stream_kernel<NT, DEPTH, VEC><<<grid, kUpdThreads, 0, s>>>(
+        g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
+}
+
+// OCC = workgroups per CU allowed by a dynamic-LDS reservation (0 = no cap).
+template <bool NT, int VEC, int OCC>
+static void updr(const Geometry& g, const double* colq, const double* prow, const DevState* st,
+                 PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+    constexpr int TILE = kUpdThreads * VEC;
+    const int ntiles = (int)((g.width + TILE - 1) / TILE);
+    const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
+    dim3 grid(ntiles, (unsigned)bands);
+    // static LDS is ~2.2 KB; reserve the rest so that only OCC workgroups fit in 160 KiB
+    const size_t dyn = OCC > 0 ? (size_t)(160 * 1024 / OCC) - 4096 : 0;
+    update_serial_kernel<NT, VEC><<<grid, kUpdThreads, dyn, s>>>(
         g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
 }
 
@@ -547,6 +835,28 @@ static void upd_variant(int variant, const Geometry& g, const double* colq, cons
         case 5: upd<NT, 2, 4, false>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
         case 6: upd<NT, 4, 4, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
         case 7: upd<NT, 16, 2, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 8: upd<NT, 16, 2, false>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 9: upd<NT, 32, 2, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 10: upd<NT, 8, 4, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 11: upd<NT, 16, 4, true>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 12: updf<NT, 16, 256>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 13: updf<NT, 8, 256>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 14: updf<NT, 16, 512>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 15: updf<NT, 32, 256>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 16: upds<NT, 1, 2>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 17: upds<NT, 2, 2>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 18: upds<NT, 4, 2>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 19: upds<NT, 1, 4>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 20: upds<NT, 2, 4>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 21: upds<NT, 8, 2>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 22: updr<NT, 2, 4>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 23: updr<NT, 2, 2>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 24: updr<NT, 2, 3>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 25: updr<NT, 2, 6>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 26: updr<NT, 2, 0>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 27: updr<NT, 4, 4>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 28: updr<NT, 4, 2>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
+        case 29: updr<NT, 2, 5>(g, colq, prow, st, pp, tol_dj, log, log_cap, s); break;
     }
 }
 

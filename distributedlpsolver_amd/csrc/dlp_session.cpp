@@ -54,7 +54,8 @@ using dlp::set_error;
 struct dlp_session {
     dlp_options opt{};
     int device = 0, rank = 0, nranks = 1;
-    int64_t m = 0, n = 0, N = 0, ld = 0, row_first = 0, rows = 0;
+    int64_t m = 0, n = 0, N = 0, ld = 0, width = 0, row_first = 0, rows = 0;
+    bool streaming = false;         // tableau >> Infinity Cache (auto-tuning regime)
     hipStream_t stream = nullptr;
     dlp::Geometry g{};
     double* T = nullptr;
@@ -95,13 +96,7 @@ namespace {
 
 int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
 
-int auto_rows_per_block(int64_t rows_total, int ntiles) {
-    // Aim for ~8 K workgroups (>= 32 per CU of 256) with bands of 4..128 rows.
-    int64_t rb = (rows_total * ntiles + 8191) / 8192;
-    rb = std::max<int64_t>(4, std::min<int64_t>(128, rb));
-    rb = (rb + 3) / 4 * 4;
-    return (int)rb;
-}
+int auto_rows_per_block(const dlp_session* s) { return s->streaming ? 8 : 4; }
 
 // Host build of a tableau slice (dense / ad-allocation problems).
 void host_tableau(const dlp_problem* p, int64_t row_first, int64_t rows, int64_t ld,
@@ -177,8 +172,27 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     s->m = prob->m;
     s->n = prob->n;
     s->N = prob->n + prob->m;
-    s->ld = round16(s->N + 1);
+    s->width = round16(s->N + 1);
     CALL_TRY(dlp_rank_rows(s->m, rank, nranks, &s->row_first, &s->rows));
+    // "auto" tuning (negative / zero option values), from the interleaved A/B
+    // sweeps of tools/tune_update.py on MI355X (update kernel):
+    //  - tableaus far beyond the 256 MiB Infinity Cache stream from HBM: the
+    //    row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt stores;
+    //  - smaller ones stay partly cache-resident: uncapped, 4-row bands,
+    //    default cache policy;
+    //  - rows of >= 4096 doubles are aligned to 4 KiB (whole-tile alignment).
+    const bool streaming = (double)(s->rows + 1) * (double)s->width * 8.0 > (double)(1ll << 30);
+    if (s->opt.ld_align <= 0) s->opt.ld_align = s->width >= 4096 ? 512 : 16;
+    if (s->opt.update_variant < 0) s->opt.update_variant = streaming ? 22 : 26;
+    if (s->opt.nontemporal < 0) s->opt.nontemporal = streaming ? 1 : 0;
+    s->streaming = streaming;
+    const int64_t align = s->opt.ld_align;
+    if (align % 16 != 0) {
+        set_error("ld_align must be a multiple of 16 doubles");
+        return DLP_ERR_ARG;
+    }
+    s->ld = (s->width + align - 1) / align * align;
+    opt = &s->opt;
     s->prob_dims.m = prob->m;
     s->prob_dims.n = prob->n;
 
@@ -194,6 +208,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     const int64_t rows_total = s->rows + 1;
     dlp::Geometry& g = s->g;
     g.ld = s->ld;
+    g.width = s->width;
     g.rows = s->rows;
     g.row_first = s->row_first;
     g.ncols = s->N;
@@ -202,9 +217,8 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         return DLP_ERR_ARG;
     }
     const int tile = dlp::update_tile(opt->update_variant);
-    g.ntiles = (int)((s->ld + tile - 1) / tile);
-    g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block
-                                               : auto_rows_per_block(rows_total, g.ntiles);
+    g.ntiles = (int)((s->width + tile - 1) / tile);
+    g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block : auto_rows_per_block(s);
     g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
     const size_t tbytes = (size_t)rows_total * s->ld * sizeof(double);
     if (hipMalloc(&s->T, tbytes) != hipSuccess) {
@@ -423,10 +437,11 @@ void dlp_options_default(dlp_options* o) {
     o->log_pivots = 1;
     o->check_interval = 64;
     o->timing = 0;
-    o->nontemporal = 1;
+    o->nontemporal = -1;   // auto
     o->rows_per_block = 0;
     o->use_graph = 1;
-    o->update_variant = 0;
+    o->update_variant = -1;   // auto
+    o->ld_align = 0;          // auto
 }
 
 const char* dlp_status_string(int st) {
@@ -483,6 +498,8 @@ int dlp_candidate_select(const dlp_candidate* cands, int n, int* winner) {
 }
 
 int64_t dlp_tableau_ld(int64_t m, int64_t n) { return round16(n + m + 1); }
+
+int dlp_update_variants(void) { return dlp::update_variants(); }
 
 int dlp_problem_create_dense(int64_t m, int64_t n, const double* A, const double* b,
                              const double* c, dlp_problem** out) {
@@ -726,16 +743,16 @@ int dlp_session_timings(dlp_session* s, double* ms_out, int64_t* nsamples) {
 
 int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_block,
                            int nontemporal) {
-    if (!s || update_variant < 0 || update_variant >= dlp::update_variants() || rows_per_block < 0)
-        return DLP_ERR_ARG;
+    if (!s || update_variant >= dlp::update_variants() || rows_per_block < 0) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    if (update_variant < 0) update_variant = s->streaming ? 22 : 26;   // auto, as session_init
+    if (nontemporal < 0) nontemporal = s->streaming ? 1 : 0;
     s->opt.update_variant = update_variant;
     s->opt.nontemporal = nontemporal;
     const int tile = dlp::update_tile(update_variant);
-    s->g.ntiles = (int)((s->ld + tile - 1) / tile);
-    s->g.rows_per_block = rows_per_block > 0 ? rows_per_block
-                                             : auto_rows_per_block(s->rows + 1, s->g.ntiles);
+    s->g.ntiles = (int)((s->width + tile - 1) / tile);
+    s->g.rows_per_block = rows_per_block > 0 ? rows_per_block : auto_rows_per_block(s);
     s->g.rows_per_block = std::min(s->g.rows_per_block, dlp::kMaxBandLdsHost);
     if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
     if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }

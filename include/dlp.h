@@ -126,11 +126,17 @@ typedef struct dlp_options {
     int32_t log_pivots;      /* keep the pivot log (default 1) */
     int32_t check_interval;  /* pivots between host status polls (default 64) */
     int32_t timing;          /* 0 none, 1 update kernel, 2 every phase */
-    int32_t nontemporal;     /* update kernel uses nt loads/stores (default 1) */
-    int32_t rows_per_block;  /* update-kernel rows per workgroup (0 = auto) */
+    int32_t nontemporal;     /* update kernel nt loads/stores: 1/0, -1 = auto (default) */
+    int32_t rows_per_block;  /* update-kernel rows per workgroup band (0 = auto, default) */
     int32_t use_graph;       /* replay each poll window as a hipGraph (default 1) */
-    int32_t update_variant;  /* rank-1 kernel variant (tuning; default 0), see dlp_session_set_tuning */
+    int32_t update_variant;  /* rank-1 kernel variant 0..dlp_update_variants()-1, -1 = auto (default) */
+    int32_t ld_align;        /* tableau row stride alignment in doubles, multiple of 16, 0 = auto
+                                (default: 512 when a row has >= 4096 columns, else 16); the
+                                kernels only touch the first roundup(N+1,16) columns */
 } dlp_options;
+/* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
+ * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;
+ * otherwise it is partly Infinity-Cache resident -> uncapped, 4-row bands. */
 
 /* ---- library ---------------------------------------------------------- */
 void        dlp_options_default(dlp_options* opt);
@@ -141,7 +147,8 @@ int         dlp_device_count(int* count);
 int         dlp_rank_rows(int64_t m, int rank, int nranks, int64_t* first, int64_t* count);
 /* Deterministic winner of nranks candidates (same rule as the device select). */
 int         dlp_candidate_select(const dlp_candidate* cands, int n, int* winner);
-int64_t     dlp_tableau_ld(int64_t m, int64_t n);
+int64_t     dlp_tableau_ld(int64_t m, int64_t n);   /* roundup(N+1,16); sessions may pad more */
+int         dlp_update_variants(void);               /* number of rank-1 update variants */
 
 /* ---- problems ------------------------------------------------------------ */
 /* Dense LP: A is m x n row-major; inputs are copied. Requires b >= 0. */

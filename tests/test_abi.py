@@ -47,7 +47,9 @@ def test_options_default():
     o = dlp.options()
     assert o.pricing == L.PRICING_DANTZIG_BLAND and o.tol_dj == 1e-9 and o.tol_piv == 1e-9
     assert o.max_pivots == 1_000_000 and o.log_pivots == 1 and o.check_interval == 64
-    assert o.nontemporal == 1 and o.use_graph == 1 and o.timing == 0
+    assert o.nontemporal == -1 and o.use_graph == 1 and o.timing == 0
+    assert o.update_variant == -1 and o.ld_align == 0 and o.rows_per_block == 0
+    assert L.lib().dlp_update_variants() >= 30
 
 
 def test_status_strings():

@@ -76,6 +76,16 @@ def test_device_generator_matches_oracle(m, n, seed, degen):
     np.testing.assert_array_equal(T, O.gen_tableau(m, n, seed, degen))
 
 
+def test_aligned_row_stride_generation():
+    m, n, seed = 300, 129, 4
+    with dlp.Session(dlp.Problem.random(m, n, seed), ld_align=512) as s:
+        assert s.ld % 512 == 0 and s.ld >= O.ld(m, n)
+        T = s.tableau()
+    ref = O.gen_tableau(m, n, seed)
+    np.testing.assert_array_equal(T[:, :ref.shape[1]], ref)
+    assert not T[:, ref.shape[1]:].any()
+
+
 def test_device_generated_c1_solve():
     p = dlp.Problem.random(200, 400, 1)
     res = dlp.solve(p)
@@ -86,7 +96,9 @@ def test_device_generated_c1_solve():
 
 @pytest.mark.parametrize("opts", [dict(rows_per_block=4), dict(rows_per_block=8, nontemporal=0),
                                   dict(rows_per_block=128), dict(use_graph=0, check_interval=1),
-                                  dict(check_interval=7, timing=2), dict(timing=1)],
+                                  dict(check_interval=7, timing=2), dict(timing=1),
+                                  dict(ld_align=512, update_variant=12, rows_per_block=8),
+                                  dict(ld_align=64, update_variant=17)],
                          ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_launch_options_do_not_change_results(opts):
     A, b, c = O.gen_dense(200, 400, 2)
@@ -213,7 +225,7 @@ def test_batched_matches_single_gpu_path():
         _same_log(br.logs[k][:res.num_pivots], res.pivot_log)
 
 
-@pytest.mark.parametrize("variant", range(8))
+@pytest.mark.parametrize("variant", range(L.lib().dlp_update_variants()))
 def test_update_variants_bit_identical(variant):
     A, b, c = O.gen_dense(150, 260, 6)
     ref = O.solve_dense(A, b, c)
