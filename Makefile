@@ -13,7 +13,7 @@ LIBDLP    := $(PKG)/libdlp.so
 OBJS      := build/dlp_kernels.o build/dlp_batched.o build/dlp_session.o build/dlp_adalloc.o \
              build/dlp_instance.o
 
-all: $(LIBDLP) oracle
+all: $(LIBDLP) oracle tools
 
 build:
 	mkdir -p build
@@ -41,3 +41,10 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle ref asm clean
+
+tools: build/hbm_ceiling
+
+build/hbm_ceiling: tools/hbm_ceiling.hip | build
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
+.PHONY: tools
