@@ -10,7 +10,7 @@ CSRC      := $(PKG)/csrc
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -I$(CSRC) \
              -Wall -Wno-unused-function
 LIBDLP    := $(PKG)/libdlp.so
-OBJS      := build/dlp_kernels.o build/dlp_batched.o build/dlp_session.o build/dlp_adalloc.o \
+OBJS      := build/dlp_kernels.o build/dlp_batched.o build/dlp_mw.o build/dlp_session.o build/dlp_adalloc.o \
              build/dlp_instance.o
 
 all: $(LIBDLP) oracle tools

@@ -8,7 +8,7 @@ from ._lib import (NativeLibraryMissing, DLPError, OK, INFEASIBLE, UNBOUNDED, PI
                    RUNNING, PRICING_DANTZIG_BLAND, PRICING_BLAND, lib)
 from .solver import (Problem, Result, Session, BatchResult, solve, batched_solve, options,  # noqa: F401
                      rank_rows, candidate_select, tableau_ld, device_count, comm_unique_id,
-                     PIVOT_DTYPE, CAND_DTYPE)
+                     PIVOT_DTYPE, CAND_DTYPE, MW, MW_ITER_DTYPE)
 
 __all__ = ["Problem", "Result", "Session", "solve", "batched_solve", "options", "rank_rows",
            "candidate_select", "tableau_ld", "device_count", "comm_unique_id", "lib",

@@ -72,7 +72,19 @@ class Candidate(C.Structure):
     ]
 
 
-assert C.sizeof(Pivot) == 32 and C.sizeof(Candidate) == 32
+class MWOptions(C.Structure):
+    _fields_ = [("device", C.c_int32), ("binary", C.c_int32), ("epsilon", C.c_double),
+                ("tolerance", C.c_double)]
+
+
+class MWIter(C.Structure):
+    _fields_ = [("dual_value", C.c_double), ("max_infeasibility", C.c_double),
+                ("infeasible_advertiser", C.c_int32), ("pad", C.c_int32),
+                ("min_weight", C.c_double), ("max_weight", C.c_double),
+                ("weighted_budget", C.c_double)]
+
+
+assert C.sizeof(Pivot) == 32 and C.sizeof(Candidate) == 32 and C.sizeof(MWIter) == 48
 
 _P = C.c_void_p
 _I64 = C.c_int64
@@ -123,6 +135,11 @@ SIGNATURES = [
     ("dlp_session_read_rows", C.c_int, [_P, _I64, _I64, _DP]),
     ("dlp_session_result", C.c_int, [_P, C.POINTER(_P)]),
     ("dlp_session_free", None, [_P]),
+    ("dlp_mw_options_default", None, [C.POINTER(MWOptions)]),
+    ("dlp_mw_create", C.c_int, [_P, C.POINTER(MWOptions), C.POINTER(_P)]),
+    ("dlp_mw_run", C.c_int, [_P, C.c_int, C.POINTER(MWIter), _DP]),
+    ("dlp_mw_solution", C.c_int, [_P, _DP, _DP]),
+    ("dlp_mw_free", None, [_P]),
     ("dlp_result_status", C.c_int, [_P]),
     ("dlp_result_objective", C.c_double, [_P]),
     ("dlp_result_num_pivots", _I64, [_P]),

@@ -81,6 +81,7 @@ int build_adalloc(int A, int I, double sparsity, double scaling, AdAlloc* out) {
         }
     out->budget.assign(A, (double)(0.5L * (long double)(I / A) * (long double)scaling));
     out->max_bid = (double)max_bid;
+    out->sparsity = sparsity;
     return DLP_OK;
 }
 

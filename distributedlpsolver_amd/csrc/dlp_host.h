@@ -16,6 +16,7 @@ struct AdAlloc {
     std::vector<double> bid, budget;
     std::vector<int32_t> draws;      // draws per advertiser (loop bound check, R/instance.cpp:44)
     double max_bid = 0.0;
+    double sparsity = 0.0;           // bid_sparsity as given (MW width, R/allocation_mw.cpp:155)
 };
 
 int build_adalloc(int A, int I, double sparsity, double scaling, AdAlloc* out);

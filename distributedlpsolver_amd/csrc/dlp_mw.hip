@@ -1,0 +1,704 @@
+// dlp_mw.hip — SURVEY.md §8f row f3: the reference's multiplicative-weights
+// (MW) iteration, sort mode, on the GPU.  One MW iteration =
+//   weighted budget B = sum_fixed(w_a B_a)                 R/allocation_mw.cpp:102-108
+//   per impression: upper envelope of (price*w, price) + origin, envelope
+//     points (u, v) and budget cutoffs                      R/subproblem.cpp:186-233,
+//                                                           R/upper_envelope.cpp:15-38
+//   global split of B over envelope regions by slope       R/global_problem.cpp:224-255
+//   per impression: primal x from the allocated region     R/global_problem.cpp:325-412
+//   dual value = sum over impressions of u*beta + v        R/global_problem.cpp:306-322
+//   running average of x                                   R/instance.cpp:143-152
+//   per advertiser: slack, average slack, weight update    R/allocation_mw.cpp:163-203
+// with the fp64 spec of DESIGN.md §9 (fixed tie orders, fixed-order sums,
+// deterministic exp), so the result is bit-identical to the CPU restatement.
+//
+// Layout: bids in impression-major CSR (advertiser ascending inside an
+// impression) for the envelope/primal kernels, plus an advertiser-major index
+// for the slack gather (no float atomics: every sum has a fixed order).
+// Kernels: one wave per impression for the envelope (bitonic sort of the
+// points in LDS, then the monotone chain on one lane); a stable hipCUB radix
+// sort of all regions by slope; a chunked budget prefix; one lane per
+// impression / advertiser for primal and weights.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "dlp_host.h"
+#include "dlp_internal.h"
+
+namespace dlp {
+namespace mw {
+
+constexpr int kDegMax = 1024;   // points per impression (bids + origin) the envelope kernel holds
+constexpr int kChunk = 256;     // budget-prefix chunk (spec)
+constexpr double kHullTol = 1e-14;   // R/subproblem.cpp:205, 224
+
+// Deterministic exp (spec): x = k ln2 + r with k = rint(x / ln2), r by two
+// fma with ln2 split hi/lo, e^r by the degree-13 Taylor polynomial in Horner
+// form with fma, scaled by 2^k.  Identical IEEE operation sequence on host
+// oracle and device, hence bit-identical weights.
+__device__ inline double dexp(double x) {
+    const double inv_ln2 = 0x1.71547652b82fep+0;
+    const double ln2_hi = 0x1.62e42fefa39efp-1;
+    const double ln2_lo = 0x1.abc9e3b39803fp-56;
+    const double k = __builtin_rint(x * inv_ln2);
+    double r = __builtin_fma(-k, ln2_hi, x);
+    r = __builtin_fma(-k, ln2_lo, r);
+    double p = 0x1.6124613a86d09p-33;              // 1/13!
+    p = __builtin_fma(p, r, 0x1.1eed8eff8d898p-29);  // 1/12!
+    p = __builtin_fma(p, r, 0x1.ae64567f544e4p-26);  // 1/11!
+    p = __builtin_fma(p, r, 0x1.27e4fb7789f5cp-22);  // 1/10!
+    p = __builtin_fma(p, r, 0x1.71de3a556c734p-19);  // 1/9!
+    p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-16);  // 1/8!
+    p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-13);  // 1/7!
+    p = __builtin_fma(p, r, 0x1.6c16c16c16c17p-10);  // 1/6!
+    p = __builtin_fma(p, r, 0x1.1111111111111p-7);   // 1/5!
+    p = __builtin_fma(p, r, 0x1.5555555555555p-5);   // 1/4!
+    p = __builtin_fma(p, r, 0x1.5555555555555p-3);   // 1/3!
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return __builtin_ldexp(p, (int)k);
+}
+
+// Fixed-order sum (spec): 64 strided sequential chains, then the halving tree.
+__global__ __launch_bounds__(64) void sum_fixed_kernel(const double* __restrict__ x, int64_t n,
+                                                       double* __restrict__ out) {
+    double acc = 0.0;
+    for (int64_t k = threadIdx.x; k < n; k += 64) acc = acc + x[k];
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) acc = acc + __shfl_down(acc, w);
+    if (threadIdx.x == 0) *out = acc;
+}
+
+__global__ void weighted_budget_kernel(const double* __restrict__ w, const double* __restrict__ b,
+                                       int A, double* __restrict__ wb) {
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a < A) wb[a] = w[a] * b[a];
+}
+
+struct HullPt {
+    double c, p;
+    int adv;
+};
+
+__device__ inline bool hull_before(const HullPt& a, const HullPt& b) {   // (c desc, p desc, adv asc)
+    if (a.c != b.c) return a.c > b.c;
+    if (a.p != b.p) return a.p > b.p;
+    return a.adv < b.adv;
+}
+
+// One 64-lane workgroup per impression: points to LDS, bitonic sort, monotone
+// chain on lane 0, envelope points and cutoffs to the impression's slots.
+// Envelope slots of impression i start at iptr[i] + i (deg + 1 entries),
+// cutoff slots at iptr[i] + 2 i (deg + 2 entries).
+__global__ __launch_bounds__(64) void envelope_kernel(const int64_t* __restrict__ iptr,
+                                                      const int32_t* __restrict__ iadv,
+                                                      const double* __restrict__ ibid,
+                                                      const double* __restrict__ w, double* env_u,
+                                                      double* env_v, double* cut, int32_t* hull_h) {
+    __shared__ double sc[kDegMax], sp[kDegMax];
+    __shared__ int sa[kDegMax], stk[kDegMax];
+    const int i = blockIdx.x, lane = threadIdx.x;
+    const int64_t b0 = iptr[i], b1 = iptr[i + 1];
+    const int deg = (int)(b1 - b0);
+    if (deg == 0) {
+        if (lane == 0) hull_h[i] = 0;
+        return;
+    }
+    const int n = deg + 1;
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int t = lane; t < np2; t += 64) {
+        if (t < deg) {
+            const double p = ibid[b0 + t];
+            const int a = iadv[b0 + t];
+            sp[t] = p;
+            sc[t] = p * w[a];
+            sa[t] = a;
+        } else if (t == deg) {
+            sp[t] = 0.0;
+            sc[t] = 0.0;
+            sa[t] = -1;
+        } else {
+            sp[t] = -__builtin_inf();
+            sc[t] = -__builtin_inf();
+            sa[t] = 0x7fffffff;
+        }
+    }
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = lane; t < np2; t += 64) {
+                const int o = t ^ j;
+                if (o > t) {
+                    const HullPt A{sc[t], sp[t], sa[t]}, B{sc[o], sp[o], sa[o]};
+                    const bool asc = (t & k) == 0;   // "ascending" = hull order
+                    if (asc ? hull_before(B, A) : hull_before(A, B)) {
+                        sc[t] = B.c; sp[t] = B.p; sa[t] = B.adv;
+                        sc[o] = A.c; sp[o] = A.p; sa[o] = A.adv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (lane != 0) return;
+    int h = 0;
+    for (int q = 0; q < n; ++q) {
+        while (h >= 2) {
+            const int O = stk[h - 2], Aq = stk[h - 1];
+            const double d1 = (sc[Aq] - sc[O]) * (sp[q] - sp[O]);
+            const double d2 = (sp[Aq] - sp[O]) * (sc[q] - sc[O]);
+            if (d1 - d2 <= kHullTol) --h; else break;
+        }
+        stk[h++] = q;
+    }
+    const int64_t bu = b0 + i, bc = b0 + 2 * (int64_t)i;
+    {
+        const int q = stk[h - 2];
+        env_u[bu] = sp[q] / sc[q];
+        env_v[bu] = 0.0;
+    }
+    int e = 1;
+    for (int k = h - 2; k > 0; --k, ++e) {
+        const int q1 = stk[k - 1], q0 = stk[k];
+        const double uu = (sp[q1] - sp[q0]) / (sc[q1] - sc[q0]);
+        env_u[bu + e] = uu;
+        const double t = sc[q1] * uu;
+        env_v[bu + e] = sp[q1] - t;
+    }
+    env_u[bu + e] = 0.0;
+    env_v[bu + e] = sp[stk[0]];
+    cut[bc] = 0.0;
+    for (int k = 0; k < h - 1; ++k) {
+        const double du = env_u[bu + k] - env_u[bu + k + 1];
+        cut[bc + k + 1] = (du > kHullTol) ? (env_v[bu + k + 1] - env_v[bu + k]) / du : cut[bc + k];
+    }
+    cut[bc + h] = DBL_MAX;
+    hull_h[i] = h;
+}
+
+__global__ void region_count_kernel(const int32_t* __restrict__ hull_h, int I, int32_t* cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < I) cnt[i] = hull_h[i] >= 2 ? hull_h[i] - 1 : 0;
+}
+
+// Regions in (impression asc, region asc) order: key = slope u_j, value = id.
+__global__ void emit_regions_kernel(const int64_t* __restrict__ iptr, const int32_t* __restrict__ hull_h,
+                                    const int32_t* __restrict__ roff, const double* __restrict__ env_u,
+                                    int I, double* keys, int32_t* ids, int32_t* reg_imp,
+                                    int32_t* reg_j) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= I) return;
+    const int h = hull_h[i];
+    const int64_t bu = iptr[i] + i;
+    for (int j = 0; j + 1 < h; ++j) {
+        const int id = roff[i] + j;
+        keys[id] = env_u[bu + j];
+        ids[id] = id;
+        reg_imp[id] = i;
+        reg_j[id] = j;
+    }
+}
+
+// Chunked budget prefix (spec): chunk sums of the region widths in sorted order.
+__global__ void chunk_sum_kernel(const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ reg_imp,
+                                 const int32_t* __restrict__ reg_j, const int64_t* __restrict__ iptr,
+                                 const double* __restrict__ cut, int64_t R, double* __restrict__ width,
+                                 double* __restrict__ chunk) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k0 = c * kChunk;
+    if (k0 >= R) return;
+    const int64_t k1 = (k0 + kChunk < R) ? k0 + kChunk : R;
+    double acc = 0.0;
+    for (int64_t k = k0; k < k1; ++k) {
+        const int id = sorted_ids[k];
+        const int i = reg_imp[id], j = reg_j[id];
+        const int64_t bc = iptr[i] + 2 * (int64_t)i;
+        const double wd = cut[bc + j + 1] - cut[bc + j];
+        width[k] = wd;
+        acc = acc + wd;
+    }
+    chunk[c] = acc;
+}
+
+__global__ void chunk_offset_kernel(const double* __restrict__ chunk, int64_t nch,
+                                    double* __restrict__ offs) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double off = 0.0;
+    for (int64_t c = 0; c < nch; ++c) {
+        offs[c] = off;
+        off = off + chunk[c];
+    }
+}
+
+__global__ void allocate_kernel(const int32_t* __restrict__ sorted_ids, const double* __restrict__ width,
+                                const double* __restrict__ offs, const double* __restrict__ Bptr,
+                                int64_t R, double* __restrict__ inc_by_id, int32_t* __restrict__ pos_by_id) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k0 = c * kChunk;
+    if (k0 >= R) return;
+    const int64_t k1 = (k0 + kChunk < R) ? k0 + kChunk : R;
+    const double B = *Bptr;
+    double acc = offs[c];
+    for (int64_t k = k0; k < k1; ++k) {
+        const double pre = acc;
+        const double wd = width[k];
+        acc = acc + wd;
+        double rem = B - pre;
+        if (!(rem > 0.0)) rem = 0.0;
+        const int id = sorted_ids[k];
+        inc_by_id[id] = (wd < rem) ? wd : rem;   // std::min(rem, width)
+        pos_by_id[id] = (int32_t)k;
+    }
+}
+
+// Primal construction + dual contribution, one lane per impression.
+__global__ void primal_kernel(const int64_t* __restrict__ iptr, const int32_t* __restrict__ iadv,
+                              const double* __restrict__ ibid, const double* __restrict__ w,
+                              const int32_t* __restrict__ hull_h, const int32_t* __restrict__ roff,
+                              const double* __restrict__ env_u, const double* __restrict__ env_v,
+                              const double* __restrict__ inc_by_id, const int32_t* __restrict__ pos_by_id,
+                              int I, double tight_tol, double* __restrict__ x,
+                              double* __restrict__ dcontrib) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= I) return;
+    const int64_t b0 = iptr[i], b1 = iptr[i + 1];
+    for (int64_t q = b0; q < b1; ++q) x[q] = 0.0;
+    dcontrib[i] = 0.0;
+    const int h = hull_h[i];
+    if (h < 2) return;
+    // visit this impression's regions in global sorted order
+    double beta = 0.0;
+    int jstar = -1;
+    int last = -1;
+    for (int step = 0; step < h - 1; ++step) {
+        int best = -1, bpos = 0x7fffffff;
+        for (int j = 0; j < h - 1; ++j) {
+            const int pos = pos_by_id[roff[i] + j];
+            if (pos > last && pos < bpos) { bpos = pos; best = j; }
+        }
+        last = bpos;
+        const double inc = inc_by_id[roff[i] + best];
+        if (inc > 0.0) {
+            beta = beta + inc;
+            jstar = best;
+        }
+    }
+    if (!(beta > 0.0)) return;
+    const int64_t bu = b0 + i;
+    const double u = env_u[bu + jstar], v = env_v[bu + jstar];
+    const double t0 = u * beta;
+    dcontrib[i] = t0 + v;
+    if (u == 0.0) {   // greedy by price
+        int64_t best = -1;
+        double mp = 0.0;
+        for (int64_t q = b0; q < b1; ++q)
+            if (mp < ibid[q]) { mp = ibid[q]; best = q; }
+        if (best >= 0) x[best] = 1.0;
+    }
+    if (v == 0.0) {   // greedy by price / coefficient
+        int64_t best = -1;
+        double mr = 0.0;
+        for (int64_t q = b0; q < b1; ++q) {
+            const double c = ibid[q] * w[iadv[q]];
+            const double r = ibid[q] / c;
+            if (mr < r) { mr = r; best = q; }
+        }
+        if (best >= 0) x[best] = beta / (ibid[best] * w[iadv[best]]);
+    }
+    if (u > 0.0 && v > 0.0) {   // the (at most two) tight constraints
+        int64_t q0 = -1, q1 = -1;
+        int nt = 0;
+        for (int64_t q = b0; q < b1; ++q) {
+            const double c = ibid[q] * w[iadv[q]];
+            const double uc = u * c;
+            double sl = ibid[q] - (uc + v);
+            if (sl < 0) sl = -sl;
+            if (sl < tight_tol) {
+                if (nt == 0) q0 = q; else if (nt == 1) q1 = q;
+                ++nt;
+            }
+        }
+        if (nt == 1) {
+            const double c = ibid[q0] * w[iadv[q0]];
+            x[q0] = __builtin_fmin(beta / c, 1.0);
+        } else if (nt == 2) {
+            const double c0 = ibid[q0] * w[iadv[q0]], c1 = ibid[q1] * w[iadv[q1]];
+            const double x1 = (beta - c1) / (c0 - c1);
+            x[q0] = x1;
+            x[q1] = 1.0 - x1;
+        }
+    }
+}
+
+__global__ void average_kernel(const double* __restrict__ x, double* __restrict__ xa, int64_t nnz,
+                               double fa, double fb) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nnz) {
+        const double a = fa * xa[q], b = fb * x[q];
+        xa[q] = a + b;
+    }
+}
+
+// Per advertiser: slack (impressions ascending), running average, weight.
+__global__ void advertiser_kernel(const int64_t* __restrict__ aptr, const int64_t* __restrict__ apos,
+                                  const double* __restrict__ abid, const double* __restrict__ budgets,
+                                  const double* __restrict__ x, int A, double fa, double fb,
+                                  double width, double lp, double lm, double* __restrict__ slack,
+                                  double* __restrict__ avg_slack, double* __restrict__ w) {
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= A) return;
+    double s = -budgets[a];
+    for (int64_t k = aptr[a]; k < aptr[a + 1]; ++k) {
+        const double t = x[apos[k]] * abid[k];
+        s = s + t;
+    }
+    slack[a] = s;
+    const double p = fa * avg_slack[a], q = fb * s;
+    avg_slack[a] = p + q;
+    const double tt = s / width;
+    const double f = (tt >= 0.0) ? dexp(tt * lp) : dexp(-tt * lm);
+    w[a] = w[a] * f;
+}
+
+// Per-iteration report (one wave): worst average infeasibility (first index
+// on ties), min / max weight; writes log[t].
+__global__ __launch_bounds__(64) void report_kernel(const double* __restrict__ avg_slack,
+                                                    const double* __restrict__ budgets,
+                                                    const double* __restrict__ w, int A,
+                                                    const double* __restrict__ dual,
+                                                    const double* __restrict__ Bptr,
+                                                    dlp_mw_iter* __restrict__ log) {
+    double worst = 0.0, mn = 100000.0, mx = 0.0;
+    int wi = -1;
+    for (int a = threadIdx.x; a < A; a += 64) {
+        const double s = avg_slack[a];
+        if (s > 0.0) {
+            const double r = s / budgets[a];
+            if (r > worst) { worst = r; wi = a; }
+        }
+        mn = __builtin_fmin(mn, w[a]);
+        mx = __builtin_fmax(mx, w[a]);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const double ow = __shfl_xor(worst, m);
+        const int oi = __shfl_xor(wi, m);
+        if (ow > worst || (ow == worst && oi >= 0 && (wi < 0 || oi < wi))) { worst = ow; wi = oi; }
+        mn = __builtin_fmin(mn, __shfl_xor(mn, m));
+        mx = __builtin_fmax(mx, __shfl_xor(mx, m));
+    }
+    if (threadIdx.x == 0) {
+        dlp_mw_iter e;
+        e.dual_value = *dual;
+        e.max_infeasibility = worst;
+        e.infeasible_advertiser = wi;
+        e.pad = 0;
+        e.min_weight = mn;
+        e.max_weight = mx;
+        e.weighted_budget = *Bptr;
+        *log = e;
+    }
+}
+
+}  // namespace mw
+}  // namespace dlp
+
+struct dlp_mw {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int A = 0, I = 0;
+    int64_t nnz = 0;
+    double width = 0, lp = 0, lm = 0, tight_tol = 1e-12;
+    int t = 0;   // iterations done
+    // device arrays
+    int64_t *iptr = nullptr, *aptr = nullptr, *apos = nullptr;
+    int32_t *iadv = nullptr;
+    double *ibid = nullptr, *abid = nullptr, *budgets = nullptr, *w = nullptr, *wb = nullptr;
+    double *slack = nullptr, *avg_slack = nullptr, *x = nullptr, *xa = nullptr;
+    double *env_u = nullptr, *env_v = nullptr, *cut = nullptr;
+    int32_t *hull_h = nullptr, *rcnt = nullptr, *roff = nullptr;
+    double *keys = nullptr, *keys_sorted = nullptr, *width_sorted = nullptr;
+    int32_t *ids = nullptr, *ids_sorted = nullptr, *reg_imp = nullptr, *reg_j = nullptr, *pos_by_id = nullptr;
+    double *inc_by_id = nullptr, *chunk = nullptr, *offs = nullptr, *dcontrib = nullptr;
+    double *B = nullptr, *dual = nullptr;
+    int32_t *rtotal = nullptr;
+    dlp_mw_iter* dlog = nullptr;
+    int log_cap = 0;
+    void* cub_tmp = nullptr;
+    size_t cub_bytes = 0;
+    std::vector<int64_t> var_to_imp;   // problem variable k -> impression-major index
+};
+
+namespace {
+using dlp::set_error;
+
+#define MW_TRY(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));              \
+            return DLP_ERR_HIP;                                                        \
+        }                                                                              \
+    } while (0)
+
+template <typename T>
+int dalloc(T** p, size_t n) {
+    if (hipMalloc((void**)p, sizeof(T) * std::max<size_t>(n, 1)) != hipSuccess) {
+        set_error("dlp_mw: hipMalloc failed");
+        return DLP_ERR_OOM;
+    }
+    return DLP_OK;
+}
+
+void mw_free(dlp_mw* m) {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    void* ptrs[] = {m->iptr, m->aptr, m->apos, m->iadv, m->ibid, m->abid, m->budgets, m->w, m->wb,
+                    m->slack, m->avg_slack, m->x, m->xa, m->env_u, m->env_v, m->cut, m->hull_h,
+                    m->rcnt, m->roff, m->keys, m->keys_sorted, m->width_sorted, m->ids,
+                    m->ids_sorted, m->reg_imp, m->reg_j, m->pos_by_id, m->inc_by_id, m->chunk,
+                    m->offs, m->dcontrib, m->B, m->dual, m->rtotal, m->dlog, m->cub_tmp};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+}
+
+int mw_init(const dlp_problem* prob, const dlp_mw_options* o, dlp_mw* m) {
+    const auto& ad = prob->ad;
+    m->device = o->device;
+    m->A = ad.num_advertisers;
+    m->I = ad.num_impressions;
+    m->nnz = (int64_t)ad.adv.size();
+    const int A = m->A, I = m->I;
+    const int64_t nnz = m->nnz;
+    // impression-major order (impression asc, advertiser asc); problem variables are (a asc, i asc)
+    std::vector<int64_t> order(nnz);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int64_t a, int64_t b) { return ad.imp[a] < ad.imp[b]; });
+    std::vector<int64_t> iptr(I + 1, 0), aptr(A + 1, 0), apos(nnz);
+    std::vector<int32_t> iadv(nnz);
+    std::vector<double> ibid(nnz);
+    m->var_to_imp.resize(nnz);
+    for (int64_t k = 0; k < nnz; ++k) {
+        iptr[ad.imp[k] + 1]++;
+        aptr[ad.adv[k] + 1]++;
+    }
+    for (int i = 0; i < I; ++i) iptr[i + 1] += iptr[i];
+    for (int a = 0; a < A; ++a) aptr[a + 1] += aptr[a];
+    int maxdeg = 0;
+    for (int i = 0; i < I; ++i) maxdeg = std::max<int>(maxdeg, (int)(iptr[i + 1] - iptr[i]));
+    if (maxdeg + 1 > dlp::mw::kDegMax) {
+        set_error("dlp_mw: an impression has more bids than the envelope kernel holds");
+        return DLP_ERR_UNSUPPORTED;
+    }
+    for (int64_t q = 0; q < nnz; ++q) {
+        const int64_t k = order[q];
+        iadv[q] = ad.adv[k];
+        ibid[q] = ad.bid[k];
+        m->var_to_imp[k] = q;
+    }
+    for (int64_t k = 0; k < nnz; ++k) apos[k] = m->var_to_imp[k];   // advertiser-major = variable order
+    // width R/allocation_mw.cpp:154-161
+    double width = ad.max_bid * ((double)I * ad.sparsity);
+    for (int a = 0; a < A; ++a) width = std::max(width, ad.budget[a]);
+    m->width = width;
+    m->lp = std::log1p(o->epsilon);
+    m->lm = std::log1p(-o->epsilon);
+    m->tight_tol = std::max(o->tolerance, 1e-12);
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_error("no HIP device visible (libdlp has no CPU fallback)");
+        return DLP_ERR_NODEVICE;
+    }
+    MW_TRY(hipSetDevice(m->device));
+    MW_TRY(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+    int rc = DLP_OK;
+#define MW_ALLOC(ptr, n) if ((rc = dalloc(&(ptr), (n))) != DLP_OK) return rc
+    MW_ALLOC(m->iptr, I + 1); MW_ALLOC(m->aptr, A + 1); MW_ALLOC(m->apos, nnz);
+    MW_ALLOC(m->iadv, nnz); MW_ALLOC(m->ibid, nnz); MW_ALLOC(m->abid, nnz);
+    MW_ALLOC(m->budgets, A); MW_ALLOC(m->w, A); MW_ALLOC(m->wb, A);
+    MW_ALLOC(m->slack, A); MW_ALLOC(m->avg_slack, A); MW_ALLOC(m->x, nnz); MW_ALLOC(m->xa, nnz);
+    MW_ALLOC(m->env_u, nnz + I); MW_ALLOC(m->env_v, nnz + I); MW_ALLOC(m->cut, nnz + 2 * (int64_t)I);
+    MW_ALLOC(m->hull_h, I); MW_ALLOC(m->rcnt, I); MW_ALLOC(m->roff, I);
+    MW_ALLOC(m->keys, nnz); MW_ALLOC(m->keys_sorted, nnz); MW_ALLOC(m->width_sorted, nnz);
+    MW_ALLOC(m->ids, nnz); MW_ALLOC(m->ids_sorted, nnz); MW_ALLOC(m->reg_imp, nnz);
+    MW_ALLOC(m->reg_j, nnz); MW_ALLOC(m->pos_by_id, nnz); MW_ALLOC(m->inc_by_id, nnz);
+    MW_ALLOC(m->chunk, nnz / dlp::mw::kChunk + 2); MW_ALLOC(m->offs, nnz / dlp::mw::kChunk + 2);
+    MW_ALLOC(m->dcontrib, I); MW_ALLOC(m->B, 1); MW_ALLOC(m->dual, 1); MW_ALLOC(m->rtotal, 1);
+#undef MW_ALLOC
+    std::vector<double> ones(A, 1.0), zeros_a(A, 0.0), zeros_n(nnz, 0.0);
+    MW_TRY(hipMemcpy(m->iptr, iptr.data(), sizeof(int64_t) * (I + 1), hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->aptr, aptr.data(), sizeof(int64_t) * (A + 1), hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->apos, apos.data(), sizeof(int64_t) * nnz, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->iadv, iadv.data(), sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->ibid, ibid.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->abid, ad.bid.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->budgets, ad.budget.data(), sizeof(double) * A, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->w, ones.data(), sizeof(double) * A, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->slack, zeros_a.data(), sizeof(double) * A, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->avg_slack, zeros_a.data(), sizeof(double) * A, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->xa, zeros_n.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    MW_TRY(hipMemcpy(m->x, zeros_n.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    // hipCUB temporary storage: region sort (<= nnz items) and the region-count scan
+    size_t b1 = 0, b2 = 0;
+    MW_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b1, m->keys, m->keys_sorted, m->ids,
+                                                       m->ids_sorted, (int)std::max<int64_t>(nnz, 1),
+                                                       0, 64, m->stream));
+    MW_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, m->rcnt, m->roff, std::max(I, 1), m->stream));
+    m->cub_bytes = std::max(b1, b2);
+    MW_TRY(hipMalloc(&m->cub_tmp, std::max<size_t>(m->cub_bytes, 16)));
+    return DLP_OK;
+}
+
+int mw_iteration(dlp_mw* m, dlp_mw_iter* dlog_entry) {
+    using namespace dlp::mw;
+    const int A = m->A, I = m->I;
+    const int64_t nnz = m->nnz;
+    hipStream_t s = m->stream;
+    const int tb = 256;
+    const int t = m->t + 1;
+    const double fa = (double)(t - 1) / (double)t, fb = 1.0 / (double)t;
+    weighted_budget_kernel<<<(A + tb - 1) / tb, tb, 0, s>>>(m->w, m->budgets, A, m->wb);
+    sum_fixed_kernel<<<1, 64, 0, s>>>(m->wb, A, m->B);
+    envelope_kernel<<<I, 64, 0, s>>>(m->iptr, m->iadv, m->ibid, m->w, m->env_u, m->env_v, m->cut,
+                                     m->hull_h);
+    region_count_kernel<<<(I + tb - 1) / tb, tb, 0, s>>>(m->hull_h, I, m->rcnt);
+    size_t bytes = m->cub_bytes;
+    MW_TRY(hipcub::DeviceScan::ExclusiveSum(m->cub_tmp, bytes, m->rcnt, m->roff, I, s));
+    emit_regions_kernel<<<(I + tb - 1) / tb, tb, 0, s>>>(m->iptr, m->hull_h, m->roff, m->env_u, I,
+                                                         m->keys, m->ids, m->reg_imp, m->reg_j);
+    // region count R = roff[I-1] + rcnt[I-1]: read back (the sort needs it on the host)
+    int32_t last[2] = {0, 0};
+    MW_TRY(hipMemcpyAsync(&last[0], m->roff + (I - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    MW_TRY(hipMemcpyAsync(&last[1], m->rcnt + (I - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    MW_TRY(hipStreamSynchronize(s));
+    const int64_t R = (int64_t)last[0] + last[1];
+    if (R > 0) {
+        bytes = m->cub_bytes;
+        MW_TRY(hipcub::DeviceRadixSort::SortPairsDescending(m->cub_tmp, bytes, m->keys, m->keys_sorted,
+                                                           m->ids, m->ids_sorted, (int)R, 0, 64, s));
+        const int64_t nch = (R + kChunk - 1) / kChunk;
+        chunk_sum_kernel<<<(unsigned)((nch + tb - 1) / tb), tb, 0, s>>>(
+            m->ids_sorted, m->reg_imp, m->reg_j, m->iptr, m->cut, R, m->width_sorted, m->chunk);
+        chunk_offset_kernel<<<1, 64, 0, s>>>(m->chunk, nch, m->offs);
+        allocate_kernel<<<(unsigned)((nch + tb - 1) / tb), tb, 0, s>>>(
+            m->ids_sorted, m->width_sorted, m->offs, m->B, R, m->inc_by_id, m->pos_by_id);
+    }
+    primal_kernel<<<(I + tb - 1) / tb, tb, 0, s>>>(m->iptr, m->iadv, m->ibid, m->w, m->hull_h, m->roff,
+                                                   m->env_u, m->env_v, m->inc_by_id, m->pos_by_id, I,
+                                                   m->tight_tol, m->x, m->dcontrib);
+    sum_fixed_kernel<<<1, 64, 0, s>>>(m->dcontrib, I, m->dual);
+    average_kernel<<<(unsigned)((nnz + tb - 1) / tb), tb, 0, s>>>(m->x, m->xa, nnz, fa, fb);
+    advertiser_kernel<<<(A + tb - 1) / tb, tb, 0, s>>>(m->aptr, m->apos, m->abid, m->budgets, m->x, A,
+                                                       fa, fb, m->width, m->lp, m->lm, m->slack,
+                                                       m->avg_slack, m->w);
+    report_kernel<<<1, 64, 0, s>>>(m->avg_slack, m->budgets, m->w, A, m->dual, m->B, dlog_entry);
+    MW_TRY(hipGetLastError());
+    m->t = t;
+    return DLP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void dlp_mw_options_default(dlp_mw_options* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->device = 0;
+    o->binary = 0;
+    o->epsilon = 0.01;
+    o->tolerance = 1e-18;
+}
+
+int dlp_mw_create(const dlp_problem* prob, const dlp_mw_options* opt, dlp_mw** out) {
+    dlp_mw_options o;
+    if (opt) o = *opt; else dlp_mw_options_default(&o);
+    if (!prob || !out || prob->kind != dlp::PROB_ADALLOC || prob->ad.num_impressions <= 0) {
+        set_error("dlp_mw_create: needs an ad-allocation problem (dlp_problem_create_adalloc)");
+        return DLP_ERR_ARG;
+    }
+    if (o.binary) {
+        set_error("dlp_mw: binary-search mode stops at 1e-16, below fp64 resolution; use sort mode");
+        return DLP_ERR_UNSUPPORTED;
+    }
+    if (!(o.epsilon > 0.0 && o.epsilon < 1.0)) {
+        set_error("dlp_mw: epsilon must be in (0, 1)");
+        return DLP_ERR_ARG;
+    }
+    auto* m = new (std::nothrow) dlp_mw();
+    if (!m) return DLP_ERR_OOM;
+    int rc = DLP_OK;
+    try {
+        rc = mw_init(prob, &o, m);
+    } catch (const std::exception& e) {
+        set_error(std::string("dlp_mw_create: ") + e.what());
+        rc = DLP_ERR_OOM;
+    }
+    if (rc != DLP_OK) {
+        mw_free(m);
+        return rc;
+    }
+    *out = m;
+    return DLP_OK;
+}
+
+int dlp_mw_run(dlp_mw* m, int iterations, dlp_mw_iter* log, double* kernel_ms) {
+    if (!m || iterations < 0) return DLP_ERR_ARG;
+    MW_TRY(hipSetDevice(m->device));
+    if (iterations > m->log_cap) {
+        if (m->dlog) (void)hipFree(m->dlog);
+        m->dlog = nullptr;
+        MW_TRY(hipMalloc(&m->dlog, sizeof(dlp_mw_iter) * std::max(iterations, 1)));
+        m->log_cap = iterations;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    MW_TRY(hipEventCreate(&e0));
+    MW_TRY(hipEventCreate(&e1));
+    MW_TRY(hipEventRecord(e0, m->stream));
+    int rc = DLP_OK;
+    for (int k = 0; k < iterations && rc == DLP_OK; ++k) rc = mw_iteration(m, m->dlog + k);
+    if (rc == DLP_OK) {
+        MW_TRY(hipEventRecord(e1, m->stream));
+        MW_TRY(hipStreamSynchronize(m->stream));
+        float ms = 0.f;
+        MW_TRY(hipEventElapsedTime(&ms, e0, e1));
+        if (kernel_ms) *kernel_ms = ms;
+        if (log && iterations > 0)
+            MW_TRY(hipMemcpy(log, m->dlog, sizeof(dlp_mw_iter) * iterations, hipMemcpyDeviceToHost));
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}
+
+int dlp_mw_solution(dlp_mw* m, double* x_avg, double* weights) {
+    if (!m) return DLP_ERR_ARG;
+    MW_TRY(hipSetDevice(m->device));
+    MW_TRY(hipStreamSynchronize(m->stream));
+    if (x_avg) {
+        std::vector<double> xi(m->nnz);
+        MW_TRY(hipMemcpy(xi.data(), m->xa, sizeof(double) * m->nnz, hipMemcpyDeviceToHost));
+        for (int64_t k = 0; k < m->nnz; ++k) x_avg[k] = xi[m->var_to_imp[k]];
+    }
+    if (weights) MW_TRY(hipMemcpy(weights, m->w, sizeof(double) * m->A, hipMemcpyDeviceToHost));
+    return DLP_OK;
+}
+
+void dlp_mw_free(dlp_mw* m) { mw_free(m); }
+
+}  // extern "C"

@@ -68,7 +68,9 @@ class Problem:
         L.check(L.lib().dlp_problem_create_adalloc(num_advertisers, num_impressions, num_slots,
                                                    bid_sparsity, scaling_factor, C.byref(h)),
                 "dlp_problem_create_adalloc")
-        return cls(h.value, "adalloc")
+        p = cls(h.value, "adalloc")
+        p.num_advertisers, p.num_impressions = num_advertisers, num_impressions
+        return p
 
     def to_dense(self):
         A = np.zeros((self.m, self.n))
@@ -291,6 +293,53 @@ def batched_solve(nlp: int, m: int, n: int, seed: int, degenerate: bool = False,
         logs.ctypes.data_as(C.POINTER(L.Pivot)) if logs is not None else None, log_cap,
         C.byref(ms)), "dlp_batched_solve")
     return BatchResult(obj, st, npv, basis, logs, ms.value)
+
+
+MW_ITER_DTYPE = np.dtype([("dual_value", "<f8"), ("max_infeasibility", "<f8"),
+                          ("infeasible_advertiser", "<i4"), ("pad", "<i4"), ("min_weight", "<f8"),
+                          ("max_weight", "<f8"), ("weighted_budget", "<f8")])
+
+
+class MW:
+    """The reference's multiplicative-weights loop (sort mode) on the GPU
+    (dlp_mw_*): replaces Instance::RunMultiplicativeWeights(T, tol, false),
+    R/instance.cpp:117-124.  Needs a Problem.adalloc problem."""
+
+    def __init__(self, problem: Problem, epsilon: float = 0.01, tolerance: float = 1e-18,
+                 device: int = 0):
+        o = L.MWOptions()
+        L.lib().dlp_mw_options_default(C.byref(o))
+        o.epsilon, o.tolerance, o.device = epsilon, tolerance, device
+        self.problem = problem
+        h = C.c_void_p()
+        L.check(L.lib().dlp_mw_create(problem._h, C.byref(o), C.byref(h)), "dlp_mw_create")
+        self._h = h
+
+    def run(self, iterations: int):
+        """Run iterations; returns (per-iteration log array, device ms)."""
+        log = np.zeros(iterations, MW_ITER_DTYPE)
+        ms = C.c_double()
+        L.check(L.lib().dlp_mw_run(self._h, iterations, log.ctypes.data_as(C.POINTER(L.MWIter)),
+                                   C.byref(ms)), "dlp_mw_run")
+        return log, ms.value
+
+    def solution(self):
+        """(averaged x in the problem's variable order, advertiser weights)."""
+        x = np.zeros(self.problem.n)
+        w = np.zeros(self.problem.num_advertisers)
+        L.check(L.lib().dlp_mw_solution(self._h, _dptr(x), _dptr(w)), "dlp_mw_solution")
+        return x, w
+
+    def close(self):
+        if self._h:
+            L.lib().dlp_mw_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def rank_rows(m: int, rank: int, nranks: int) -> tuple[int, int]:

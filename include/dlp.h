@@ -228,6 +228,40 @@ int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, uint64_t seed
                       int64_t* npivots, int32_t* basis, dlp_pivot* logs, int64_t log_cap,
                       double* kernel_ms);
 
+/* ---- multiplicative-weights path ------------------
+ * The reference's own epsilon-approximate MW loop (R/allocation_mw.cpp:271-326,
+ * sort mode) on the GPU for an ad-allocation problem (dlp_problem_create_adalloc),
+ * with the fp64 spec of DESIGN.md §9 (fixed tie orders, fixed-order sums,
+ * deterministic exp): per impression an upper envelope (wave-level bitonic
+ * sort + monotone chain), a global slope sort (hipCUB radix sort), a blocked
+ * budget prefix, primal construction, per-advertiser slacks and weights.
+ * Scales to the reference's 100k x 1M x 1e-4 scenario, where a dense tableau
+ * cannot exist.  Replaces Instance::RunMultiplicativeWeights(T, tol, false)
+ * (R/instance.h:52, R/instance.cpp:117-124). */
+typedef struct dlp_mw dlp_mw;
+typedef struct dlp_mw_options {
+    int32_t device;
+    int32_t binary;        /* must be 0: binary mode's 1e-16 stop is below fp64 */
+    double  epsilon;       /* default 0.01 (R/main.cpp:33) */
+    double  tolerance;     /* numerical_accuracy_tolerance, default 1e-18; tight-set test uses max(tol, 1e-12) */
+} dlp_mw_options;
+typedef struct dlp_mw_iter {   /* per-iteration report (the reference's stdout, R/global_problem.cpp:320,
+                                  R/allocation_mw.cpp:214-220,264-268) */
+    double  dual_value;
+    double  max_infeasibility;
+    int32_t infeasible_advertiser;
+    int32_t pad;
+    double  min_weight, max_weight, weighted_budget;
+} dlp_mw_iter;
+void dlp_mw_options_default(dlp_mw_options* opt);
+int  dlp_mw_create(const dlp_problem* adalloc, const dlp_mw_options* opt, dlp_mw** out);
+/* Run `iterations` more MW iterations; log (may be NULL) gets one entry per iteration;
+ * *kernel_ms (may be NULL) the device time of the run. */
+int  dlp_mw_run(dlp_mw* mw, int iterations, dlp_mw_iter* log, double* kernel_ms);
+/* Averaged primal x in the problem's variable order (dlp_problem_adalloc_bids) and weights. */
+int  dlp_mw_solution(dlp_mw* mw, double* x_avg, double* weights);
+void dlp_mw_free(dlp_mw* mw);
+
 /* ---- results ------------------------------------------------------------- */
 int     dlp_result_status(const dlp_result* r);
 double  dlp_result_objective(const dlp_result* r);

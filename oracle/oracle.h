@@ -87,6 +87,17 @@ int oracle_run_generated(int kind, int64_t m, int64_t n, uint64_t seed, int64_t 
                          oracle_pivot* log, int64_t* npivots, const int64_t* rows_idx,
                          int64_t nrows, double* rows_out, int32_t* basis_out);
 
+/* fp64 restatement of the reference's MW loop, sort mode (oracle_mw.cpp): T
+ * iterations on the generated ad-allocation instance.  Per-iteration outputs
+ * (length T): dual value, max average infeasibility (+ advertiser), min / max
+ * weight, weighted budget.  x_avg_out: averaged primal in impression-major
+ * order (impression asc, advertiser asc), nnz entries. */
+int oracle_mw_run(int A, int I, double sparsity, double scaling, double epsilon, int T, double tol,
+                  double* dual, double* infeas, int32_t* infeas_idx, double* wmin, double* wmax,
+                  double* budget_w, double* x_avg_out, double* weights_out, int64_t* nnz_out);
+double oracle_dexp(double x);
+double oracle_sum_fixed(const double* x, int64_t n);
+
 /* CPU baseline: generate the tableau, do `warmup` pivots, time `k` pivots. */
 int oracle_bench_pivots(int kind, int64_t m, int64_t n, uint64_t seed, int64_t warmup, int64_t k,
                         int32_t nthreads, double* seconds, int64_t* done, double* gen_seconds);

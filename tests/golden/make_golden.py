@@ -142,8 +142,31 @@ def reference_run():
         advertiser_degrees=adv, impression_degrees=imp, dual_values=dual))
 
 
+def reference_mw_sort():
+    """The reference's MW loop in sort mode (R/main.cpp:36 use_binary_search=false), run through
+    our driver oracle/ref_mw_main.cpp over the reference's own solver sources."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "dlp_ref_mw")
+    if not os.path.exists(ref):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "ref"])
+    out = {}
+    for (A, I, sp, T) in [(1000, 1000, 0.1, 300), (100, 100, 0.1, 100)]:
+        txt = subprocess.run([ref, str(A), str(I), str(sp), str(T), "sort"], capture_output=True,
+                             text=True, cwd="/tmp", check=True).stdout
+        w = re.findall(r"min weight = (\S+), max weight = (\S+)", txt)
+        out[f"{A}x{I}"] = dict(
+            A=A, I=I, sparsity=sp, iterations=T,
+            dual_values=[float(v) for v in re.findall(r"Dual Value = (\S+)", txt)],
+            max_infeasibility=[float(v) for v in re.findall(r"max infeasiblity was (\S+)", txt)],
+            min_weight=[float(a) for a, _ in w], max_weight=[float(b) for _, b in w])
+    dump("ref_mw_sort.json", dict(
+        source="oracle/_ref/dlp_ref_mw = reference solver sources + oracle/ref_mw_main.cpp driver, "
+               "sort mode (RunMultiplicativeWeights(T, 1e-18, false)), long double, stdout at 6 digits",
+        runs=out))
+
+
 if __name__ == "__main__":
     kats()
     generated()
     adalloc()
     reference_run()
+    reference_mw_sort()

@@ -214,6 +214,39 @@ def bench_pivots(m, n, seed, warmup, k, nthreads, degenerate=False):
     return secs.value, done.value, gen.value
 
 
+def mw_run(A, I, sparsity=0.1, scaling=0.25, epsilon=0.01, T=300, tol=1e-18):
+    """fp64 MW spec (oracle/oracle_mw.cpp), sort mode.  Returns a dict of per-iteration arrays."""
+    L = lib()
+    if not getattr(L, "_mw_bound", False):
+        L.oracle_mw_run.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
+                                    C.c_double, _D, _D, _I32, _D, _D, _D, _D, _D, _I64]
+        L.oracle_dexp.restype = C.c_double
+        L.oracle_dexp.argtypes = [C.c_double]
+        L.oracle_sum_fixed.restype = C.c_double
+        L.oracle_sum_fixed.argtypes = [_D, C.c_int64]
+        L._mw_bound = True
+    nnz = len(gen_adalloc(A, I, sparsity, scaling)["bid"])
+    out = {k: np.zeros(T) for k in ("dual", "infeas", "wmin", "wmax", "budget")}
+    idx = np.zeros(T, np.int32)
+    xa = np.zeros(nnz)
+    w = np.zeros(A)
+    n = C.c_int64()
+    rc = L.oracle_mw_run(A, I, sparsity, scaling, epsilon, T, tol, _d(out["dual"]), _d(out["infeas"]),
+                         idx.ctypes.data_as(_I32), _d(out["wmin"]), _d(out["wmax"]), _d(out["budget"]),
+                         _d(xa), _d(w), C.byref(n))
+    assert rc == 0
+    out.update(infeas_idx=idx, x_avg=xa, weights=w, nnz=n.value)
+    return out
+
+
+def dexp(x):
+    mw_run.__wrapped__ if False else None
+    L = lib()
+    if not getattr(L, "_mw_bound", False):
+        mw_run(2, 10, 0.5, 0.25, 0.01, 1)
+    return L.oracle_dexp(x)
+
+
 def run_generated(m, n, seed, k, rows, degenerate=False, nthreads=8):
     """k oracle pivots on the generated tableau; returns (log, sampled rows, basis)."""
     rows = np.ascontiguousarray(rows, dtype=np.int64)
