@@ -101,16 +101,22 @@ def test_mw_gpu_run_in_pieces_equals_one_run():
 @pytest.mark.gpu
 def test_mw_large_scenario_properties():
     """The reference's commented-out large scenario shape, scaled to a test
-    (10k advertisers x 100k impressions x 1e-3): runs, every dual value is an
-    upper bound candidate (non-decreasing budget split), averaged x is feasible
-    for the assignment rows (sum over advertisers <= 1 per impression)."""
+    (10k advertisers x 100k impressions x 1e-3): size-independent properties.
+    The weighted budget is exactly split (sum of allocations = B when the
+    regions suffice), dual values are finite and positive, weights stay
+    positive, x >= 0.  (Per-impression sums of x are NOT <= 1: at iteration 1
+    all ratios tie and the reference's v == 0 branch gives beta / c to the
+    first tied constraint, R/global_problem.cpp:350-365 — reproduced as is.)"""
     A, I = 10000, 100000
     p = dlp.Problem.adalloc(A, I, 1, 1e-3, 0.25)
     mw = dlp.MW(p)
     log, ms = mw.run(20)
     x, w = mw.solution()
     assert np.isfinite(log["dual_value"]).all() and (log["dual_value"] > 0).all()
-    adv, imp, bid = p.adalloc_bids()
-    per_imp = np.bincount(imp, weights=x, minlength=I)
-    assert per_imp.max() <= 1.0 + 1e-9
-    assert (w > 0).all()
+    assert (x >= 0).all() and np.isfinite(x).all()
+    assert (w > 0).all() and np.isfinite(w).all()
+    # iteration 1: all weights 1 -> B = A * 0.5 * (I // A) * 0.25 exactly, every region has
+    # slope 1 and v = 0, so the dual value is the whole budget (the regions hold far more)
+    B0 = A * 0.5 * (I // A) * 0.25
+    assert log["weighted_budget"][0] == B0
+    assert abs(log["dual_value"][0] - B0) <= 1e-9 * B0
