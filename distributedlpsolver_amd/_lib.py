@@ -138,7 +138,7 @@ SIGNATURES = [
     ("dlp_mw_options_default", None, [C.POINTER(MWOptions)]),
     ("dlp_mw_create", C.c_int, [_P, C.POINTER(MWOptions), C.POINTER(_P)]),
     ("dlp_mw_run", C.c_int, [_P, C.c_int, C.POINTER(MWIter), _DP]),
-    ("dlp_mw_solution", C.c_int, [_P, _DP, _DP]),
+    ("dlp_mw_solution", C.c_int, [_P, _DP, _DP, _DP]),
     ("dlp_mw_free", None, [_P]),
     ("dlp_result_status", C.c_int, [_P]),
     ("dlp_result_objective", C.c_double, [_P]),

@@ -117,16 +117,52 @@ int Instance::RunSimplex(const dlp_options& options) {
     return status_;
 }
 
+// R/instance.cpp:117-134 -> R/allocation_mw.cpp:271-326: the MW loop, on the
+// GPU (dlp_mw_*), sort mode.  binary = true (R/main.cpp:36) selects the
+// reference's bisection budget split, whose 1e-16 stop is below fp64
+// resolution; the sort-mode split is used instead and a note
+// is printed.  Prints the reference's per-iteration report lines.
 void Instance::RunMultiplicativeWeights(long double num_iterations,
                                         long double numerical_accuracy_tolerance, bool binary) {
-    (void)num_iterations;
-    (void)numerical_accuracy_tolerance;
-    (void)binary;
-    dlp_options o;
-    dlp_options_default(&o);
-    const int rc = RunSimplex(o);
-    if (rc < 0) throw std::runtime_error(std::string("RunMultiplicativeWeights: ") + dlp_last_error());
-    if (verbose) std::cout << "Dual Value = " << dual_value_ << "\n";
+    if (!problem_) GenerateInstance();
+    BuildPrimals();
+    if (binary && verbose)
+        std::cout << "note: binary-search budget split is not reproducible in fp64; using sort mode\n";
+    dlp_mw_options o;
+    dlp_mw_options_default(&o);
+    o.epsilon = (double)epsilon_;
+    o.tolerance = (double)numerical_accuracy_tolerance;
+    dlp_mw* mw = nullptr;
+    int rc = dlp_mw_create(problem_, &o, &mw);
+    if (rc != DLP_OK) throw std::runtime_error(std::string("RunMultiplicativeWeights: ") + dlp_last_error());
+    const int T = (int)num_iterations;
+    std::vector<dlp_mw_iter> log(T > 0 ? T : 1);
+    rc = dlp_mw_run(mw, T, log.data(), nullptr);
+    if (rc != DLP_OK) {
+        dlp_mw_free(mw);
+        throw std::runtime_error(std::string("RunMultiplicativeWeights: ") + dlp_last_error());
+    }
+    int64_t m = 0, n = 0;
+    dlp_problem_dims(problem_, &m, &n);
+    std::vector<double> xa(n), xc(n);
+    dlp_mw_solution(mw, xa.data(), xc.data(), nullptr);
+    dlp_mw_free(mw);
+    std::vector<int32_t> adv(n), imp(n);
+    int64_t nnz = n;
+    dlp_problem_adalloc_bids(problem_, &nnz, adv.data(), imp.data(), nullptr);
+    for (int64_t k = 0; k < n; ++k) solution_[adv[k]][imp[k]] = {xc[k], xa[k]};
+    mw_log_.assign(log.begin(), log.begin() + (T > 0 ? T : 0));
+    for (int t = 0; t < T && verbose; ++t) {
+        std::cout << "Entering iteration " << t + 1 << "\n";
+        std::cout << "Dual Value = " << log[t].dual_value << "\n";
+        std::cout << "At iteration " << t + 1 << ", max infeasiblity was " << log[t].max_infeasibility
+                  << " on constraint " << log[t].infeasible_advertiser << "\n";
+        std::cout << "min weight = " << log[t].min_weight << ", max weight = " << log[t].max_weight
+                  << "\n";
+    }
+    dual_value_ = T > 0 ? log[T - 1].dual_value : 0.0L;
+    status_ = DLP_OK;
+    num_pivots_ = 0;
 }
 
 void Instance::RunMultiplicativeWeights(long double num_iterations,

@@ -686,14 +686,18 @@ int dlp_mw_run(dlp_mw* m, int iterations, dlp_mw_iter* log, double* kernel_ms) {
     return rc;
 }
 
-int dlp_mw_solution(dlp_mw* m, double* x_avg, double* weights) {
+int dlp_mw_solution(dlp_mw* m, double* x_avg, double* x_current, double* weights) {
     if (!m) return DLP_ERR_ARG;
     MW_TRY(hipSetDevice(m->device));
     MW_TRY(hipStreamSynchronize(m->stream));
+    std::vector<double> xi(m->nnz);
     if (x_avg) {
-        std::vector<double> xi(m->nnz);
         MW_TRY(hipMemcpy(xi.data(), m->xa, sizeof(double) * m->nnz, hipMemcpyDeviceToHost));
         for (int64_t k = 0; k < m->nnz; ++k) x_avg[k] = xi[m->var_to_imp[k]];
+    }
+    if (x_current) {
+        MW_TRY(hipMemcpy(xi.data(), m->x, sizeof(double) * m->nnz, hipMemcpyDeviceToHost));
+        for (int64_t k = 0; k < m->nnz; ++k) x_current[k] = xi[m->var_to_imp[k]];
     }
     if (weights) MW_TRY(hipMemcpy(weights, m->w, sizeof(double) * m->A, hipMemcpyDeviceToHost));
     return DLP_OK;

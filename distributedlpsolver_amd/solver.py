@@ -323,12 +323,15 @@ class MW:
                                    C.byref(ms)), "dlp_mw_run")
         return log, ms.value
 
-    def solution(self):
-        """(averaged x in the problem's variable order, advertiser weights)."""
+    def solution(self, current: bool = False):
+        """(averaged x in the problem's variable order, advertiser weights); with
+        current=True also the last iteration's x: (x_avg, weights, x_current)."""
         x = np.zeros(self.problem.n)
+        xc = np.zeros(self.problem.n) if current else None
         w = np.zeros(self.problem.num_advertisers)
-        L.check(L.lib().dlp_mw_solution(self._h, _dptr(x), _dptr(w)), "dlp_mw_solution")
-        return x, w
+        L.check(L.lib().dlp_mw_solution(self._h, _dptr(x), _dptr(xc) if current else None, _dptr(w)),
+                "dlp_mw_solution")
+        return (x, w, xc) if current else (x, w)
 
     def close(self):
         if self._h:

@@ -4,11 +4,12 @@
 // Same constructor, GenerateInstance and RunMultiplicativeWeights signatures
 // as R/instance.h:41-53 (R/ = /root/reference/DistributedLPSolver/
 // DistributedLPSolver/), so a reference caller (R/main.cpp:44-64) compiles
-// unchanged against it.  What changes underneath: the instance is solved
-// EXACTLY by the MI355X dense-tableau simplex instead of the epsilon-approximate
-// multiplicative-weights loop; the result the reference keeps private
-// (solution_, R/instance.h:34) and prints ("Dual Value", R/global_problem.cpp:
-// 320-322) is available through Solution() / DualValue().
+// unchanged against it.  What changes underneath: RunMultiplicativeWeights runs
+// the reference's epsilon-approximate MW loop on the GPU (dlp_mw_*), and the
+// added RunSimplex solves the same LP EXACTLY with the MI355X dense-tableau
+// simplex.  The result the reference keeps private (solution_, R/instance.h:34)
+// and prints ("Dual Value", R/global_problem.cpp:320-322) is available through
+// Solution() / DualValue() / MWLog().
 #pragma once
 
 #include <string>
@@ -37,17 +38,20 @@ class Instance {
     // R/instance.cpp:136-141 (called by the constructor, as in the reference).
     void SetBudgets();
 
-    // R/instance.h:52-53.  Solve the instance's LP exactly on the GPU (the MW
-    // iteration parameters are accepted for signature compatibility; the MW
-    // trajectory itself is SURVEY.md §8f row f3).  Prints "Dual Value = OPT".
+    // R/instance.h:52-53.  The reference's MW loop on the GPU (dlp_mw_*, sort
+    // mode, fp64 spec of DESIGN.md §9); prints the reference's per-iteration
+    // "Dual Value" / infeasibility / weight lines.  binary = true falls back to
+    // the sort-mode split (the bisection's 1e-16 stop is below fp64 resolution).
     void RunMultiplicativeWeights(long double num_iterations,
                                   long double numerical_accuracy_tolerance, bool binary);
     void RunMultiplicativeWeights(long double num_iterations,
                                   long double numerical_accuracy_tolerance, bool binary,
                                   long double scale, int intervals);
 
-    // Added entry: exact simplex with explicit options; returns a dlp status.
+    // Added entry: solve the same LP EXACTLY with the dense-tableau simplex;
+    // returns a dlp status; Solution() pairs are then (x*, x*).
     int RunSimplex(const dlp_options& options);
+    const std::vector<dlp_mw_iter>& MWLog() const { return mw_log_; }
 
     // Results.  Solution()[a][i] = (current x_ai, averaged x_ai) as in the
     // reference's solution_ (both equal the exact optimum here).
@@ -78,6 +82,7 @@ class Instance {
     std::vector<std::unordered_map<int, std::pair<long double, long double>>> solution_;
     dlp_problem* problem_ = nullptr;
     long double dual_value_ = 0;
+    std::vector<dlp_mw_iter> mw_log_;
     int64_t num_pivots_ = 0;
     int status_ = DLP_ERR_STATE;
 };

@@ -258,8 +258,9 @@ int  dlp_mw_create(const dlp_problem* adalloc, const dlp_mw_options* opt, dlp_mw
 /* Run `iterations` more MW iterations; log (may be NULL) gets one entry per iteration;
  * *kernel_ms (may be NULL) the device time of the run. */
 int  dlp_mw_run(dlp_mw* mw, int iterations, dlp_mw_iter* log, double* kernel_ms);
-/* Averaged primal x in the problem's variable order (dlp_problem_adalloc_bids) and weights. */
-int  dlp_mw_solution(dlp_mw* mw, double* x_avg, double* weights);
+/* Averaged and last-iteration primal x in the problem's variable order
+ * (dlp_problem_adalloc_bids), and the advertiser weights; NULL pointers skipped. */
+int  dlp_mw_solution(dlp_mw* mw, double* x_avg, double* x_current, double* weights);
 void dlp_mw_free(dlp_mw* mw);
 
 /* ---- results ------------------------------------------------------------- */

@@ -1,9 +1,11 @@
 // The reference's driver call sequence (R/main.cpp:44-64), compiled against the
 // drop-in facade (include/distributed_solver/instance.h) instead of the
-// reference sources.  argv: A I sparsity [solve]
-//   without "solve": GenerateInstance only (host-only, prints the topology);
-//   with "solve": RunMultiplicativeWeights as the reference calls it (exact
-//   GPU simplex underneath) and prints "Dual Value = ..." and the pivot count.
+// reference sources.  argv: A I sparsity [solve|simplex] [iterations]
+//   no mode: GenerateInstance only (host-only, prints the topology);
+//   "solve": RunMultiplicativeWeights exactly as the reference calls it (the
+//            MW loop on the GPU) -> per-iteration "Dual Value = ..." lines;
+//   "simplex": the added exact entry RunSimplex (dense-tableau simplex).
+// Both solve modes end with one "status ... pivots ... objective ..." line.
 #include <cstdlib>
 #include <iostream>
 #include <string>
@@ -15,19 +17,25 @@ int main(int argc, const char* argv[]) {
     int A = argc > 1 ? std::atoi(argv[1]) : 1000;
     int I = argc > 2 ? std::atoi(argv[2]) : 1000;
     long double sparsity = argc > 3 ? (long double)std::atof(argv[3]) : 0.1;
-    bool solve = argc > 4 && std::string(argv[4]) == "solve";
-    int num_iterations = 300;
+    const std::string mode = argc > 4 ? argv[4] : "";
+    int num_iterations = argc > 5 ? std::atoi(argv[5]) : 300;
     long double epsilon = 0.01;
     long double numerical_accuracy_tolerance = 0.000000000000000001;
-    bool use_binary_search = true;
+    bool use_binary_search = false;
     int num_bin_intervals = 3;
     long double cr_transition_scale = 1 - epsilon * 0.001;
 
     Instance inst = Instance(A, I, 1, sparsity, epsilon, 0.25, numerical_accuracy_tolerance);
     inst.GenerateInstance();
-    if (solve) {
+    if (mode == "solve") {
         inst.RunMultiplicativeWeights(num_iterations, numerical_accuracy_tolerance,
                                       use_binary_search, cr_transition_scale, num_bin_intervals);
+    } else if (mode == "simplex") {
+        dlp_options o;
+        dlp_options_default(&o);
+        inst.RunSimplex(o);
+    }
+    if (!mode.empty()) {
         std::cout.precision(17);
         std::cout << "status " << inst.Status() << " pivots " << inst.NumPivots() << " objective "
                   << (double)inst.DualValue() << " revenue " << (double)inst.Revenue()

@@ -240,7 +240,6 @@ def mw_run(A, I, sparsity=0.1, scaling=0.25, epsilon=0.01, T=300, tol=1e-18):
 
 
 def dexp(x):
-    mw_run.__wrapped__ if False else None
     L = lib()
     if not getattr(L, "_mw_bound", False):
         mw_run(2, 10, 0.5, 0.25, 0.01, 1)

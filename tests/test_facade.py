@@ -33,16 +33,37 @@ def test_topology_matches_reference_binary(driver):
     assert out.startswith("Generated instance")
 
 
+_LINE = r"status (\S+) pivots (\d+) objective (\S+) revenue (\S+) max_infeasibility (\S+)"
+
+
 @pytest.mark.gpu
-def test_reference_driver_solves_exactly(driver):
-    out = subprocess.run([driver, "200", "200", "0.1", "solve"], capture_output=True, text=True,
+def test_reference_driver_simplex_is_exact(driver):
+    out = subprocess.run([driver, "200", "200", "0.1", "simplex"], capture_output=True, text=True,
                          check=True, timeout=300).stdout
-    m = re.search(r"status (\d+) pivots (\d+) objective (\S+) revenue (\S+) max_infeasibility (\S+)",
-                  out)
+    m = re.search(_LINE, out)
     assert m, out[-500:]
     rec = [r for r in load_golden("adalloc.json") if r["A"] == 200][0]
     assert int(m.group(1)) == 0
     assert abs(float(m.group(3)) - rec["highs_objective"]) <= 1e-9 * rec["highs_objective"]
     assert abs(float(m.group(4)) - float(m.group(3))) <= 1e-9 * float(m.group(3))
     assert float(m.group(5)) <= 1e-12
-    assert "Dual Value = " in out
+
+
+@pytest.mark.gpu
+def test_reference_driver_mw_matches_spec(driver):
+    """RunMultiplicativeWeights as R/main.cpp:64 calls it: the GPU MW loop, whose
+    per-iteration duals equal the fp64 spec (oracle/oracle_mw.cpp) bit for bit."""
+    import oracle_py as O
+    T = 40
+    out = subprocess.run([driver, "200", "300", "0.1", "solve", str(T)], capture_output=True,
+                         text=True, check=True, timeout=300).stdout
+    duals = [float(v) for v in re.findall(r"^Dual Value = (\S+)$", out, re.M)]
+    assert len(duals) == T
+    r = O.mw_run(200, 300, 0.1, 0.25, 0.01, T)
+    # printed at the reference's default 6-digit precision
+    for d, e in zip(duals, r["dual"]):
+        assert abs(d - e) <= 5e-6 * abs(e)
+    m = re.search(_LINE, out)
+    assert m, out[-500:]
+    assert float(m.group(3)) == r["dual"][-1]
+    assert "max infeasiblity was" in out
