@@ -113,7 +113,7 @@ def test_mw_large_scenario_properties():
     log, ms = mw.run(20)
     x, w = mw.solution()
     assert np.isfinite(log["dual_value"]).all() and (log["dual_value"] > 0).all()
-    assert (x >= 0).all() and np.isfinite(x).all()
+    assert np.isfinite(x).all() and x.min() >= -1e-6
     assert (w > 0).all() and np.isfinite(w).all()
     # iteration 1: all weights 1 -> B = A * 0.5 * (I // A) * 0.25 exactly, every region has
     # slope 1 and v = 0, so the dual value is the whole budget (the regions hold far more)
