@@ -5,7 +5,7 @@ The drop-in for the per-iteration solver core of shidanxu/DistributedLPSolver
 behind the C ABI of include/dlp.h); this package is the thin host binding.
 """
 from ._lib import (NativeLibraryMissing, DLPError, OK, INFEASIBLE, UNBOUNDED, PIVOT_LIMIT,  # noqa: F401
-                   RUNNING, PRICING_DANTZIG_BLAND, PRICING_BLAND, lib)
+                   RUNNING, PRICING_DANTZIG_BLAND, PRICING_BLAND, MINIMIZE, MAXIMIZE, lib)
 from .solver import (Problem, Result, Session, BatchResult, solve, batched_solve, options,  # noqa: F401
                      rank_rows, candidate_select, tableau_ld, device_count, comm_unique_id,
                      PIVOT_DTYPE, CAND_DTYPE, MW, MW_ITER_DTYPE)

@@ -17,6 +17,7 @@ OK, INFEASIBLE, UNBOUNDED, PIVOT_LIMIT, RUNNING = 0, 1, 2, 3, 4
 ERR_ARG, ERR_OOM, ERR_HIP, ERR_RCCL, ERR_NODEVICE, ERR_STATE, ERR_UNSUPPORTED = -1, -2, -3, -4, -5, -6, -7
 PRICING_DANTZIG_BLAND, PRICING_BLAND = 0, 1
 GEN_DENSE, GEN_DEGENERATE = 0, 1
+MINIMIZE, MAXIMIZE = 1, -1
 BUF_CAND_SEND, BUF_CAND_RECV, BUF_PROW_SEND, BUF_PROW_RECV = 0, 1, 2, 3
 PHASE_RATIO, PHASE_EXCHANGE, PHASE_PROW, PHASE_UPDATE = 0, 1, 2, 3
 NUM_PHASES = 4
@@ -47,6 +48,8 @@ class Options(C.Structure):
         ("use_graph", C.c_int32),
         ("update_variant", C.c_int32),
         ("ld_align", C.c_int32),
+        ("pad_", C.c_int32),
+        ("tol_feas", C.c_double),
     ]
 
 
@@ -105,6 +108,13 @@ SIGNATURES = [
     ("dlp_problem_create_random", C.c_int, [C.c_int, _I64, _I64, C.c_uint64, C.POINTER(_P)]),
     ("dlp_problem_create_adalloc", C.c_int,
      [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.POINTER(_P)]),
+    ("dlp_problem_create_general", C.c_int,
+     [_I64, _I64, _DP, _DP, _DP, _DP, _DP, _DP, C.c_double, C.c_int, C.POINTER(_P)]),
+    ("dlp_problem_create_mps", C.c_int, [C.c_char_p, C.POINTER(_P)]),
+    ("dlp_problem_get_general", C.c_int,
+     [_P, _DP, _DP, _DP, _DP, _DP, _DP, _DP, C.POINTER(C.c_int)]),
+    ("dlp_problem_std_dims", C.c_int,
+     [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64)]),
     ("dlp_problem_dims", C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     ("dlp_problem_get_dense", C.c_int, [_P, _DP, _DP, _DP]),
     ("dlp_problem_adalloc_bids", C.c_int,
@@ -146,6 +156,7 @@ SIGNATURES = [
     ("dlp_result_x", C.c_int, [_P, _DP, _I64]),
     ("dlp_result_y", C.c_int, [_P, _DP, _I64]),
     ("dlp_result_basis", C.c_int, [_P, C.POINTER(_I32), _I64]),
+    ("dlp_result_info", C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     ("dlp_result_pivot_log", C.c_int, [_P, C.POINTER(Pivot), _I64, C.POINTER(_I64)]),
     ("dlp_result_timings", C.c_int, [_P, _DP]),
     ("dlp_result_free", None, [_P]),

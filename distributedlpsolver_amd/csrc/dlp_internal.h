@@ -18,6 +18,7 @@ constexpr int kRatioThreads = 256;
 constexpr int kProwThreads = 256;
 constexpr int32_t kNoIndex = 0x7fffffff;
 constexpr int kColqPad = 16;   // colq allocated with rows + 1 + kColqPad entries
+constexpr int32_t kStatusSkip = 5;   // DevState.status: redundant row, forced pivot skipped
 
 // Pricing partial of one column tile of the objective row.
 struct alignas(16) PricePart {
@@ -69,7 +70,10 @@ struct Geometry {
     int64_t width;        // round16(N+1): columns the kernels touch
     int64_t rows;         // local constraint rows
     int64_t row_first;    // global index of local row 0
-    int64_t ncols;        // N = n + m (pricing columns; RHS column index)
+    int64_t ncols;        // N (RHS column index): n + m, or the general LP's total columns
+    int64_t nprice;       // columns [0, nprice) are priced (general LPs: artificials excluded)
+    int64_t rows_elig;    // local rows [0, rows_elig) take part in the ratio test (the
+                          // carried Phase II objective row, when present, is local row rows-1)
     int ntiles;           // ceil(ld / kUpdTile)
     int rows_per_block;   // update kernel
 };
@@ -88,7 +92,19 @@ hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* bas
 int ratio_blocks(const Geometry& g);
 hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32_t* basis,
                          DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
-                         hipStream_t s);
+                         hipStream_t s, bool forced = false);
+// General LPs (Phase I -> II).  drive: forced-pivot candidate for global row
+// `row` (nranks == 1: also select + colq capture); gather_q: colq of st->q;
+// carry_out / carry_in: ship the carried objective row through the int64 MAX
+// exchange buffers and install it as the objective row (status -> running).
+hipError_t launch_drive(const Geometry& g, int64_t row, int32_t* basis, DevState* st,
+                        double tol_piv, Cand* cand_out, int nranks, int pricing, dlp_pivot* log,
+                        int64_t log_cap, double* colq, hipStream_t s);
+hipError_t launch_gather_q(const Geometry& g, const DevState* st, double* colq, hipStream_t s);
+hipError_t launch_carry_out(const Geometry& g, int64_t carry_local, int64_t* out, hipStream_t s);
+hipError_t launch_carry_in(const Geometry& g, const int64_t* in, DevState* st, int pricing,
+                           hipStream_t s);
+hipError_t launch_set_status(DevState* st, int status, hipStream_t s);
 hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits, int nranks,
                        hipStream_t s);
 hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,

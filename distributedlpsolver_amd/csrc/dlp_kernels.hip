@@ -154,17 +154,17 @@ __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* ba
 // a1 at start-up: pricing partials of the initial objective row, one per
 // 512-column tile (the same tiling the update kernel's fused epilogue uses).
 __global__ __launch_bounds__(kUpdThreads) void price_init_kernel(const double* __restrict__ zrow,
-                                                                 int64_t ncols, int tile,
+                                                                 int64_t nprice, int tile,
                                                                  PricePart* pp, double tol_dj) {
     __shared__ PricePart lds[4];
     PricePart acc = pp_empty();
     const int per_lane = tile / kUpdThreads;   // 2 or 4 columns per lane, ascending
     const int64_t j = (int64_t)blockIdx.x * tile + (int64_t)threadIdx.x * per_lane;
     for (int k = 0; k < per_lane; k += 2)
-        if (j + k < ncols) {
+        if (j + k < nprice) {
             const double z0 = zrow[j + k];
-            const double z1 = (j + k + 1 < ncols) ? zrow[j + k + 1] : 0.0;
-            price_pair(acc, z0, z1, j + k, ncols, tol_dj);
+            const double z1 = (j + k + 1 < nprice) ? zrow[j + k + 1] : 0.0;
+            price_pair(acc, z0, z1, j + k, nprice, tol_dj);
         }
     acc = block_price(acc, lds);
     if (threadIdx.x == 0) pp[blockIdx.x] = acc;
@@ -179,8 +179,8 @@ __global__ __launch_bounds__(kUpdThreads) void price_init_kernel(const double* _
 // Nearest reference analog: the tolerance-gated tight-set test
 // R/global_problem.cpp:372-380 and first-wins scans :335-361.
 __global__ __launch_bounds__(kRatioThreads) void ratio_kernel(
-    const double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t row_first,
-    const int32_t* basis, int32_t* basis_w, const PricePart* __restrict__ pp, int ntiles,
+    const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
+    int64_t row_first, const int32_t* basis, int32_t* basis_w, const PricePart* __restrict__ pp, int ntiles,
     DevState* st, double* __restrict__ colq, Cand* partials, Cand* cand_out, int nranks,
     double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap) {
     __shared__ PricePart lds_pp[4];
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kRatioThreads) void ratio_kernel(
     if (i <= rows) {
         const double a = T[i * ld + q];
         colq[i] = a;
-        if (i < rows && a > tol_piv) {
+        if (i < rows_elig && a > tol_piv) {
             double rhs = T[i * ld + ncols];
             if (!(rhs > 0.0)) rhs = 0.0;
             c.ratio = rhs / a;
@@ -258,14 +258,115 @@ __global__ __launch_bounds__(kRatioThreads) void ratio_kernel(
 
 // a4 for nranks > 1: every rank reduces the same all-gathered candidates in
 // the same order, so all ranks agree on p with no MINLOC collective.
+// Forced (Phase I drive-out) pivot: q travels in the candidate's pad0; a row
+// with no usable column is redundant and the pivot is skipped.
+__device__ inline void forced_select(DevState* st, const Cand& best, int32_t* basis,
+                                     int64_t row_first, int64_t rows, int pricing,
+                                     dlp_pivot* log, int64_t log_cap) {
+    if (!best.valid) {
+        st->status = kStatusSkip;
+        return;
+    }
+    do_select(st, best, best.pad0, basis, row_first, rows, pricing, log, log_cap);
+}
+
 __global__ void select_kernel(const Cand* cands, int nranks, int32_t* basis, DevState* st,
                               int64_t row_first, int64_t rows, int pricing, dlp_pivot* log,
-                              int64_t log_cap) {
+                              int64_t log_cap, int forced) {
     if (st->status != DLP_RUNNING || threadIdx.x != 0) return;
     Cand best = cand_empty();
     for (int r = 0; r < nranks; ++r)
         if (cand_better(cands[r], best)) best = cands[r];
-    do_select(st, best, st->q, basis, row_first, rows, pricing, log, log_cap);
+    if (forced)
+        forced_select(st, best, basis, row_first, rows, pricing, log, log_cap);
+    else
+        do_select(st, best, st->q, basis, row_first, rows, pricing, log, log_cap);
+}
+
+// ---- general LPs: Phase I -> Phase II transition (include/dlp.h, "general LPs")
+// Drive-out candidate for the artificial basic in global row `row`: the first
+// priced column with |T[row][q]| > tol_piv (block min over each lane's first
+// hit in its stride).  One workgroup; the owner rank produces the candidate.
+__global__ __launch_bounds__(kRatioThreads) void drive_kernel(
+    const double* __restrict__ T, int64_t ld, int64_t rows_elig, int64_t row_first, int64_t nprice,
+    int64_t row, int32_t* basis, DevState* st, double tol_piv, Cand* cand_out, int nranks,
+    int pricing, dlp_pivot* log, int64_t log_cap, int64_t rows) {
+    __shared__ int32_t lds[kRatioThreads / 64];
+    if (threadIdx.x == 0 && st->status == kStatusSkip) st->status = DLP_RUNNING;
+    const int64_t pl = row - row_first;
+    const bool mine = pl >= 0 && pl < rows_elig;
+    int32_t q = kNoIndex;
+    if (mine)
+        for (int64_t j = threadIdx.x; j < nprice; j += blockDim.x)
+            if (__builtin_fabs(T[pl * ld + j]) > tol_piv) {
+                q = (int32_t)j;
+                break;
+            }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const int32_t o = __shfl_xor(q, m);
+        q = o < q ? o : q;
+    }
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = q;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) q = lds[w] < q ? lds[w] : q;
+    Cand c = cand_empty();
+    if (mine && q != kNoIndex) {
+        c.valid = 1;
+        c.ratio = 0.0;
+        c.row = (int32_t)row;
+        c.basis_var = basis[row];
+        c.pad0 = q;
+        c.pivot = T[pl * ld + q];
+    }
+    if (nranks == 1) {
+        if (st->status == DLP_RUNNING)
+            forced_select(st, c, basis, row_first, rows, pricing, log, log_cap);
+    } else {
+        cand_out[0] = c;
+    }
+}
+
+// colq capture for a forced pivot (q known only after the select).
+__global__ void gather_q_kernel(const double* __restrict__ T, int64_t ld, int64_t rows,
+                                const DevState* st, double* __restrict__ colq) {
+    if (st->status != DLP_RUNNING) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= rows) colq[i] = T[i * ld + st->q];
+}
+
+// The carried Phase II objective row's fp64 bits (owner) / INT64_MIN (others),
+// delivered to every rank by the same int64 MAX exchange as a pivot row.
+__global__ __launch_bounds__(kProwThreads) void carry_out_kernel(const double* __restrict__ T,
+                                                                 int64_t ld, int64_t carry_local,
+                                                                 int64_t* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ld) return;
+    if (carry_local >= 0) {
+        const double v = T[carry_local * ld + j];
+        out[j] = __builtin_bit_cast(int64_t, v);
+    } else {
+        out[j] = INT64_MIN;
+    }
+}
+
+// Install the received row as the objective row; Phase II starts running.
+__global__ __launch_bounds__(kProwThreads) void carry_in_kernel(double* __restrict__ T, int64_t ld,
+                                                                int64_t rows,
+                                                                const int64_t* __restrict__ in,
+                                                                DevState* st, int pricing) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < ld) T[rows * ld + j] = __builtin_bit_cast(double, in[j]);
+    if (j == 0) {
+        st->status = DLP_RUNNING;
+        st->q = -1;
+        st->bland = pricing == DLP_PRICING_BLAND ? 1 : 0;
+    }
+}
+
+__global__ void set_status_kernel(DevState* st, int status) {
+    if (threadIdx.x == 0) st->status = status;
 }
 
 // a3 (first half): normalised pivot row, IEEE division (never a reciprocal
@@ -328,7 +429,7 @@ __device__ inline void price_lane(PricePart& acc, const d2* z, int64_t j, int64_
 
 template <bool NT, int U, int VEC, bool LDSQ>
 __global__ __launch_bounds__(kUpdThreads) void update_kernel(
-    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
     PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
     constexpr int TILE = kUpdThreads * VEC;
@@ -403,7 +504,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(
             }
         }
         PricePart acc = pp_empty();
-        if (colok) price_lane<VEC>(acc, z, j, ncols, tol_dj);
+        if (colok) price_lane<VEC>(acc, z, j, nprice, tol_dj);
         acc = block_price(acc, lds_pp);
         if (threadIdx.x == 0) pp[tile] = acc;
         if (log && colok && j <= ncols && ncols < j + VEC) {
@@ -423,7 +524,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(
 // to update_kernel (same fma per element, same skipped rows).
 template <bool NT, int U, int THREADS>
 __global__ __launch_bounds__(THREADS) void update_fast_kernel(
-    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
     PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
     constexpr int TILE = THREADS * 2;
@@ -487,7 +588,7 @@ __global__ __launch_bounds__(THREADS) void update_fast_kernel(
             *(d2*)zp = z;
         }
         PricePart acc = pp_empty();
-        if (colok) price_pair(acc, z.x, z.y, j, ncols, tol_dj);
+        if (colok) price_pair(acc, z.x, z.y, j, nprice, tol_dj);
         acc = block_price(acc, lds_pp);
         if (threadIdx.x == 0) pp[tile] = acc;
         if (log && colok && j <= ncols && ncols < j + 2) {
@@ -505,7 +606,7 @@ __global__ __launch_bounds__(THREADS) void update_fast_kernel(
 // (tuning log).  Same arithmetic and skip rules as update_kernel.
 template <bool NT, int VEC>
 __global__ __launch_bounds__(kUpdThreads) void update_serial_kernel(
-    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
     PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
     constexpr int TILE = kUpdThreads * VEC;
@@ -561,7 +662,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_serial_kernel(
             }
         }
         PricePart acc = pp_empty();
-        if (colok) price_lane<VEC>(acc, z, j, ncols, tol_dj);
+        if (colok) price_lane<VEC>(acc, z, j, nprice, tol_dj);
         acc = block_price(acc, lds_pp);
         if (threadIdx.x == 0) pp[tile] = acc;
         if (log && colok && j <= ncols && ncols < j + VEC) {
@@ -578,7 +679,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_serial_kernel(
 // arithmetic and skip rules as update_kernel.
 template <bool NT, int DEPTH, int VEC>
 __global__ __launch_bounds__(kUpdThreads) void update_stream_kernel(
-    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const double* __restrict__ colq, const double* __restrict__ prow, const DevState* st,
     PricePart* __restrict__ pp, int rb, double tol_dj, dlp_pivot* log, int64_t log_cap) {
     constexpr int TILE = kUpdThreads * VEC;
@@ -649,7 +750,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_stream_kernel(
             }
         }
         PricePart acc = pp_empty();
-        if (colok) price_lane<VEC>(acc, z, j, ncols, tol_dj);
+        if (colok) price_lane<VEC>(acc, z, j, nprice, tol_dj);
         acc = block_price(acc, lds_pp);
         if (threadIdx.x == 0) pp[tile] = acc;
         if (log && colok && j <= ncols && ncols < j + VEC) {
@@ -742,7 +843,7 @@ hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, in
     const double* z = g.T + g.rows * g.ld;
     const int tile = update_tile(variant);
     const int ntiles = (int)((g.width + tile - 1) / tile);
-    price_init_kernel<<<ntiles, kUpdThreads, 0, s>>>(z, g.ncols, tile, pp, tol_dj);
+    price_init_kernel<<<ntiles, kUpdThreads, 0, s>>>(z, g.nprice, tile, pp, tol_dj);
     return hipGetLastError();
 }
 
@@ -750,7 +851,8 @@ hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* bas
                         const PricePart* pp, DevState* st, double* colq, Cand* partials,
                         int nblocks, Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                         int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
-    ratio_kernel<<<nblocks, kRatioThreads, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.row_first,
+    ratio_kernel<<<nblocks, kRatioThreads, 0, s>>>(g.T, g.ld, g.rows, g.rows_elig, g.ncols,
+                                                   g.row_first,
                                                    basis_in, basis_out, pp, g.ntiles, st, colq,
                                                    partials, cand_out, nranks, tol_dj, tol_piv,
                                                    pricing, log, log_cap);
@@ -759,9 +861,43 @@ hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* bas
 
 hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32_t* basis,
                          DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
-                         hipStream_t s) {
+                         hipStream_t s, bool forced) {
     select_kernel<<<1, 64, 0, s>>>(cands, nranks, basis, st, g.row_first, g.rows, pricing, log,
-                                   log_cap);
+                                   log_cap, forced ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_drive(const Geometry& g, int64_t row, int32_t* basis, DevState* st,
+                        double tol_piv, Cand* cand_out, int nranks, int pricing, dlp_pivot* log,
+                        int64_t log_cap, double* colq, hipStream_t s) {
+    drive_kernel<<<1, kRatioThreads, 0, s>>>(g.T, g.ld, g.rows_elig, g.row_first, g.nprice, row,
+                                             basis, st, tol_piv, cand_out, nranks, pricing, log,
+                                             log_cap, g.rows);
+    if (nranks == 1) return launch_gather_q(g, st, colq, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_q(const Geometry& g, const DevState* st, double* colq, hipStream_t s) {
+    const int64_t blocks = (g.rows + 1 + 255) / 256;
+    gather_q_kernel<<<(unsigned)blocks, 256, 0, s>>>(g.T, g.ld, g.rows, st, colq);
+    return hipGetLastError();
+}
+
+hipError_t launch_carry_out(const Geometry& g, int64_t carry_local, int64_t* out, hipStream_t s) {
+    const int blocks = (int)((g.ld + kProwThreads - 1) / kProwThreads);
+    carry_out_kernel<<<blocks, kProwThreads, 0, s>>>(g.T, g.ld, carry_local, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_carry_in(const Geometry& g, const int64_t* in, DevState* st, int pricing,
+                           hipStream_t s) {
+    const int blocks = (int)((g.ld + kProwThreads - 1) / kProwThreads);
+    carry_in_kernel<<<blocks, kProwThreads, 0, s>>>(g.T, g.ld, g.rows, in, st, pricing);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_status(DevState* st, int status, hipStream_t s) {
+    set_status_kernel<<<1, 64, 0, s>>>(st, status);
     return hipGetLastError();
 }
 
@@ -782,7 +918,8 @@ static void upd(const Geometry& g, const double* colq, const double* prow, const
     const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
     dim3 grid(ntiles, (unsigned)bands);
     update_kernel<NT, U, VEC, LDSQ><<<grid, kUpdThreads, 0, s>>>(
-        g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
+        g.T, g.ld, g.rows, g.ncols, g.nprice, colq, prow, st, pp, g.rows_per_block, tol_dj,
+        log, log_cap);
 }
 
 template <bool NT, int U, int THREADS>
@@ -793,7 +930,8 @@ static void updf(const Geometry& g, const double* colq, const double* prow, cons
     const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
     dim3 grid(ntiles, (unsigned)bands);
     update_fast_kernel<NT, U, THREADS><<<grid, THREADS, 0, s>>>(
-        g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
+        g.T, g.ld, g.rows, g.ncols, g.nprice, colq, prow, st, pp, g.rows_per_block, tol_dj,
+        log, log_cap);
 }
 
 template <bool NT, int DEPTH, int VEC>
@@ -804,7 +942,8 @@ static void upds(const Geometry& g, const double* colq, const double* prow, cons
     const int64_t bands = (g.rows + 1 + g.rows_per_block - 1) / g.rows_per_block;
     dim3 grid(ntiles, (unsigned)bands);
     update_stream_kernel<NT, DEPTH, VEC><<<grid, kUpdThreads, 0, s>>>(
-        g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
+        g.T, g.ld, g.rows, g.ncols, g.nprice, colq, prow, st, pp, g.rows_per_block, tol_dj,
+        log, log_cap);
 }
 
 // OCC = workgroups per CU allowed by a dynamic-LDS reservation (0 = no cap).
@@ -818,7 +957,8 @@ static void updr(const Geometry& g, const double* colq, const double* prow, cons
     // static LDS is ~2.2 KB; reserve the rest so that only OCC workgroups fit in 160 KiB
     const size_t dyn = OCC > 0 ? (size_t)(160 * 1024 / OCC) - 4096 : 0;
     update_serial_kernel<NT, VEC><<<grid, kUpdThreads, dyn, s>>>(
-        g.T, g.ld, g.rows, g.ncols, colq, prow, st, pp, g.rows_per_block, tol_dj, log, log_cap);
+        g.T, g.ld, g.rows, g.ncols, g.nprice, colq, prow, st, pp, g.rows_per_block, tol_dj,
+        log, log_cap);
 }
 
 template <bool NT>

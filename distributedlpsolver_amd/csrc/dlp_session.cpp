@@ -90,6 +90,19 @@ struct dlp_session {
     int64_t graph_chunk = 0;
     // problem copy for results
     dlp_problem prob_dims{};
+    // general LPs (two-phase): phase 1 / 2, the carried Phase II objective row
+    // (local index, -1 elsewhere), artificial drive-out queue, caller-driven step kind
+    bool general = false;
+    int phase = 2;
+    int64_t carry_local = -1;
+    int64_t nprice = 0;
+    double bmax = 0.0;
+    std::vector<int32_t> drive;
+    size_t drive_next = 0;
+    bool carry_pending = false;
+    int64_t phase1_pivots = 0;
+    enum StepKind { STEP_PIVOT, STEP_FORCED, STEP_CARRY } step_kind = STEP_PIVOT;
+    bool step_void = false;
 };
 
 namespace {
@@ -98,11 +111,47 @@ int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
 
 int auto_rows_per_block(const dlp_session* s) { return s->streaming ? 8 : 4; }
 
-// Host build of a tableau slice (dense / ad-allocation problems).
+// Row i of a general LP's standard-form tableau (include/dlp.h, "general LPs").
+void std_row(const dlp::StdForm& f, int64_t i, double* r) {
+    std::memcpy(r, f.A.data() + i * f.ns, sizeof(double) * f.ns);
+    if (f.slack_col[i] >= 0) r[f.slack_col[i]] = f.type[i] == dlp::ROW_G ? -1.0 : 1.0;
+    if (f.art_col[i] >= 0) r[f.art_col[i]] = 1.0;
+    r[f.ncols()] = f.b[i];
+}
+
+// Host build of a tableau slice (dense / ad-allocation / general problems).
+// General LPs with artificials: `rows` includes the carried Phase II
+// objective row at local index carry_local (>= 0 on the last rank only).
 void host_tableau(const dlp_problem* p, int64_t row_first, int64_t rows, int64_t ld,
-                  std::vector<double>& T) {
+                  std::vector<double>& T, int64_t carry_local = -1) {
     const int64_t m = p->m, n = p->n, N = n + m;
     T.assign((size_t)(rows + 1) * ld, 0.0);
+    if (p->kind == dlp::PROB_GENERAL) {
+        const dlp::StdForm& f = p->sf;
+        const int64_t NG = f.ncols();
+        for (int64_t il = 0; il < rows; ++il) {
+            double* r = T.data() + il * ld;
+            if (il == carry_local) {
+                for (int64_t j = 0; j < f.ns; ++j) r[j] = -f.c[j];
+            } else {
+                std_row(f, row_first + il, r);
+            }
+        }
+        double* z = T.data() + rows * ld;
+        if (f.nart == 0) {
+            for (int64_t j = 0; j < f.ns; ++j) z[j] = -f.c[j];
+        } else {   // Phase I: z_j = fold over artificial rows ascending of (z_j - T[i][j])
+            std::vector<double> r(NG + 1);
+            for (int64_t i = 0; i < f.m; ++i) {
+                if (f.art_col[i] < 0) continue;
+                std::fill(r.begin(), r.end(), 0.0);
+                std_row(f, i, r.data());
+                for (int64_t j = 0; j < f.nprice(); ++j) z[j] = z[j] - r[j];
+                z[NG] = z[NG] - r[NG];
+            }
+        }
+        return;
+    }
     if (p->kind == dlp::PROB_DENSE) {
         for (int64_t il = 0; il < rows; ++il) {
             const int64_t i = row_first + il;
@@ -156,7 +205,8 @@ int validate_options(const dlp_options* o) {
         set_error("unknown pricing rule");
         return DLP_ERR_ARG;
     }
-    if (!(o->tol_dj >= 0.0) || !(o->tol_piv >= 0.0) || o->max_pivots < 0 || o->check_interval <= 0) {
+    if (!(o->tol_dj >= 0.0) || !(o->tol_piv >= 0.0) || !(o->tol_feas >= 0.0) || o->max_pivots < 0 ||
+        o->check_interval <= 0) {
         set_error("invalid tolerance / pivot limit / check interval");
         return DLP_ERR_ARG;
     }
@@ -172,8 +222,23 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     s->m = prob->m;
     s->n = prob->n;
     s->N = prob->n + prob->m;
+    s->nprice = s->N;
+    s->general = prob->kind == dlp::PROB_GENERAL;
+    if (s->general) {   // standard-form dimensions; the carried row goes to the last rank
+        s->m = prob->sf.m;
+        s->n = prob->sf.ns;
+        s->N = prob->sf.ncols();
+        s->nprice = prob->sf.nprice();
+        s->phase = prob->sf.nart > 0 ? 1 : 2;
+        for (double v : prob->sf.b) s->bmax = std::max(s->bmax, v);
+    }
     s->width = round16(s->N + 1);
     CALL_TRY(dlp_rank_rows(s->m, rank, nranks, &s->row_first, &s->rows));
+    int64_t rows_elig = s->rows;
+    if (s->phase == 1 && rank == nranks - 1) {
+        s->carry_local = s->rows;
+        s->rows += 1;
+    }
     // "auto" tuning (negative / zero option values), from the interleaved A/B
     // sweeps of tools/tune_update.py on MI355X (update kernel):
     //  - tableaus far beyond the 256 MiB Infinity Cache stream from HBM: the
@@ -195,6 +260,12 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     opt = &s->opt;
     s->prob_dims.m = prob->m;
     s->prob_dims.n = prob->n;
+    s->prob_dims.kind = prob->kind;
+    if (s->general) {   // back-mapping for results (the matrix itself is not kept)
+        s->prob_dims.sf = prob->sf;
+        s->prob_dims.sf.A.clear();
+        s->prob_dims.sf.A.shrink_to_fit();
+    }
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -212,6 +283,8 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     g.rows = s->rows;
     g.row_first = s->row_first;
     g.ncols = s->N;
+    g.nprice = s->nprice;
+    g.rows_elig = rows_elig;
     if (opt->update_variant < 0 || opt->update_variant >= dlp::update_variants()) {
         set_error("update_variant out of range");
         return DLP_ERR_ARG;
@@ -251,12 +324,14 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         HIP_TRY(dlp::launch_generate(g, prob->gen_kind, s->m, s->n, prob->seed, s->stream));
     } else {
         std::vector<double> host;
-        host_tableau(prob, s->row_first, s->rows, s->ld, host);
+        host_tableau(prob, s->row_first, s->rows, s->ld, host, s->carry_local);
         HIP_TRY(hipMemcpyAsync(s->T, host.data(), tbytes, hipMemcpyHostToDevice, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
     }
     std::vector<int32_t> basis(s->m);
-    for (int64_t i = 0; i < s->m; ++i) basis[i] = (int32_t)(s->n + i);
+    for (int64_t i = 0; i < s->m; ++i)
+        basis[i] = s->general ? (prob->sf.art_col[i] >= 0 ? prob->sf.art_col[i] : prob->sf.slack_col[i])
+                              : (int32_t)(s->n + i);
     HIP_TRY(hipMemcpyAsync(s->basis, basis.data(), sizeof(int32_t) * s->m, hipMemcpyHostToDevice,
                            s->stream));
     dlp::DevState st0{};
@@ -337,6 +412,92 @@ int enqueue_pivot(dlp_session* s, int64_t slot) {
     return DLP_OK;
 }
 
+// General LPs: forced drive-out pivot on global row `row` (same exchange shape
+// as a pivot: candidate all-gather, pivot-row MAX all-reduce).
+int enqueue_forced_candidate(dlp_session* s, int64_t row) {
+    const dlp_options& o = s->opt;
+    HIP_TRY(dlp::launch_drive(s->g, row, s->basis, s->st, o.tol_piv, s->cand_send,
+                              s->exchange ? 2 : 1, o.pricing, s->log, s->log_cap, s->colq,
+                              s->stream));
+    return DLP_OK;
+}
+int enqueue_forced_select(dlp_session* s) {
+    if (s->exchange) {
+        HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, s->opt.pricing,
+                                   s->log, s->log_cap, s->stream, true));
+        HIP_TRY(dlp::launch_gather_q(s->g, s->st, s->colq, s->stream));
+    }
+    return enqueue_prow(s);
+}
+int enqueue_forced(dlp_session* s, int64_t row) {
+    CALL_TRY(enqueue_forced_candidate(s, row));
+    if (s->exchange)
+        NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
+                               s->stream));
+    CALL_TRY(enqueue_forced_select(s));
+    if (s->exchange)
+        NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
+                               s->comm, s->stream));
+    return enqueue_update(s);
+}
+// Carried Phase II objective row -> objective row on every rank.
+int enqueue_carry_out(dlp_session* s) {
+    HIP_TRY(dlp::launch_carry_out(s->g, s->carry_local, s->prow_send, s->stream));
+    return DLP_OK;
+}
+int enqueue_carry_in(dlp_session* s) {
+    HIP_TRY(dlp::launch_carry_in(s->g, s->prow_recv, s->st, s->opt.pricing, s->stream));
+    HIP_TRY(dlp::launch_price_init(s->g, s->pp, s->opt.tol_dj, s->opt.update_variant, s->stream));
+    return DLP_OK;
+}
+int enqueue_carry(dlp_session* s) {
+    CALL_TRY(enqueue_carry_out(s));
+    if (s->exchange)
+        NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
+                               s->comm, s->stream));
+    return enqueue_carry_in(s);
+}
+
+int poll(dlp_session* s);
+
+// Phase I optimum reached (device status "optimal" in phase 1): decide
+// infeasibility from the Phase I objective, queue the drive-out pivots of the
+// rows whose basic variable is artificial (replicated basis: every rank
+// queues the same rows) and the carried-row switch.
+int begin_phase2(dlp_session* s) {
+    double zN = 0.0;
+    std::vector<int32_t> basis(s->m);
+    HIP_TRY(hipMemcpyAsync(&zN, s->T + s->rows * s->ld + s->N, sizeof(double),
+                           hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(basis.data(), s->basis, sizeof(int32_t) * s->m, hipMemcpyDeviceToHost,
+                           s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->phase1_pivots = s->npivots;
+    s->step_void = true;   // a caller-driven step begun in Phase I is void
+    if (zN < -s->opt.tol_feas * (1.0 + s->bmax)) {
+        s->status = DLP_INFEASIBLE;
+        s->phase = 3;
+        return DLP_OK;
+    }
+    s->drive.clear();
+    for (int64_t i = 0; i < s->m; ++i)
+        if (basis[i] >= s->nprice) s->drive.push_back((int32_t)i);
+    s->drive_next = 0;
+    s->carry_pending = true;
+    s->phase = 2;
+    s->status = DLP_RUNNING;
+    HIP_TRY(dlp::launch_set_status(s->st, DLP_RUNNING, s->stream));
+    return DLP_OK;
+}
+
+// After the carry-in: the Phase I pivot count (drive-out included) is final.
+int finish_phase1(dlp_session* s) {
+    s->carry_pending = false;
+    CALL_TRY(poll(s));
+    s->phase1_pivots = s->npivots;
+    return DLP_OK;
+}
+
 // Sync, read the device state, fold event timings of pivots that really ran.
 int poll(dlp_session* s) {
     const int64_t before = s->npivots;
@@ -344,7 +505,9 @@ int poll(dlp_session* s) {
                            s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     s->npivots = s->host_st->npivots;
-    if (s->host_st->status != DLP_RUNNING) s->status = s->host_st->status;
+    if (s->host_st->status != DLP_RUNNING && s->host_st->status != dlp::kStatusSkip &&
+        s->status == DLP_RUNNING)
+        s->status = s->host_st->status;
     if (s->ev_per_pivot && s->ev_pending > 0) {
         const int64_t real = std::min<int64_t>(s->ev_pending, s->npivots - before);
         for (int64_t k = 0; k < real; ++k) {
@@ -363,6 +526,7 @@ int poll(dlp_session* s) {
         s->nsamples += real;
     }
     s->ev_pending = 0;
+    if (s->general && s->phase == 1 && s->status == DLP_OK) CALL_TRY(begin_phase2(s));
     return DLP_OK;
 }
 
@@ -382,6 +546,45 @@ int run_window_graph(dlp_session* s, int64_t chunk) {
         s->graph_chunk = chunk;
     }
     HIP_TRY(hipGraphLaunch(s->gexec, s->stream));
+    return DLP_OK;
+}
+
+// General LP results in user terms (include/dlp.h, "general LPs": results).
+// Before Phase II has started (infeasible, or a pivot limit in Phase I) the
+// objective is NaN and y is zero; x is the current (Phase I) point.
+int general_result(dlp_session* s, const std::vector<double>& z, const std::vector<double>& rhs,
+                   dlp_result* r) {
+    const dlp::StdForm& f = s->prob_dims.sf;
+    const int64_t mu = s->prob_dims.m, nu = s->prob_dims.n;
+    r->m = mu;
+    r->n = nu;
+    r->phase1_pivots = s->phase == 1 ? s->npivots : s->phase1_pivots;
+    std::vector<double> xs(f.ns, 0.0);
+    for (int64_t il = 0; il < s->g.rows_elig; ++il) {
+        const int32_t v = r->basis[s->row_first + il];
+        if (v < f.ns) xs[v] = rhs[il];
+    }
+    r->x.resize(nu);
+    for (int64_t j = 0; j < nu; ++j) {
+        const int32_t k = f.var_col[j];
+        switch (f.var_kind[j]) {
+            case dlp::VAR_LO: r->x[j] = f.var_const[j] + xs[k]; break;
+            case dlp::VAR_HI: r->x[j] = f.var_const[j] - xs[k]; break;
+            default: r->x[j] = xs[k] - xs[k + 1]; break;
+        }
+    }
+    r->y.assign(mu, 0.0);
+    const bool phase2 = s->phase == 2 && !s->carry_pending;
+    if (!phase2) {
+        r->objective = NAN;
+        return DLP_OK;
+    }
+    r->objective = f.obj_sign * z[s->N] + f.obj_const;
+    for (int64_t i = 0; i < f.m; ++i) {
+        if (f.user_row[i] < 0) continue;
+        const int32_t ident = f.type[i] == dlp::ROW_L ? f.slack_col[i] : f.art_col[i];
+        r->y[f.user_row[i]] += f.obj_sign * f.row_sign[i] * z[ident];
+    }
     return DLP_OK;
 }
 
@@ -409,15 +612,17 @@ int extract_result(dlp_session* s, dlp_result* r) {
         HIP_TRY(hipMemcpyAsync(r->log.data(), s->log, sizeof(dlp_pivot) * nlog,
                                hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) r->timings[ph] = s->timings[ph];
+    const int64_t rows_elig = s->g.rows_elig;
+    if (s->general) return general_result(s, z, rhs, r);
     r->objective = z[s->N];
     r->x.assign(s->n, 0.0);
-    for (int64_t il = 0; il < s->rows; ++il) {
+    for (int64_t il = 0; il < rows_elig; ++il) {
         const int32_t v = r->basis[s->row_first + il];
         if (v < s->n) r->x[v] = rhs[il];
     }
     r->y.resize(s->m);
     for (int64_t i = 0; i < s->m; ++i) r->y[i] = z[s->n + i];
-    for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) r->timings[ph] = s->timings[ph];
     return DLP_OK;
 }
 
@@ -442,6 +647,7 @@ void dlp_options_default(dlp_options* o) {
     o->use_graph = 1;
     o->update_variant = -1;   // auto
     o->ld_align = 0;          // auto
+    o->tol_feas = 1e-9;
 }
 
 const char* dlp_status_string(int st) {
@@ -563,6 +769,122 @@ int dlp_problem_create_adalloc(int num_advertisers, int num_impressions, int num
     return DLP_OK;
 }
 
+int dlp_problem_create_general(int64_t m, int64_t n, const double* A, const double* row_lo,
+                               const double* row_hi, const double* col_lo, const double* col_hi,
+                               const double* c, double c0, int sense, dlp_problem** out) {
+    if (!out || m < 0 || n <= 0 || (m > 0 && (!A || !row_lo || !row_hi)) || !col_lo || !col_hi ||
+        !c || (sense != DLP_MINIMIZE && sense != DLP_MAXIMIZE) || std::isnan(c0)) {
+        set_error("dlp_problem_create_general: bad arguments");
+        return DLP_ERR_ARG;
+    }
+    for (int64_t j = 0; j < n; ++j)
+        if (std::isnan(c[j]) || std::isinf(c[j])) {
+            set_error("dlp_problem_create_general: c must be finite");
+            return DLP_ERR_ARG;
+        }
+    auto* p = new (std::nothrow) dlp_problem();
+    if (!p) return DLP_ERR_OOM;
+    try {
+        dlp::General& g = p->gen;
+        g.m = m;
+        g.n = n;
+        if (m > 0) {
+            g.A.assign(A, A + m * n);
+            g.row_lo.assign(row_lo, row_lo + m);
+            g.row_hi.assign(row_hi, row_hi + m);
+        }
+        g.col_lo.assign(col_lo, col_lo + n);
+        g.col_hi.assign(col_hi, col_hi + n);
+        g.c.assign(c, c + n);
+        g.c0 = c0;
+        g.sense = sense;
+        const int rc = dlp::build_stdform(g, &p->sf);
+        if (rc != DLP_OK) {
+            delete p;
+            return rc;
+        }
+    } catch (const std::bad_alloc&) {
+        delete p;
+        set_error("dlp_problem_create_general: out of host memory");
+        return DLP_ERR_OOM;
+    }
+    p->kind = dlp::PROB_GENERAL;
+    p->m = m;
+    p->n = n;
+    *out = p;
+    return DLP_OK;
+}
+
+int dlp_problem_create_mps(const char* path, dlp_problem** out) {
+    if (!path || !out) {
+        set_error("dlp_problem_create_mps: bad arguments");
+        return DLP_ERR_ARG;
+    }
+    dlp::General g;
+    try {
+        CALL_TRY(dlp::parse_mps(path, &g));
+    } catch (const std::bad_alloc&) {
+        set_error("dlp_problem_create_mps: out of host memory");
+        return DLP_ERR_OOM;
+    }
+    return dlp_problem_create_general(g.m, g.n, g.A.data(), g.row_lo.data(), g.row_hi.data(),
+                                      g.col_lo.data(), g.col_hi.data(), g.c.data(), g.c0, g.sense,
+                                      out);
+}
+
+int dlp_problem_get_general(const dlp_problem* p, double* A, double* row_lo, double* row_hi,
+                            double* col_lo, double* col_hi, double* c, double* c0, int* sense) {
+    if (!p) return DLP_ERR_ARG;
+    if (p->kind == dlp::PROB_RANDOM) {
+        set_error("random problems are generated on the device; use dlp_session_tableau");
+        return DLP_ERR_UNSUPPORTED;
+    }
+    const int64_t m = p->m, n = p->n;
+    if (p->kind == dlp::PROB_GENERAL) {
+        const dlp::General& g = p->gen;
+        if (A && m > 0) std::memcpy(A, g.A.data(), sizeof(double) * m * n);
+        if (row_lo && m > 0) std::memcpy(row_lo, g.row_lo.data(), sizeof(double) * m);
+        if (row_hi && m > 0) std::memcpy(row_hi, g.row_hi.data(), sizeof(double) * m);
+        if (col_lo) std::memcpy(col_lo, g.col_lo.data(), sizeof(double) * n);
+        if (col_hi) std::memcpy(col_hi, g.col_hi.data(), sizeof(double) * n);
+        if (c) std::memcpy(c, g.c.data(), sizeof(double) * n);
+        if (c0) *c0 = g.c0;
+        if (sense) *sense = g.sense;
+        return DLP_OK;
+    }
+    // dense / ad-allocation: max c^T x, A x <= b, x >= 0
+    std::vector<double> b(m);
+    CALL_TRY(dlp_problem_get_dense(p, A, b.data(), c));
+    for (int64_t i = 0; i < m; ++i) {
+        if (row_lo) row_lo[i] = -HUGE_VAL;
+        if (row_hi) row_hi[i] = b[i];
+    }
+    for (int64_t j = 0; j < n; ++j) {
+        if (col_lo) col_lo[j] = 0.0;
+        if (col_hi) col_hi[j] = HUGE_VAL;
+    }
+    if (c0) *c0 = 0.0;
+    if (sense) *sense = DLP_MAXIMIZE;
+    return DLP_OK;
+}
+
+int dlp_problem_std_dims(const dlp_problem* p, int64_t* m_std, int64_t* ncols, int64_t* nprice,
+                         int64_t* nart) {
+    if (!p) return DLP_ERR_ARG;
+    if (p->kind == dlp::PROB_GENERAL) {
+        if (m_std) *m_std = p->sf.m;
+        if (ncols) *ncols = p->sf.ncols();
+        if (nprice) *nprice = p->sf.nprice();
+        if (nart) *nart = p->sf.nart;
+    } else {
+        if (m_std) *m_std = p->m;
+        if (ncols) *ncols = p->m + p->n;
+        if (nprice) *nprice = p->m + p->n;
+        if (nart) *nart = 0;
+    }
+    return DLP_OK;
+}
+
 int dlp_problem_dims(const dlp_problem* p, int64_t* m, int64_t* n) {
     if (!p) return DLP_ERR_ARG;
     if (m) *m = p->m;
@@ -572,6 +894,10 @@ int dlp_problem_dims(const dlp_problem* p, int64_t* m, int64_t* n) {
 
 int dlp_problem_get_dense(const dlp_problem* p, double* A, double* b, double* c) {
     if (!p) return DLP_ERR_ARG;
+    if (p->kind == dlp::PROB_GENERAL) {
+        set_error("general LPs have row / column bounds: use dlp_problem_get_general");
+        return DLP_ERR_UNSUPPORTED;
+    }
     if (p->kind == dlp::PROB_RANDOM) {
         set_error("random problems are generated on the device; use dlp_session_tableau");
         return DLP_ERR_UNSUPPORTED;
@@ -648,6 +974,20 @@ int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
     int64_t budget = std::min<int64_t>(max_pivots, s->opt.max_pivots - s->launched);
     const bool graph = s->opt.use_graph && !s->exchange && s->ev_per_pivot == 0;
     while (s->status == DLP_RUNNING && budget > 0) {
+        if (s->drive_next < s->drive.size() || s->carry_pending) {   // Phase I -> II switch
+            while (s->drive_next < s->drive.size() && budget > 0) {
+                CALL_TRY(enqueue_forced(s, s->drive[s->drive_next++]));
+                s->launched += 1;
+                budget -= 1;
+            }
+            if (s->drive_next == s->drive.size() && s->carry_pending) {
+                CALL_TRY(enqueue_carry(s));
+                CALL_TRY(finish_phase1(s));
+            } else {
+                CALL_TRY(poll(s));
+            }
+            continue;
+        }
         const int64_t chunk = std::min<int64_t>(budget, s->opt.check_interval);
         if (graph && chunk == s->opt.check_interval) {
             CALL_TRY(run_window_graph(s, chunk));
@@ -665,15 +1005,35 @@ int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
     return DLP_RUNNING;
 }
 
+// Caller-driven steps.  A general LP's Phase I -> II switch is carried by the
+// same three-step exchange: forced drive-out pivots, then one carry step
+// (its candidate is an empty slot, its "pivot row" the carried objective row).
 int dlp_session_step_candidate(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
+    s->step_void = false;
+    if (s->drive_next < s->drive.size()) {
+        s->step_kind = dlp_session::STEP_FORCED;
+        return enqueue_forced_candidate(s, s->drive[s->drive_next++]);
+    }
+    if (s->carry_pending) {
+        s->step_kind = dlp_session::STEP_CARRY;
+        HIP_TRY(hipMemsetAsync(s->cand_send, 0, sizeof(dlp::Cand), s->stream));
+        return DLP_OK;
+    }
+    s->step_kind = dlp_session::STEP_PIVOT;
     return enqueue_candidate(s);
 }
 
 int dlp_session_step_select(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
+    if (s->step_void) return DLP_OK;
+    switch (s->step_kind) {
+        case dlp_session::STEP_FORCED: return enqueue_forced_select(s);
+        case dlp_session::STEP_CARRY: return enqueue_carry_out(s);
+        default: break;
+    }
     CALL_TRY(enqueue_select(s));
     return enqueue_prow(s);
 }
@@ -681,6 +1041,11 @@ int dlp_session_step_select(dlp_session* s) {
 int dlp_session_step_update(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
+    if (s->step_void) return DLP_OK;
+    if (s->step_kind == dlp_session::STEP_CARRY) {
+        CALL_TRY(enqueue_carry_in(s));
+        return finish_phase1(s);
+    }
     CALL_TRY(enqueue_update(s));
     s->launched += 1;
     return DLP_OK;
@@ -855,8 +1220,14 @@ int dlp_result_y(const dlp_result* r, double* y, int64_t m) {
     return DLP_OK;
 }
 int dlp_result_basis(const dlp_result* r, int32_t* basis, int64_t m) {
-    if (!r || !basis || m != r->m) return DLP_ERR_ARG;
+    if (!r || !basis || m != (int64_t)r->basis.size()) return DLP_ERR_ARG;
     std::memcpy(basis, r->basis.data(), sizeof(int32_t) * m);
+    return DLP_OK;
+}
+int dlp_result_info(const dlp_result* r, int64_t* m_basis, int64_t* phase1_pivots) {
+    if (!r) return DLP_ERR_ARG;
+    if (m_basis) *m_basis = (int64_t)r->basis.size();
+    if (phase1_pivots) *phase1_pivots = r->phase1_pivots;
     return DLP_OK;
 }
 int dlp_result_pivot_log(const dlp_result* r, dlp_pivot* log, int64_t cap, int64_t* count) {

@@ -30,7 +30,10 @@ def _dptr(a: np.ndarray):
 
 
 class Problem:
-    """An LP  max c^T x  s.t.  A x <= b, x >= 0 (b >= 0), owned by libdlp."""
+    """An LP owned by libdlp: dense / random / ad-allocation problems are
+    max c^T x s.t. A x <= b, x >= 0 (b >= 0); general problems
+    (``Problem.general`` / ``Problem.mps``) have row and column bounds and are
+    solved in two phases (include/dlp.h, "general LPs")."""
 
     def __init__(self, handle: int, kind: str):
         self._h = C.c_void_p(handle)
@@ -71,6 +74,54 @@ class Problem:
         p = cls(h.value, "adalloc")
         p.num_advertisers, p.num_impressions = num_advertisers, num_impressions
         return p
+
+    @classmethod
+    def general(cls, A, row_lo, row_hi, col_lo, col_hi, c, c0: float = 0.0,
+                sense: int = L.MINIMIZE) -> "Problem":
+        """min (sense=MINIMIZE) or max c^T x + c0 s.t. row_lo <= A x <= row_hi,
+        col_lo <= x <= col_hi; +-inf (or |v| >= 1e30) for missing bounds."""
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        n = c.shape[0]
+        row_lo = np.ascontiguousarray(row_lo, dtype=np.float64)
+        row_hi = np.ascontiguousarray(row_hi, dtype=np.float64)
+        m = row_lo.shape[0]
+        A = np.ascontiguousarray(np.asarray(A, dtype=np.float64).reshape(m, n))
+        col_lo = np.ascontiguousarray(np.broadcast_to(np.asarray(col_lo, np.float64), (n,)))
+        col_hi = np.ascontiguousarray(np.broadcast_to(np.asarray(col_hi, np.float64), (n,)))
+        if row_hi.shape != (m,):
+            raise ValueError("row_lo / row_hi must have one entry per row of A")
+        h = C.c_void_p()
+        L.check(L.lib().dlp_problem_create_general(m, n, _dptr(A), _dptr(row_lo), _dptr(row_hi),
+                                                   _dptr(col_lo), _dptr(col_hi), _dptr(c),
+                                                   float(c0), int(sense), C.byref(h)),
+                "dlp_problem_create_general")
+        return cls(h.value, "general")
+
+    @classmethod
+    def mps(cls, path: str) -> "Problem":
+        """Load a free- or fixed-format MPS file (dlp_problem_create_mps)."""
+        h = C.c_void_p()
+        L.check(L.lib().dlp_problem_create_mps(str(path).encode(), C.byref(h)),
+                "dlp_problem_create_mps")
+        return cls(h.value, "general")
+
+    def to_general(self):
+        """(A, row_lo, row_hi, col_lo, col_hi, c, c0, sense) of this problem."""
+        m, n = self.m, self.n
+        A, rl, rh = np.zeros((m, n)), np.zeros(m), np.zeros(m)
+        cl, ch, c = np.zeros(n), np.zeros(n), np.zeros(n)
+        c0, sense = C.c_double(), C.c_int()
+        L.check(L.lib().dlp_problem_get_general(self._h, _dptr(A), _dptr(rl), _dptr(rh), _dptr(cl),
+                                                _dptr(ch), _dptr(c), C.byref(c0), C.byref(sense)),
+                "dlp_problem_get_general")
+        return A, rl, rh, cl, ch, c, c0.value, sense.value
+
+    def std_dims(self):
+        """(standard-form rows, tableau columns, priced columns, artificial columns)."""
+        v = [C.c_int64() for _ in range(4)]
+        L.check(L.lib().dlp_problem_std_dims(self._h, *[C.byref(x) for x in v]),
+                "dlp_problem_std_dims")
+        return tuple(x.value for x in v)
 
     def to_dense(self):
         A = np.zeros((self.m, self.n))
@@ -114,6 +165,7 @@ class Result:
     basis: np.ndarray
     pivot_log: np.ndarray
     timings_ms: np.ndarray = field(default_factory=lambda: np.zeros(4))
+    phase1_pivots: int = 0
 
     @property
     def status_name(self) -> str:
@@ -125,10 +177,12 @@ def _result_from_handle(h: C.c_void_p, m: int, n: int) -> Result:
     try:
         x = np.zeros(n)
         y = np.zeros(m)
-        basis = np.zeros(m, np.int32)
+        mb, p1 = C.c_int64(), C.c_int64()
+        L.check(lib.dlp_result_info(h, C.byref(mb), C.byref(p1)), "dlp_result_info")
+        basis = np.zeros(mb.value, np.int32)
         L.check(lib.dlp_result_x(h, _dptr(x), n), "dlp_result_x")
         L.check(lib.dlp_result_y(h, _dptr(y), m), "dlp_result_y")
-        L.check(lib.dlp_result_basis(h, basis.ctypes.data_as(C.POINTER(C.c_int32)), m),
+        L.check(lib.dlp_result_basis(h, basis.ctypes.data_as(C.POINTER(C.c_int32)), mb.value),
                 "dlp_result_basis")
         cnt = C.c_int64()
         L.check(lib.dlp_result_pivot_log(h, None, 0, C.byref(cnt)), "dlp_result_pivot_log")
@@ -140,7 +194,7 @@ def _result_from_handle(h: C.c_void_p, m: int, n: int) -> Result:
         L.check(lib.dlp_result_timings(h, _dptr(tm)), "dlp_result_timings")
         return Result(status=lib.dlp_result_status(h), objective=lib.dlp_result_objective(h),
                       num_pivots=lib.dlp_result_num_pivots(h), x=x, y=y, basis=basis,
-                      pivot_log=log, timings_ms=tm)
+                      pivot_log=log, timings_ms=tm, phase1_pivots=p1.value)
     finally:
         lib.dlp_result_free(h)
 
@@ -179,7 +233,8 @@ class Session:
     def run(self, max_pivots: int) -> tuple[int, int]:
         done = C.c_int64()
         st = L.lib().dlp_session_run(self._h, max_pivots, C.byref(done))
-        L.check(st, "dlp_session_run", ok=(L.OK, L.UNBOUNDED, L.PIVOT_LIMIT, L.RUNNING))
+        L.check(st, "dlp_session_run",
+                ok=(L.OK, L.INFEASIBLE, L.UNBOUNDED, L.PIVOT_LIMIT, L.RUNNING))
         return st, done.value
 
     # caller-driven exchange (host-side communicators, see rowblock.py)

@@ -60,7 +60,7 @@ extern "C" {
 
 /* ---- status codes ---------------------------------------------------- */
 #define DLP_OK              0   /* optimal (or the step/run completed) */
-#define DLP_INFEASIBLE      1
+#define DLP_INFEASIBLE      1   /* general LPs: Phase I ended with artificials > tol_feas */
 #define DLP_UNBOUNDED       2
 #define DLP_PIVOT_LIMIT     3
 #define DLP_RUNNING         4   /* session has pivots left to do */
@@ -133,6 +133,9 @@ typedef struct dlp_options {
     int32_t ld_align;        /* tableau row stride alignment in doubles, multiple of 16, 0 = auto
                                 (default: 512 when a row has >= 4096 columns, else 16); the
                                 kernels only touch the first roundup(N+1,16) columns */
+    int32_t pad_;
+    double  tol_feas;        /* general LPs: infeasible when the Phase I optimum is below
+                                -tol_feas * (1 + max_i b'_i) (default 1e-9) */
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
  * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;
@@ -160,6 +163,66 @@ int dlp_problem_create_random(int kind, int64_t m, int64_t n, uint64_t seed, dlp
  * max sum b_ai x_ai  s.t.  sum_i b_ai x_ai <= B_a (A rows),  sum_a x_ai <= 1 (I rows). */
 int dlp_problem_create_adalloc(int num_advertisers, int num_impressions, int num_slots,
                                double bid_sparsity, double scaling_factor, dlp_problem** out);
+/* ---- general LPs: row/column bounds + two-phase -------
+ *   minimise (sense = DLP_MINIMIZE) or maximise (DLP_MAXIMIZE)  c^T x + c0
+ *   s.t.  row_lo <= A x <= row_hi,  col_lo <= x <= col_hi,
+ * A dense m x n row-major; any bound may be infinite (|v| >= 1e30 counts as
+ * infinite).  No reference interface: the reference only builds its own
+ * ad-allocation LP in memory (R/instance.cpp:32-57).  Netlib-style inputs come
+ * through dlp_problem_create_mps.
+ *
+ * Canonical standard form (the rule spec; oracle/oracle.cpp restates it):
+ *  columns: user variable j in order -> lo finite: x_j = lo + x' (one column;
+ *           plus a bound row x' <= hi - lo when hi is finite); lo = -inf, hi
+ *           finite: x_j = hi - x' (column -A_j, cost -c_j); both infinite:
+ *           x_j = x'+ - x'- (two adjacent columns +A_j, -A_j).
+ *  rows:    user rows in order, then the bound rows in column order.  shift_i
+ *           = fma-chain over j ascending of A_ij * const_j (const = lo or hi).
+ *           lo == hi -> E row (rhs lo - shift); only hi finite -> L row; only lo
+ *           finite -> G row; both finite -> L row (hi) then G row (lo); both
+ *           infinite -> dropped.  A row with rhs < 0 is negated (L <-> G); a G
+ *           row with rhs == 0 is negated into an L row; rhs -0.0 becomes +0.0.
+ *  tableau: [structural | one slack (+1, L) / surplus (-1, G) column per L/G
+ *           row, in row order | one artificial (+1) column per G/E row, in row
+ *           order | RHS].  Pricing covers structural + slack/surplus columns
+ *           only (artificials never enter).  Basis: slack of L rows,
+ *           artificial of G/E rows.  Objective (max form) c' = -c for minimise.
+ *  phase I  (only when there are artificials): objective row z_j = sum over
+ *           artificial rows i ascending of (-T[i][j]) for every non-artificial
+ *           column j and the RHS (left fold from 0.0, z_j - T[i][j]); the
+ *           phase II objective (-c', 0 elsewhere) rides along as an extra
+ *           tableau row (global row m', owned by the last rank, never in the
+ *           ratio test).  Pivot rule exactly as above.  At the Phase I optimum:
+ *           infeasible if z_N < -tol_feas (1 + max b'); else every row whose
+ *           basic variable is artificial, ascending, is pivoted on its first
+ *           column q < n_price with |T[i][q]| > tol_piv (a logged pivot with
+ *           ratio 0; a row without one is redundant and keeps its artificial);
+ *           then the carried row becomes the objective row and Phase II runs
+ *           in the pricing mode of the options (Bland state reset).
+ *  results: x in user variables; y[i] = d(user objective)/d(bound of user row
+ *           i) (HiGHS / scipy "marginals" sign convention), summed over the
+ *           two rows of a ranged row; objective in the user's sense incl. c0. */
+#define DLP_MINIMIZE   1
+#define DLP_MAXIMIZE  -1
+int dlp_problem_create_general(int64_t m, int64_t n, const double* A, const double* row_lo,
+                               const double* row_hi, const double* col_lo, const double* col_hi,
+                               const double* c, double c0, int sense, dlp_problem** out);
+/* Free- or fixed-format MPS file (whitespace-separated fields; names without
+ * blanks): NAME, OBJSENSE (MIN/MAX), ROWS (N/L/G/E; the first N row is the
+ * objective, later N rows are dropped), COLUMNS (MARKER lines ignored: integer
+ * columns are relaxed; repeated entries are summed), RHS (an objective-row RHS
+ * v sets c0 = -v), RANGES (standard L/G/E semantics), BOUNDS (UP LO FX FR MI
+ * PL BV LI UI; UP < 0 with lower 0 sets lower = -inf), ENDATA. */
+int dlp_problem_create_mps(const char* path, dlp_problem** out);
+/* The general form of any non-random problem (arrays may be NULL). */
+int dlp_problem_get_general(const dlp_problem* prob, double* A, double* row_lo, double* row_hi,
+                            double* col_lo, double* col_hi, double* c, double* c0, int* sense);
+/* Standard-form sizes: constraint rows m' (the tableau adds the carried row
+ * when nart > 0), total columns N, priced columns, artificial columns.  For
+ * dense / random / ad-allocation problems: m' = m, N = n_price = n + m, 0. */
+int dlp_problem_std_dims(const dlp_problem* prob, int64_t* m_std, int64_t* ncols,
+                         int64_t* nprice, int64_t* nart);
+
 int dlp_problem_dims(const dlp_problem* prob, int64_t* m, int64_t* n);
 /* Dense copy of the problem data (A m x n row-major, b, c); NULL pointers skipped. */
 int dlp_problem_get_dense(const dlp_problem* prob, double* A, double* b, double* c);
@@ -267,10 +330,14 @@ void dlp_mw_free(dlp_mw* mw);
 int     dlp_result_status(const dlp_result* r);
 double  dlp_result_objective(const dlp_result* r);
 int64_t dlp_result_num_pivots(const dlp_result* r);
-/* x (n, this rank's basic rows only when nranks > 1), y (m, duals), basis (m). */
+/* x (n, this rank's basic rows only when nranks > 1), y (m, duals), basis
+ * (m_basis).  Dense problems: y_i = z_{n+i}, the max-form dual of row i. */
 int dlp_result_x(const dlp_result* r, double* x, int64_t n);
 int dlp_result_y(const dlp_result* r, double* y, int64_t m);
-int dlp_result_basis(const dlp_result* r, int32_t* basis, int64_t m);
+int dlp_result_basis(const dlp_result* r, int32_t* basis, int64_t m /* = m_basis */);
+/* m_basis: basis length (standard-form rows; m for dense problems);
+ * phase1_pivots: pivots of Phase I incl. the artificial drive-out (0 without). */
+int dlp_result_info(const dlp_result* r, int64_t* m_basis, int64_t* phase1_pivots);
 int dlp_result_pivot_log(const dlp_result* r, dlp_pivot* log, int64_t cap, int64_t* count);
 int dlp_result_timings(const dlp_result* r, double* ms_out /* DLP_NUM_PHASES */);
 void dlp_result_free(dlp_result* r);

@@ -73,6 +73,8 @@ inline int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
 struct Tab {
     int64_t m = 0, n = 0, N = 0, ld = 0;
     int64_t row_first = 0, rows = 0;      // local constraint rows; objective row is rows
+    int64_t nprice = 0;                   // priced columns [0, nprice)
+    int64_t rows_elig = 0;                // rows [0, rows_elig) enter the ratio test
     std::vector<double> T;                // (rows+1) x ld
     std::vector<int32_t> basis;           // global, m entries (replicated)
     std::vector<double> colq, prow;
@@ -88,6 +90,7 @@ struct Tab {
 void tab_init(Tab& t, int64_t m, int64_t n, int64_t row_first, int64_t rows, const oracle_opts* o) {
     t.m = m; t.n = n; t.N = n + m; t.ld = round16(t.N + 1);
     t.row_first = row_first; t.rows = rows;
+    t.nprice = t.N; t.rows_elig = rows;
     t.T.assign((size_t)(rows + 1) * t.ld, 0.0);
     t.basis.resize(m);
     for (int64_t i = 0; i < m; ++i) t.basis[i] = (int32_t)(n + i);   // slack basis
@@ -119,13 +122,13 @@ void tab_fill_dense(Tab& t, const double* A, const double* b, const double* c) {
 int32_t price(Tab& t) {
     const double* z = t.row(t.rows);
     if (t.bland) {
-        for (int64_t j = 0; j < t.N; ++j)
+        for (int64_t j = 0; j < t.nprice; ++j)
             if (z[j] < -t.tol_dj) return (int32_t)j;
         return -1;
     }
     double best = std::numeric_limits<double>::infinity();
     int64_t q = -1;
-    for (int64_t j = 0; j < t.N; ++j)
+    for (int64_t j = 0; j < t.nprice; ++j)
         if (z[j] < best) { best = z[j]; q = j; }
     if (q < 0 || !(best < -t.tol_dj)) return -1;
     return (int32_t)q;
@@ -145,7 +148,7 @@ oracle_cand local_ratio(Tab& t, int32_t q) {
     oracle_cand best{};
     best.valid = 0;
     for (int64_t il = 0; il <= t.rows; ++il) t.colq[il] = t.row(il)[q];
-    for (int64_t il = 0; il < t.rows; ++il) {
+    for (int64_t il = 0; il < t.rows_elig; ++il) {
         double a = t.colq[il];
         if (!(a > t.tol_piv)) continue;
         double rhs = t.row(il)[t.N];
@@ -216,6 +219,8 @@ int pivot_once(Tab& t) {
 }
 
 }  // namespace
+
+#include "oracle_general.inc"
 
 struct oracle_slice { Tab t; };
 

@@ -61,6 +61,20 @@ int oracle_solve_dense(int64_t m, int64_t n, const double* A, const double* b, c
                        int32_t* basis, oracle_pivot* log, int64_t log_cap, int64_t* npivots,
                        int* status);
 
+/* General LP (include/dlp.h "general LPs"; sense 1 = minimise, -1 = maximise):
+ * canonical standard form + two-phase simplex with the same rule.  Outputs in
+ * user terms; basis (standard-form rows, up to basis_cap); phase1 = pivots of
+ * Phase I incl. the drive-out.  Returns -7 when the LP has no constraint rows. */
+int oracle_general_std_dims(int64_t m, int64_t n, const double* A, const double* rl,
+                            const double* ru, const double* cl, const double* cu, const double* c,
+                            double c0, int sense, int64_t* m_std, int64_t* ncols, int64_t* nprice,
+                            int64_t* nart);
+int oracle_solve_general(int64_t m, int64_t n, const double* A, const double* rl, const double* ru,
+                         const double* cl, const double* cu, const double* c, double c0, int sense,
+                         const oracle_opts* opt, double tol_feas, double* x, double* y, double* obj,
+                         int32_t* basis, int64_t basis_cap, oracle_pivot* log, int64_t log_cap,
+                         int64_t* npivots, int64_t* phase1, int* status);
+
 /* Row-slice engine (one simulated rank) for multi-rank protocol tests. */
 typedef struct oracle_slice oracle_slice;
 int  oracle_slice_create(int64_t m, int64_t n, const double* A, const double* b, const double* c,

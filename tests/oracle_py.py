@@ -258,3 +258,67 @@ def run_generated(m, n, seed, k, rows, degenerate=False, nthreads=8):
                                     basis.ctypes.data_as(_I32))
     assert rc == 0
     return log[:npiv.value], out, basis
+
+
+# ---- general LPs (include/dlp.h "general LPs", oracle/oracle_general.inc)
+INF = float("inf")
+
+
+class GeneralLP:
+    """min/max c^T x + c0 s.t. row_lo <= A x <= row_hi, col_lo <= x <= col_hi (sense 1 = min)."""
+
+    def __init__(self, A, row_lo, row_hi, col_lo, col_hi, c, c0=0.0, sense=1):
+        self.A = np.ascontiguousarray(A, dtype=np.float64).reshape(len(row_lo), len(c))
+        self.row_lo = np.ascontiguousarray(row_lo, dtype=np.float64)
+        self.row_hi = np.ascontiguousarray(row_hi, dtype=np.float64)
+        self.col_lo = np.ascontiguousarray(col_lo, dtype=np.float64)
+        self.col_hi = np.ascontiguousarray(col_hi, dtype=np.float64)
+        self.c = np.ascontiguousarray(c, dtype=np.float64)
+        self.c0, self.sense = float(c0), int(sense)
+        self.m, self.n = self.A.shape
+
+    def args(self):
+        return (self.m, self.n, _d(self.A), _d(self.row_lo), _d(self.row_hi), _d(self.col_lo),
+                _d(self.col_hi), _d(self.c), self.c0, self.sense)
+
+
+def _bind_general(L):
+    if getattr(L, "_gen_bound", False):
+        return
+    base = [C.c_int64, C.c_int64, _D, _D, _D, _D, _D, _D, C.c_double, C.c_int]
+    L.oracle_general_std_dims.argtypes = base + [_I64, _I64, _I64, _I64]
+    L.oracle_solve_general.argtypes = base + [C.POINTER(Opts), C.c_double, _D, _D, _D, _I32,
+                                              C.c_int64, C.c_void_p, C.c_int64, _I64, _I64,
+                                              C.POINTER(C.c_int)]
+    L._gen_bound = True
+
+
+def general_std_dims(lp: GeneralLP):
+    L = lib()
+    _bind_general(L)
+    v = [C.c_int64() for _ in range(4)]
+    rc = L.oracle_general_std_dims(*lp.args(), *[C.byref(x) for x in v])
+    assert rc == 0, rc
+    return tuple(x.value for x in v)
+
+
+def solve_general(lp: GeneralLP, pricing=0, tol_dj=1e-9, tol_piv=1e-9, tol_feas=1e-9,
+                  max_pivots=1_000_000, nthreads=1, log_cap=200_000):
+    L = lib()
+    _bind_general(L)
+    m_std, _, _, _ = general_std_dims(lp)
+    o = Opts(pricing, tol_dj, tol_piv, max_pivots, nthreads)
+    x = np.zeros(lp.n)
+    y = np.zeros(lp.m)
+    obj = C.c_double()
+    basis = np.zeros(m_std, np.int32)
+    log = np.zeros(log_cap, PIVOT_DTYPE)
+    npiv, p1 = C.c_int64(), C.c_int64()
+    st = C.c_int()
+    rc = L.oracle_solve_general(*lp.args(), C.byref(o), tol_feas, _d(x), _d(y), C.byref(obj),
+                                basis.ctypes.data_as(_I32), m_std, log.ctypes.data, log_cap,
+                                C.byref(npiv), C.byref(p1), C.byref(st))
+    assert rc == 0, rc
+    return Solution(status=st.value, objective=obj.value, x=x, y=y, basis=basis,
+                    pivot_log=log[:min(npiv.value, log_cap)], num_pivots=npiv.value,
+                    phase1_pivots=p1.value)
