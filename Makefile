@@ -11,14 +11,14 @@ HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinc
              -Wall -Wno-unused-function
 LIBDLP    := $(PKG)/libdlp.so
 OBJS      := build/dlp_kernels.o build/dlp_batched.o build/dlp_mw.o build/dlp_session.o build/dlp_adalloc.o \
-             build/dlp_instance.o build/dlp_general.o
+             build/dlp_instance.o build/dlp_general.o build/dlp_defer.o
 
 all: $(LIBDLP) oracle tools
 
 build:
 	mkdir -p build
 
-build/%.o: $(CSRC)/%.hip $(CSRC)/dlp_internal.h include/dlp.h | build
+build/%.o: $(CSRC)/%.hip $(CSRC)/dlp_internal.h $(CSRC)/dlp_device.h include/dlp.h | build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 build/%.o: $(CSRC)/%.cpp $(CSRC)/dlp_internal.h $(CSRC)/dlp_host.h include/dlp.h | build

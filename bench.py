@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--variant", type=int, default=-1, help="update-kernel variant, -1 = auto")
     ap.add_argument("--ld-align", type=int, default=0, help="row alignment (doubles), 0 = auto")
     ap.add_argument("--timing", type=int, default=2)
+    ap.add_argument("--defer", type=int, default=0,
+                    help="pivots per tableau pass (1 = eager rank-1 per pivot, 0 = auto)")
+    ap.add_argument("--occupancy", type=int, default=-1, help="pass workgroups/CU cap (-1 = default)")
+    ap.add_argument("--form", type=int, default=-1, help="pass kernel form (-1 = default)")
     ap.add_argument("--pmc-dir", default=None,
                     help="rocprofv3 --pmc output dir (FETCH_SIZE / WRITE_SIZE) to fill roofline.traffic")
     return ap.parse_args()
@@ -100,6 +104,10 @@ def cpu_baseline(m, n, seed, k, threads):
                       f"(host tableau generation {gen:.1f} s not timed)"}
 
 
+def defer_of(sess) -> int:
+    return sess.update_stats()[2]
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -134,7 +142,10 @@ def main():
                        timing=args.timing, nontemporal=args.nontemporal,
                        update_variant=args.variant, ld_align=args.ld_align,
                        rows_per_block=args.rows_per_block, max_pivots=args.warmup + args.steps + 1,
-                       log_pivots=1)
+                       log_pivots=1, defer=args.defer)
+    if args.occupancy >= 0 or args.form >= 0:
+        if defer_of(sess) > 1:
+            sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 4, args.form)
     st, done = sess.run(args.warmup)
     if done != args.warmup:
         raise SystemExit(f"warm-up ended early: status {st} after {done} pivots")
@@ -149,11 +160,14 @@ def main():
         raise SystemExit(f"timed window ended early: status {st} after {done} pivots")
 
     tm, nsamp = sess.timings()
+    launches, upd_total_ms, defer = sess.update_stats()
     variant, rb_used, nt_used = sess.get_tuning()
     ld_used = sess.ld
     rows_local, N1 = sess.rows, sess.ncols + 1
-    upd_ms = tm[3] / max(nsamp, 1)
-    bytes_launch = 16.0 * (rows_local + 1) * N1
+    upd_ms = upd_total_ms / max(launches, 1)   # per update-kernel launch (rank-1, or rank-k pass)
+    # algorithmic bytes of one launch: one read + one write of every resident element
+    # (the deferred pass skips the objective row, kept current by the pivot-row kernel)
+    bytes_launch = 16.0 * (rows_local + (1 if defer == 1 else 0)) * N1
     achieved = bytes_launch / (upd_ms * 1e-3) / 1e9
 
     if dist is not None:
@@ -187,17 +201,22 @@ def main():
             "dtype": "f64",
             "data": "synthetic (device-generated splitmix64 dense LP, seed = config id)",
             "config": {"workload": desc, "m": m, "n": n, "N": m + n, "ld": ld_used, "seed": seed, "rows_per_rank": rows_local,
-                       "parallelism": f"rowblock{world}", "pricing": "dantzig->bland on degeneracy"},
+                       "parallelism": f"rowblock{world}", "pricing": "dantzig->bland on degeneracy",
+                       "pivots_per_tableau_pass": defer},
             "achieved_hbm_gbs": achieved,
             "phases_ms_per_pivot": {"ratio": tm[0] / max(nsamp, 1), "exchange": tm[1] / max(nsamp, 1),
-                                    "prow": tm[2] / max(nsamp, 1), "update": upd_ms},
+                                    "prow": tm[2] / max(nsamp, 1), "update": tm[3] / max(nsamp, 1)},
+            "update_launches": launches,
             "objective_after_window": res.objective,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": bytes_launch,
-                         "kernel": f"rank-1 update variant {variant} (rows/band {rb_used}, "
-                                   f"nt {nt_used}, ld {ld_used})", "launch_ms": upd_ms},
+                         "kernel": (f"rank-1 update variant {variant} (rows/band {rb_used}, "
+                                    f"nt {nt_used}, ld {ld_used})" if defer == 1 else
+                                    f"rank-{defer} tableau pass pass_kernel (rows/band {rb_used}, "
+                                    f"nt {nt_used}, ld {ld_used}): {defer} pivots per launch"),
+                         "launch_ms": upd_ms},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -50,6 +50,8 @@ class Options(C.Structure):
         ("ld_align", C.c_int32),
         ("pad_", C.c_int32),
         ("tol_feas", C.c_double),
+        ("defer", C.c_int32),
+        ("pad2_", C.c_int32),
     ]
 
 
@@ -136,6 +138,8 @@ SIGNATURES = [
     ("dlp_session_status", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(_I64)]),
     ("dlp_session_timings", C.c_int, [_P, _DP, C.POINTER(_I64)]),
     ("dlp_session_reset_timings", C.c_int, [_P]),
+    ("dlp_session_update_stats", C.c_int, [_P, C.POINTER(_I64), _DP, C.POINTER(C.c_int)]),
+    ("dlp_session_set_defer_tuning", C.c_int, [_P, C.c_int, C.c_int]),
     ("dlp_session_set_tuning", C.c_int, [_P, C.c_int, C.c_int, C.c_int]),
     ("dlp_session_get_tuning", C.c_int,
      [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),

@@ -1,0 +1,551 @@
+// dlp_defer.hip — deferred rank-k form of the pivot,
+// gfx950.  Up to K pivots are chosen against the stale HBM tableau T0, then
+// one pass applies them all: the tableau is streamed once per K pivots instead
+// of once per pivot, and every value stays bit-identical to K eager rank-1
+// updates (dlp_kernels.hip), because each element sees the same operations in
+// the same order:
+//   step l on row i:  i == p_l       -> T[i][c] := P[l][c]          (row p := prow)
+//                     C[l][i] != 0   -> T[i][c] := fma(-C[l][i], P[l][c], T[i][c])
+//                     C[l][i] == 0   -> untouched
+// where C[l][i] = T_l[i][q_l] (row i's entry in the entering column just
+// before step l) and P[l] = T_l[p_l] / T_l[p_l][q_l].  Per pivot only three
+// things are needed from the current tableau, each re-derived by replaying
+// the block's earlier steps on T0: column q (ratio_defer_kernel, one lane per
+// row), the pivot row p (prow_defer_kernel) and the RHS column (kept current
+// in `rhs`, one step per pivot).  The objective row is kept current in place
+// (updated by the pivot-row kernel, which also emits the next pricing
+// partials), and the pass (pass_kernel) skips it.
+//
+// Nearest reference analogs as for the eager kernels: the tight-set test
+// R/global_problem.cpp:372-380 (ratio), first-wins scans :335-361 (pricing),
+// the 2x2 basis solve :393-405 (elimination).  Built with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "dlp_internal.h"
+
+namespace dlp {
+namespace {
+
+#include "dlp_device.h"
+
+template <bool NT>
+__device__ inline d2 ldv(const double* p) {
+    if constexpr (NT)
+        return __builtin_nontemporal_load((const d2*)p);
+    else
+        return *(const d2*)p;
+}
+template <bool NT>
+__device__ inline double ldv1(const double* p) {
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+template <bool NT>
+__device__ inline void stv1(double* p, double v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+template <bool NT>
+__device__ inline void stv(double* p, d2 v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, (d2*)p);
+    else
+        *(d2*)p = v;
+}
+
+// a1 + a2 (+ a4 single rank) on the replayed column q.  Pricing as in the
+// eager ratio_kernel.  Lane i: a = T_j[i][q] by replaying steps 0..j-1 on
+// T0[i][q]; C[j][i] = a; the RHS cache advances by step j-1 (or is read from
+// T0 when the block is empty); then the ratio candidate.  The objective row
+// (local index rows) is current in place: C[j][rows] = z_q.
+__global__ __launch_bounds__(kRatioThreads) void ratio_defer_kernel(
+    const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
+    int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
+    DevState* st, double* __restrict__ C, int64_t ldc, const double* __restrict__ P,
+    double* __restrict__ rhs, Cand* partials, Cand* cand_out, int nranks, double tol_dj,
+    double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap) {
+    __shared__ PricePart lds_pp[4];
+    __shared__ Cand lds_c[4];
+    __shared__ int s_last;
+    __shared__ double s_pq[kMaxDefer], s_pn[kMaxDefer];
+    __shared__ int32_t s_pl[kMaxDefer];
+    if (st->status != DLP_RUNNING) return;
+
+    PricePart acc = pp_empty();
+    for (int k = threadIdx.x; k < ntiles; k += blockDim.x) pp_combine(acc, pp[k]);
+    acc = block_price(acc, lds_pp);
+    int32_t q;
+    if (st->bland)
+        q = acc.jbland;
+    else
+        q = (acc.jmin != kNoIndex && acc.zmin < -tol_dj) ? acc.jmin : kNoIndex;
+    if (q == kNoIndex) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->q = -1;
+            st->status = DLP_OK;
+        }
+        return;
+    }
+
+    const int j = st->blk;
+    for (int l = threadIdx.x; l < j; l += blockDim.x) {
+        s_pq[l] = P[(int64_t)l * ld + q];
+        s_pn[l] = P[(int64_t)l * ld + ncols];
+        s_pl[l] = st->pl[l];
+    }
+    __syncthreads();
+
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    Cand c = cand_empty();
+    if (i <= rows) {
+        double a = T[i * ld + q];
+        if (i < rows)
+            for (int l = 0; l < j; ++l) {
+                if (i == s_pl[l]) {
+                    a = s_pq[l];
+                } else {
+                    const double f = C[i * ldc + l];
+                    if (f != 0.0) a = __builtin_fma(-f, s_pq[l], a);
+                }
+            }
+        C[i * ldc + j] = a;
+        if (i < rows_elig) {
+            double r;
+            if (j == 0) {
+                r = T[i * ld + ncols];
+            } else {
+                const int l = j - 1;
+                r = rhs[i];
+                if (i == s_pl[l]) {
+                    r = s_pn[l];
+                } else {
+                    const double f = C[i * ldc + l];
+                    if (f != 0.0) r = __builtin_fma(-f, s_pn[l], r);
+                }
+            }
+            rhs[i] = r;
+            if (a > tol_piv) {
+                double b = r;
+                if (!(b > 0.0)) b = 0.0;
+                c.ratio = b / a;
+                c.row = (int32_t)(row_first + i);
+                c.basis_var = basis[row_first + i];
+                c.valid = 1;
+                c.pivot = a;
+            }
+        }
+    }
+    c = block_cand(c, lds_c);
+
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = c;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev =
+            __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    Cand best = cand_empty();
+    for (int k = threadIdx.x; k < (int)gridDim.x; k += blockDim.x) {
+        const Cand o = partials[k];
+        if (cand_better(o, best)) best = o;
+    }
+    best = block_cand(best, lds_c);
+    if (threadIdx.x == 0) {
+        st->ticket = 0;
+        st->q = q;
+        if (nranks == 1)
+            do_select(st, best, q, basis, row_first, rows, pricing, log, log_cap, true);
+        else
+            cand_out[0] = best;
+    }
+}
+
+// P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
+// pricing partial of this 512-column tile; objective value into the log.
+// Same per-element operations as the eager update kernel's objective band.
+__device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
+                                  int64_t nprice, const DevState* st, const double* __restrict__ C,
+                                  int64_t ldc, double* __restrict__ P, int s, int64_t j, d2 pr,
+                                  PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
+                                  PricePart* lds_pp) {
+    const int64_t width = (ncols + 16) & ~(int64_t)15;
+    if (j < ld) *(d2*)(P + (int64_t)s * ld + j) = pr;
+    const double zq = C[rows * ldc + s];
+    PricePart acc = pp_empty();
+    if (j < width) {
+        double* zp = T + rows * ld + j;
+        d2 z = *(const d2*)zp;
+        if (zq != 0.0) {
+            z.x = __builtin_fma(-zq, pr.x, z.x);
+            z.y = __builtin_fma(-zq, pr.y, z.y);
+            *(d2*)zp = z;
+        }
+        price_pair(acc, z.x, z.y, j, nprice, tol_dj);
+        if (log && j <= ncols && ncols < j + 2) {
+            const int64_t k = st->npivots - 1;
+            if (k >= 0 && k < log_cap) log[k].objective = (ncols == j) ? z.x : z.y;
+        }
+    }
+    acc = block_price(acc, lds_pp);
+    if (threadIdx.x == 0) pp[blockIdx.x] = acc;
+}
+
+// a3 first half on the replayed pivot row: T_s[p] = steps 0..s-1 applied to
+// T0[p], divided by the pivot element (IEEE division).  fused (single rank):
+// commit_row as well.  Otherwise the owner writes the fp64 bits and every
+// other rank INT64_MIN for the int64 MAX exchange.
+__global__ __launch_bounds__(256) void prow_defer_kernel(
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
+    const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
+    int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
+    int fused) {
+    __shared__ PricePart lds_pp[4];
+    __shared__ double s_cp[kMaxDefer];
+    __shared__ int32_t s_pl[kMaxDefer];
+    if (st->status != DLP_RUNNING) return;
+    const int s = st->blk - 1;
+    const int32_t pl = st->p_local;
+    if (pl >= 0)
+        for (int l = threadIdx.x; l < s; l += blockDim.x) {
+            s_cp[l] = C[(int64_t)pl * ldc + l];
+            s_pl[l] = st->pl[l];
+        }
+    __syncthreads();
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    d2 pr;
+    pr.x = 0.0;
+    pr.y = 0.0;
+    if (pl >= 0 && j < ld) {
+        d2 t = *(const d2*)(T + (int64_t)pl * ld + j);
+        for (int l = 0; l < s; ++l) {
+            const d2 pv = *(const d2*)(P + (int64_t)l * ld + j);
+            if (pl == s_pl[l]) {
+                t = pv;
+            } else if (s_cp[l] != 0.0) {
+                t.x = __builtin_fma(-s_cp[l], pv.x, t.x);
+                t.y = __builtin_fma(-s_cp[l], pv.y, t.y);
+            }
+        }
+        const double piv = st->piv;
+        pr.x = t.x / piv;
+        pr.y = t.y / piv;
+    }
+    if (!fused) {
+        if (j < ld) {
+            if (pl >= 0) {
+                *(d2*)(bits + j) = pr;   // the fp64 bits, as int64
+            } else {
+                bits[j] = INT64_MIN;
+                bits[j + 1] = INT64_MIN;
+            }
+        }
+        return;
+    }
+    commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
+               lds_pp);
+}
+
+// Multi-rank: P[s] from the exchanged bits, then the objective row + pricing.
+__global__ __launch_bounds__(256) void commit_defer_kernel(
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
+    const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
+    const int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log,
+    int64_t log_cap) {
+    __shared__ PricePart lds_pp[4];
+    if (st->status != DLP_RUNNING) return;
+    const int s = st->blk - 1;
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    d2 pr;
+    pr.x = 0.0;
+    pr.y = 0.0;
+    if (j < ld) pr = *(const d2*)(bits + j);
+    commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
+               lds_pp);
+}
+
+// The tableau pass.  Workgroup (tile, band): 512 columns (2 doubles per lane,
+// one 16-B access) of rb constraint rows.  Each lane holds P[0..kb)[its two
+// columns] in registers for the whole band.  The band's coefficients C[i][l]
+// (row-major, one contiguous rb*K block) are staged in LDS, negated, and one
+// lane per row classifies its row once:
+//   kUntouched  every C[i][l] == 0 and never a pivot row -> no load, no store
+//   kDense      every step touches it                   -> branch-free fma chain
+//   kSparse     some steps skip it                      -> fma + select per step
+//   >= 0        last step at which it was the pivot row  -> start from P[that step]
+// Per element the operations are exactly the eager sequence.
+constexpr int kUntouched = -3, kDense = -2, kSparse = -1;
+
+template <int K>
+__device__ inline d2 chain_dense(d2 t, const d2* pr, const double* nf) {
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        t.x = __builtin_fma(nf[l], pr[l].x, t.x);
+        t.y = __builtin_fma(nf[l], pr[l].y, t.y);
+    }
+    return t;
+}
+
+template <bool NT, int K>
+__global__ __launch_bounds__(256) void pass_kernel(double* __restrict__ T, int64_t ld, int64_t rows,
+                                                   int64_t width, const DevState* st,
+                                                   const double* __restrict__ C, int64_t ldc,
+                                                   const double* __restrict__ P, int rb) {
+    extern __shared__ double lds[];   // nf[rb][K] (negated C), then int32 cls[rb]
+    __shared__ int32_t s_pl[K];
+    const int kb = st->blk;
+    if (kb == 0) return;
+    const int64_t j = (int64_t)blockIdx.x * kDeferTile + threadIdx.x * 2;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 2;
+    d2 pr[K];
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        pr[l].x = 0.0;
+        pr[l].y = 0.0;
+        if (l < kb) pr[l] = *(const d2*)(P + (int64_t)l * ld + jc);
+    }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    double* nf = lds;
+    int32_t* cls = (int32_t*)(lds + (size_t)rb * K);
+    const double* Cb = C + i0 * ldc;   // the band's rows: one contiguous block when ldc == K
+    for (int idx = threadIdx.x; idx < nr * K; idx += blockDim.x) {
+        const int r = idx / K, l = idx - r * K;
+        nf[idx] = l < kb ? -Cb[(int64_t)r * ldc + l] : 0.0;
+    }
+    if (threadIdx.x < K) s_pl[threadIdx.x] = threadIdx.x < kb ? st->pl[threadIdx.x] : -1;
+    __syncthreads();
+    for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+        int last = -1, nz = 0;
+        for (int l = 0; l < kb; ++l) {
+            if (s_pl[l] == (int32_t)(i0 + r)) last = l;
+            nz += nf[r * K + l] != 0.0;
+        }
+        cls[r] = last >= 0 ? last : (nz == kb ? kDense : (nz == 0 ? kUntouched : kSparse));
+    }
+    __syncthreads();
+    const bool full = kb == K;
+    for (int r = 0; r < nr; ++r) {
+        const int c = cls[r];   // wave-uniform
+        if (c == kUntouched) continue;
+        double* row = T + (i0 + r) * ld;
+        const double* f = nf + r * K;
+        d2 t;
+        if (c == kDense && full) {
+            t = chain_dense<K>(ldv<NT>(row + jc), pr, f);
+        } else {
+            if (c >= 0) {
+                t.x = 0.0;
+                t.y = 0.0;
+            } else {
+                t = ldv<NT>(row + jc);
+            }
+#pragma unroll
+            for (int l = 0; l < K; ++l) {
+                if (l < kb && l >= c) {   // c < 0: every step; c >= 0: from the last pivot step on
+                    if (l == c) {
+                        t = pr[l];
+                    } else {
+                        d2 u;
+                        u.x = __builtin_fma(f[l], pr[l].x, t.x);
+                        u.y = __builtin_fma(f[l], pr[l].y, t.y);
+                        const bool skip = f[l] == 0.0;
+                        t.x = skip ? t.x : u.x;
+                        t.y = skip ? t.y : u.y;
+                    }
+                }
+            }
+        }
+        if (colok) stv<NT>(row + j, t);
+    }
+}
+
+// Narrow form of the pass: one double per lane (256 columns per workgroup),
+// so P[0..K) needs half the registers, and U rows per iteration, so each lane
+// runs U independent fma chains (the chain, not HBM, limits the wide form at
+// large K).  Dense groups (all U rows touched by every step, full block) take
+// the branch-free path; everything else goes row by row through the generic
+// replay.  Same per-element operations as pass_kernel.
+template <bool NT, int K, int U>
+__global__ __launch_bounds__(256) void pass1_kernel(double* __restrict__ T, int64_t ld, int64_t rows,
+                                                    int64_t width, const DevState* st,
+                                                    const double* __restrict__ C, int64_t ldc,
+                                                    const double* __restrict__ P, int rb) {
+    extern __shared__ double lds[];   // nf[rb][K] (negated C), then int32 cls[rb]
+    __shared__ int32_t s_pl[K];
+    const int kb = st->blk;
+    if (kb == 0) return;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 1;
+    double pr[K];
+#pragma unroll
+    for (int l = 0; l < K; ++l) pr[l] = (l < kb) ? P[(int64_t)l * ld + jc] : 0.0;
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    double* nf = lds;
+    int32_t* cls = (int32_t*)(lds + (size_t)rb * K);
+    const double* Cb = C + i0 * ldc;
+    for (int idx = threadIdx.x; idx < nr * K; idx += blockDim.x) {
+        const int r = idx / K, l = idx - r * K;
+        nf[idx] = l < kb ? -Cb[(int64_t)r * ldc + l] : 0.0;
+    }
+    if (threadIdx.x < K) s_pl[threadIdx.x] = threadIdx.x < kb ? st->pl[threadIdx.x] : -1;
+    __syncthreads();
+    for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+        int last = -1, nz = 0;
+        for (int l = 0; l < kb; ++l) {
+            if (s_pl[l] == (int32_t)(i0 + r)) last = l;
+            nz += nf[r * K + l] != 0.0;
+        }
+        cls[r] = last >= 0 ? last : (nz == kb ? kDense : (nz == 0 ? kUntouched : kSparse));
+    }
+    __syncthreads();
+    const bool full = kb == K;
+    int r = 0;
+    if (full)
+        for (; r + U <= nr; r += U) {
+            bool dense = true;
+#pragma unroll
+            for (int u = 0; u < U; ++u) dense = dense && cls[r + u] == kDense;
+            if (!dense) break;
+            double t[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) t[u] = ldv1<NT>(T + (i0 + r + u) * ld + jc);
+            const double* f = nf + r * K;
+#pragma unroll
+            for (int l = 0; l < K; l += 2) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const d2 c = *(const d2*)(f + u * K + l);   // one 16-B LDS broadcast
+                    t[u] = __builtin_fma(c.x, pr[l], t[u]);
+                    t[u] = __builtin_fma(c.y, pr[l + 1], t[u]);
+                }
+            }
+            if (colok)
+#pragma unroll
+                for (int u = 0; u < U; ++u) stv1<NT>(T + (i0 + r + u) * ld + j, t[u]);
+        }
+    for (; r < nr; ++r) {   // generic replay, one row at a time
+        const int c = cls[r];
+        if (c == kUntouched) continue;
+        double* row = T + (i0 + r) * ld;
+        const double* f = nf + r * K;
+        double t = c >= 0 ? 0.0 : ldv1<NT>(row + jc);
+#pragma unroll
+        for (int l = 0; l < K; ++l) {
+            if (l < kb && l >= c) {
+                if (l == c) {
+                    t = pr[l];
+                } else {
+                    const double u = __builtin_fma(f[l], pr[l], t);
+                    t = f[l] == 0.0 ? t : u;
+                }
+            }
+        }
+        if (colok) stv1<NT>(row + j, t);
+    }
+}
+
+__global__ void blk_reset_kernel(DevState* st) {
+    if (threadIdx.x == 0) st->blk = 0;
+}
+
+}  // namespace
+
+hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
+                              const PricePart* pp, DevState* st, Cand* partials, int nblocks,
+                              Cand* cand_out, int nranks, double tol_dj, double tol_piv,
+                              int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+    const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
+    ratio_defer_kernel<<<nblocks, kRatioThreads, 0, s>>>(
+        g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc,
+        d.P, d.rhs, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
+                             int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
+                             int64_t log_cap, int nranks, hipStream_t s) {
+    const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
+    prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
+                                             d.P, prow_bits, pp, tol_dj, log, log_cap,
+                                             nranks == 1 ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_commit_defer(const Geometry& g, const Defer& d, const DevState* st,
+                               const int64_t* prow_bits, PricePart* pp, double tol_dj,
+                               dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+    const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
+    commit_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C,
+                                               d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap);
+    return hipGetLastError();
+}
+
+template <bool NT, int K>
+static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
+                       hipStream_t s) {
+    const int cols = d.form == 0 ? kDeferTile : 256;
+    const int ntiles = (int)((g.width + cols - 1) / cols);
+    const int64_t bands = (g.rows + rb - 1) / rb;
+    size_t dyn = (size_t)K * rb * sizeof(double) + (size_t)rb * sizeof(int32_t);
+    if (dyn > 160 * 1024) return hipErrorInvalidValue;
+    if (occ > 0) {   // reserve LDS so that at most `occ` workgroups fit on a CU (160 KiB)
+        const size_t cap = (size_t)160 * 1024 / occ - 1024;
+        if (dyn < cap) dyn = cap;
+    }
+    const dim3 grid(ntiles, (unsigned)bands);
+    if (g.rows > 0) {
+        if (d.form == 0) {
+            if constexpr (K <= 32)   // 2 doubles per lane: P[0..K) in 4K VGPRs
+                pass_kernel<NT, K><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st, d.C,
+                                                          d.ldc, d.P, rb);
+            else
+                return hipErrorInvalidValue;
+        } else if (d.form == 1)
+            pass1_kernel<NT, K, 2><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st, d.C,
+                                                          d.ldc, d.P, rb);
+        else
+            pass1_kernel<NT, K, 4><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st, d.C,
+                                                          d.ldc, d.P, rb);
+    }
+    blk_reset_kernel<<<1, 64, 0, s>>>(st);
+    return hipGetLastError();
+}
+
+template <bool NT>
+static hipError_t pass_k(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
+                         hipStream_t s) {
+    if (d.K <= 4) return pass<NT, 4>(g, d, st, rb, occ, s);
+    if (d.K <= 8) return pass<NT, 8>(g, d, st, rb, occ, s);
+    if (d.K <= 16) return pass<NT, 16>(g, d, st, rb, occ, s);
+    if (d.K <= 32) return pass<NT, 32>(g, d, st, rb, occ, s);
+    return pass<NT, 64>(g, d, st, rb, occ, s);
+}
+
+hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
+                              int rows_per_block, int occupancy, hipStream_t s) {
+    if (d.K < 1 || d.K > kMaxDefer || rows_per_block < 1 || rows_per_block > 1024)
+        return hipErrorInvalidValue;
+    return nontemporal ? pass_k<true>(g, d, st, rows_per_block, occupancy, s)
+                       : pass_k<false>(g, d, st, rows_per_block, occupancy, s);
+}
+
+}  // namespace dlp

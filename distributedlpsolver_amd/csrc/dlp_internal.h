@@ -19,6 +19,8 @@ constexpr int kProwThreads = 256;
 constexpr int32_t kNoIndex = 0x7fffffff;
 constexpr int kColqPad = 16;   // colq allocated with rows + 1 + kColqPad entries
 constexpr int32_t kStatusSkip = 5;   // DevState.status: redundant row, forced pivot skipped
+constexpr int kMaxDefer = 64;        // deferred rank-k update: at most 64 pivots per tableau pass
+constexpr int kDeferTile = 512;      // deferred kernels: 256 lanes x 2 doubles per column tile
 
 // Pricing partial of one column tile of the objective row.
 struct alignas(16) PricePart {
@@ -51,7 +53,9 @@ struct alignas(16) DevState {
     double piv;        // pivot element T[p][q]
     double ratio;      // r_p
     uint32_t ticket;   // last-workgroup election of the ratio kernel
-    uint32_t pad[3];
+    int32_t blk;       // deferred mode: pivots selected since the last tableau pass
+    uint32_t pad[2];
+    int32_t pl[kMaxDefer];   // deferred mode: local pivot row of block step l (-1 elsewhere)
 };
 
 // Candidate order: valid first, then smaller ratio, then smaller basis index.
@@ -62,6 +66,23 @@ __host__ __device__ inline bool cand_better(const Cand& a, const Cand& b) {
     if (a.ratio != b.ratio) return a.ratio < b.ratio;
     return a.basis_var < b.basis_var;
 }
+
+// Deferred rank-k update (dlp_defer.hip).  Up to K pivots are selected against
+// the stale HBM tableau T0 through "replayed" views (column q and pivot row p
+// re-derived by applying the block's earlier steps, in order, with the same
+// fma / overwrite / skip per element as the eager update); the objective row
+// and the RHS column are kept current eagerly; one pass then applies all
+// steps to every element in order.  Every value is therefore bit-identical to
+// K eager rank-1 updates while the tableau is streamed once per K pivots.
+struct Defer {
+    int K = 1;             // block size (1 = eager path, no deferral)
+    double* C = nullptr;   // (rows+1) x K row-major: C[i*ldc + l] = T_l[i][q_l]
+    int64_t ldc = 0;       // = K (row `rows` = the objective row's entries)
+    double* P = nullptr;   // K x ld: normalised pivot rows
+    double* rhs = nullptr; // rows: current RHS column (eager cache)
+    int form = 2;          // pass kernel: 0 = 2 doubles/lane, 1 = 1 double/lane x 2 rows,
+                           // 2 = 1 double/lane x 4 rows (default)
+};
 
 // Launchers (dlp_kernels.hip).  All asynchronous on `stream`.
 struct Geometry {
@@ -92,7 +113,7 @@ hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* bas
 int ratio_blocks(const Geometry& g);
 hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32_t* basis,
                          DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
-                         hipStream_t s, bool forced = false);
+                         hipStream_t s, bool forced = false, bool track = false);
 // General LPs (Phase I -> II).  drive: forced-pivot candidate for global row
 // `row` (nranks == 1: also select + colq capture); gather_q: colq of st->q;
 // carry_out / carry_in: ship the carried objective row through the int64 MAX
@@ -105,6 +126,24 @@ hipError_t launch_carry_out(const Geometry& g, int64_t carry_local, int64_t* out
 hipError_t launch_carry_in(const Geometry& g, const int64_t* in, DevState* st, int pricing,
                            hipStream_t s);
 hipError_t launch_set_status(DevState* st, int status, hipStream_t s);
+
+// Deferred launchers (dlp_defer.hip).  Pricing tiles are kDeferTile columns.
+hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
+                              const PricePart* pp, DevState* st, Cand* partials, int nblocks,
+                              Cand* cand_out, int nranks, double tol_dj, double tol_piv,
+                              int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s);
+// nranks == 1: P[s] + objective row + pricing partials + log in one pass;
+// nranks > 1: the owner's replayed pivot-row bits (others INT64_MIN) to prow_bits.
+hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
+                             int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
+                             int64_t log_cap, int nranks, hipStream_t s);
+// nranks > 1, after the MAX all-reduce: P[s] from the exchanged bits + objective row + pricing.
+hipError_t launch_commit_defer(const Geometry& g, const Defer& d, const DevState* st,
+                               const int64_t* prow_bits, PricePart* pp, double tol_dj,
+                               dlp_pivot* log, int64_t log_cap, hipStream_t s);
+// The tableau pass: applies the block's st->blk steps to rows [0, rows), then blk = 0.
+hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
+                              int rows_per_block, int occupancy, hipStream_t s);
 hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits, int nranks,
                        hipStream_t s);
 hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,

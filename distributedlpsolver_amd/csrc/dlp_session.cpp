@@ -103,6 +103,13 @@ struct dlp_session {
     int64_t phase1_pivots = 0;
     enum StepKind { STEP_PIVOT, STEP_FORCED, STEP_CARRY } step_kind = STEP_PIVOT;
     bool step_void = false;
+    // deferred rank-k update (dlp_defer.hip): block arrays, pivots enqueued since
+    // the last tableau pass, pass geometry; update-kernel launch accounting
+    dlp::Defer d;
+    int since_flush = 0;
+    int defer_rb = 64, defer_occ = 4;
+    std::vector<uint8_t> ev_flush;   // per timed slot: a pass ran in it
+    int64_t upd_launches = 0;
 };
 
 namespace {
@@ -190,7 +197,7 @@ void free_session(dlp_session* s) {
     for (auto e : s->ev) (void)hipEventDestroy(e);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     void* dev[] = {s->T, s->colq, s->prow_send, s->partials, s->cand_send, s->cand_recv,
-                   s->pp, s->basis, s->st, s->log};
+                   s->pp, s->basis, s->st, s->log, s->d.C, s->d.P, s->d.rhs};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
@@ -291,6 +298,24 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     }
     const int tile = dlp::update_tile(opt->update_variant);
     g.ntiles = (int)((s->width + tile - 1) / tile);
+    // deferred rank-k update: auto = 16 pivots per tableau pass; eager when the
+    // caller drives the exchange itself (dlp_session_step_*) or when the chosen
+    // rank-1 variant tiles pricing differently from the deferred kernels
+    {
+        const bool host_driven = (nranks > 1 || uid != nullptr) && uid == nullptr;
+        int K = opt->defer;
+        if (K < 0 || K > dlp::kMaxDefer) {
+            set_error("defer must be 0 (auto) or 1..64");
+            return DLP_ERR_ARG;
+        }
+        if (K == 0) K = (host_driven || tile != dlp::kDeferTile) ? 1 : 16;
+        if (K > 1 && (host_driven || tile != dlp::kDeferTile)) {
+            set_error("defer > 1 needs dlp_session_run (not the step API) and a 512-column update variant");
+            return DLP_ERR_ARG;
+        }
+        s->d.K = K;
+        s->opt.defer = K;
+    }
     g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block : auto_rows_per_block(s);
     g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
     const size_t tbytes = (size_t)rows_total * s->ld * sizeof(double);
@@ -317,6 +342,15 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     s->log_cap = opt->log_pivots ? std::max<int64_t>(1, opt->max_pivots) : 0;
     if (s->log_cap > 0) HIP_TRY(hipMalloc(&s->log, sizeof(dlp_pivot) * s->log_cap));
     HIP_TRY(hipHostMalloc(&s->host_st, sizeof(dlp::DevState), hipHostMallocDefault));
+    if (s->d.K > 1) {
+        s->d.ldc = s->d.K;
+        HIP_TRY(hipMalloc(&s->d.C, sizeof(double) * s->d.K * (rows_total + 1)));
+        HIP_TRY(hipMalloc(&s->d.P, sizeof(double) * s->d.K * s->ld));
+        HIP_TRY(hipMalloc(&s->d.rhs, sizeof(double) * (s->rows + 1)));
+        HIP_TRY(hipMemsetAsync(s->d.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
+        HIP_TRY(hipMemsetAsync(s->d.P, 0, sizeof(double) * s->d.K * s->ld, s->stream));
+        if (opt->rows_per_block > 0) s->defer_rb = std::min(opt->rows_per_block, 1024);
+    }
     HIP_TRY(hipMemsetAsync(s->prow_send, 0, sizeof(int64_t) * s->ld, s->stream));
 
     // tableau
@@ -335,6 +369,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     HIP_TRY(hipMemcpyAsync(s->basis, basis.data(), sizeof(int32_t) * s->m, hipMemcpyHostToDevice,
                            s->stream));
     dlp::DevState st0{};
+    for (int l = 0; l < dlp::kMaxDefer; ++l) st0.pl[l] = -1;
     st0.status = DLP_RUNNING;
     st0.q = -1;
     st0.p = -1;
@@ -353,9 +388,11 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         s->use_rccl = true;
     }
     s->ev_per_pivot = opt->timing == 1 ? 2 : (opt->timing >= 2 ? 5 : 0);
+    if (s->ev_per_pivot && s->d.K > 1) s->ev_per_pivot = 5;   // the pass is timed per slot
     if (s->ev_per_pivot) {
         s->ev.resize((size_t)s->ev_per_pivot * opt->check_interval);
         for (auto& e : s->ev) HIP_TRY(hipEventCreate(&e));
+        s->ev_flush.assign(opt->check_interval, 0);
     }
     return DLP_OK;
 }
@@ -388,7 +425,54 @@ int enqueue_update(dlp_session* s) {
     return DLP_OK;
 }
 
-int enqueue_pivot(dlp_session* s, int64_t slot) {
+// Deferred mode: the tableau pass of the pivots enqueued since the last one
+// (a no-op on the device when the block is empty).
+int enqueue_flush(dlp_session* s) {
+    if (s->d.K <= 1) return DLP_OK;
+    HIP_TRY(dlp::launch_flush_defer(s->g, s->d, s->st, s->opt.nontemporal != 0, s->defer_rb,
+                                    s->defer_occ, s->stream));
+    s->since_flush = 0;
+    return DLP_OK;
+}
+
+// One deferred pivot: replayed ratio test, exchange, replayed pivot row (+
+// objective row and pricing), and the pass when the block is full or `last`.
+int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
+    const dlp_options& o = s->opt;
+    hipEvent_t* ev = s->ev_per_pivot ? &s->ev[(size_t)slot * s->ev_per_pivot] : nullptr;
+    if (ev) HIP_TRY(hipEventRecord(ev[0], s->stream));
+    HIP_TRY(dlp::launch_ratio_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
+                                    s->ratio_blocks, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
+                                    o.tol_piv, o.pricing, s->log, s->log_cap, s->stream));
+    if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
+    if (s->exchange) {
+        NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
+                               s->stream));
+        HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, o.pricing,
+                                   s->log, s->log_cap, s->stream, false, true));
+    }
+    if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
+    HIP_TRY(dlp::launch_prow_defer(s->g, s->d, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
+                                   s->log_cap, s->exchange ? 2 : 1, s->stream));
+    if (s->exchange) {
+        NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
+                               s->comm, s->stream));
+        HIP_TRY(dlp::launch_commit_defer(s->g, s->d, s->st, s->prow_recv, s->pp, o.tol_dj, s->log,
+                                         s->log_cap, s->stream));
+    }
+    if (ev) HIP_TRY(hipEventRecord(ev[3], s->stream));
+    s->since_flush += 1;
+    const bool flush = last || s->since_flush >= s->d.K;
+    if (flush) CALL_TRY(enqueue_flush(s));
+    if (ev) {
+        HIP_TRY(hipEventRecord(ev[4], s->stream));
+        s->ev_flush[slot] = flush ? 1 : 0;
+    }
+    return DLP_OK;
+}
+
+int enqueue_pivot(dlp_session* s, int64_t slot, bool last = true) {
+    if (s->d.K > 1) return enqueue_pivot_defer(s, slot, last);
     hipEvent_t* ev = s->ev_per_pivot ? &s->ev[(size_t)slot * s->ev_per_pivot] : nullptr;
     const bool all = s->ev_per_pivot == 5;
     if (all) HIP_TRY(hipEventRecord(ev[0], s->stream));
@@ -522,6 +606,7 @@ int poll(dlp_session* s) {
                     s->timings[ph] += ms;
                 }
             }
+            s->upd_launches += (s->d.K > 1) ? s->ev_flush[k] : 1;
         }
         s->nsamples += real;
     }
@@ -536,7 +621,7 @@ int run_window_graph(dlp_session* s, int64_t chunk) {
         if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
         HIP_TRY(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
         int rc = DLP_OK;
-        for (int64_t k = 0; k < chunk && rc == DLP_OK; ++k) rc = enqueue_pivot(s, 0);
+        for (int64_t k = 0; k < chunk && rc == DLP_OK; ++k) rc = enqueue_pivot(s, 0, k == chunk - 1);
         hipGraph_t gr = nullptr;
         hipError_t e = hipStreamEndCapture(s->stream, &gr);
         if (rc != DLP_OK) return rc;
@@ -648,6 +733,7 @@ void dlp_options_default(dlp_options* o) {
     o->update_variant = -1;   // auto
     o->ld_align = 0;          // auto
     o->tol_feas = 1e-9;
+    o->defer = 0;   // auto
 }
 
 const char* dlp_status_string(int st) {
@@ -992,7 +1078,7 @@ int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
         if (graph && chunk == s->opt.check_interval) {
             CALL_TRY(run_window_graph(s, chunk));
         } else {
-            for (int64_t k = 0; k < chunk; ++k) CALL_TRY(enqueue_pivot(s, k));
+            for (int64_t k = 0; k < chunk; ++k) CALL_TRY(enqueue_pivot(s, k, k == chunk - 1));
             s->ev_pending = s->ev_per_pivot ? chunk : 0;
         }
         s->launched += chunk;
@@ -1010,6 +1096,10 @@ int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
 // (its candidate is an empty slot, its "pivot row" the carried objective row).
 int dlp_session_step_candidate(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
+    if (s->d.K > 1) {
+        set_error("the step API drives eager sessions only: create the session with defer = 1");
+        return DLP_ERR_STATE;
+    }
     HIP_TRY(hipSetDevice(s->device));
     s->step_void = false;
     if (s->drive_next < s->drive.size()) {
@@ -1113,6 +1203,13 @@ int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_bloc
     HIP_TRY(hipStreamSynchronize(s->stream));
     if (update_variant < 0) update_variant = s->streaming ? 22 : 26;   // auto, as session_init
     if (nontemporal < 0) nontemporal = s->streaming ? 1 : 0;
+    if (s->d.K > 1) {   // deferred: rows_per_block sets the pass band; pricing tiles stay 512
+        if (dlp::update_tile(update_variant) != dlp::kDeferTile) {
+            set_error("a deferred session (defer > 1) needs a 512-column update variant");
+            return DLP_ERR_ARG;
+        }
+        s->defer_rb = rows_per_block > 0 ? std::min(rows_per_block, 1024) : 64;
+    }
     s->opt.update_variant = update_variant;
     s->opt.nontemporal = nontemporal;
     const int tile = dlp::update_tile(update_variant);
@@ -1131,8 +1228,21 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
                            int* nontemporal) {
     if (!s) return DLP_ERR_ARG;
     if (update_variant) *update_variant = s->opt.update_variant;
-    if (rows_per_block) *rows_per_block = s->g.rows_per_block;
+    if (rows_per_block) *rows_per_block = s->d.K > 1 ? s->defer_rb : s->g.rows_per_block;
     if (nontemporal) *nontemporal = s->opt.nontemporal;
+    return DLP_OK;
+}
+
+int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
+    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 2) return DLP_ERR_ARG;
+    if (form == 0 && s->d.K > 32) {
+        set_error("the 2-doubles-per-lane pass holds at most 32 steps");
+        return DLP_ERR_ARG;
+    }
+    s->defer_occ = occupancy;
+    if (form >= 0) s->d.form = form;
+    if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
+    if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
     return DLP_OK;
 }
 
@@ -1140,6 +1250,15 @@ int dlp_session_reset_timings(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     for (double& t : s->timings) t = 0.0;
     s->nsamples = 0;
+    s->upd_launches = 0;
+    return DLP_OK;
+}
+
+int dlp_session_update_stats(dlp_session* s, int64_t* launches, double* ms, int* defer) {
+    if (!s) return DLP_ERR_ARG;
+    if (launches) *launches = s->upd_launches;
+    if (ms) *ms = s->timings[DLP_PHASE_UPDATE];
+    if (defer) *defer = s->d.K;
     return DLP_OK;
 }
 

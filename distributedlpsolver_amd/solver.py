@@ -284,6 +284,18 @@ class Session:
                 "dlp_session_get_tuning")
         return v.value, rb.value, nt.value
 
+    def update_stats(self) -> tuple[int, float, int]:
+        """(timed update launches, their total ms, pivots per tableau pass)."""
+        n, ms, k = C.c_int64(), C.c_double(), C.c_int()
+        L.check(L.lib().dlp_session_update_stats(self._h, C.byref(n), C.byref(ms), C.byref(k)),
+                "dlp_session_update_stats")
+        return n.value, ms.value, k.value
+
+    def set_defer_tuning(self, occupancy: int, form: int = -1):
+        """Deferred pass: workgroups/CU cap (0 = none) and form (0 wide, 1/2 narrow x 2/4 rows)."""
+        L.check(L.lib().dlp_session_set_defer_tuning(self._h, occupancy, form),
+                "dlp_session_set_defer_tuning")
+
     def reset_timings(self):
         L.check(L.lib().dlp_session_reset_timings(self._h), "dlp_session_reset_timings")
 

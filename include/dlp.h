@@ -136,6 +136,11 @@ typedef struct dlp_options {
     int32_t pad_;
     double  tol_feas;        /* general LPs: infeasible when the Phase I optimum is below
                                 -tol_feas * (1 + max_i b'_i) (default 1e-9) */
+    int32_t defer;           /* pivots per tableau pass (deferred rank-k update, results
+                                bit-identical to rank-1): 1 = eager rank-1 per pivot, 2..64 =
+                                block size, 0 = auto (default: 16; eager for sessions driven
+                                through dlp_session_step_*) */
+    int32_t pad2_;
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
  * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;
@@ -262,12 +267,20 @@ int dlp_session_write_buffer(dlp_session* s, int which, const void* host, size_t
 int dlp_session_sync(dlp_session* s);
 int dlp_session_status(dlp_session* s, int* status, int64_t* npivots);
 int dlp_session_timings(dlp_session* s, double* ms_out /* DLP_NUM_PHASES */, int64_t* nsamples);
+/* Update-kernel launches timed (timing >= 1) and their total device time: one
+ * rank-1 update per pivot (defer = 1) or one rank-k tableau pass per block. */
+int dlp_session_update_stats(dlp_session* s, int64_t* launches, double* ms, int* defer);
 int dlp_session_reset_timings(dlp_session* s);
 /* Retune the rank-1 update between pivots (results are bit-identical for every
  * setting): variant 0..7 (rows in flight x doubles per lane x colq staging),
  * rows per workgroup band (0 = auto, <= 256), non-temporal loads/stores. */
 int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_block, int nontemporal);
 int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_block, int* nontemporal);
+/* Deferred sessions: workgroups per CU allowed for the tableau pass (LDS
+ * reservation; 0 = no cap, default 4) and its form (0 = 2 doubles per lane,
+ * K <= 32; 1 / 2 = 1 double per lane, 2 / 4 rows per iteration (default 2);
+ * -1 = keep).  rows_per_block (set_tuning) is the pass's row band. */
+int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
 int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,
                      int64_t* ncols);
 /* Copy the local tableau (rows_local+1 rows x ld, objective last) to the host. */

@@ -1,0 +1,113 @@
+"""Deferred rank-k update (dlp_defer.hip) against the eager rank-1 path and the
+oracle, bit for bit.  K pivots are selected on replayed views of the stale
+tableau and applied in one pass; every element must see exactly the eager
+sequence of fma / overwrite / skip, so pivot logs, x, y, basis and the whole
+tableau (incl. the objective row and padding) are identical for every block
+size, poll window (block boundaries anywhere in a window), pass geometry and
+cache policy."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+import distributedlpsolver_amd as dlp
+from distributedlpsolver_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_log(got, ref):
+    assert len(got) == len(ref), (len(got), len(ref))
+    g, r = np.ascontiguousarray(got), np.ascontiguousarray(ref)
+    if g.tobytes() != r.tobytes():
+        for k in range(len(r)):
+            if g[k].tobytes() != r[k].tobytes():
+                raise AssertionError(f"pivot {k}: gpu {g[k]} oracle {r[k]}")
+
+
+def _check(res, ref):
+    assert res.status == ref.status
+    _same_log(res.pivot_log, ref.pivot_log)
+    assert np.float64(res.objective).tobytes() == np.float64(ref.objective).tobytes()
+    assert res.x.tobytes() == ref.x.tobytes() and res.y.tobytes() == ref.y.tobytes()
+    assert res.basis.tobytes() == ref.basis.tobytes()
+
+
+@pytest.mark.parametrize("K", [2, 3, 8, 16, 32, 64])
+@pytest.mark.parametrize("ci,graph", [(5, 1), (16, 1), (64, 1), (100, 0)])
+def test_defer_c1_full_solve(K, ci, graph):
+    A, b, c = O.gen_dense(200, 400, 1)
+    ref = O.solve_dense(A, b, c)
+    res = dlp.solve(dlp.Problem.dense(A, b, c), defer=K, check_interval=ci, use_graph=graph)
+    _check(res, ref)
+
+
+@pytest.mark.parametrize("K", [4, 16])
+@pytest.mark.parametrize("pricing", [0, 1])
+def test_defer_degenerate_bland(K, pricing):
+    A, b, c = O.gen_dense(128, 128, 3, degenerate=True)
+    ref = O.solve_dense(A, b, c, pricing=pricing)
+    res = dlp.solve(dlp.Problem.dense(A, b, c), defer=K, pricing=pricing)
+    _check(res, ref)
+
+
+@pytest.mark.parametrize("K,rb,occ,nt,form", [(16, 16, 0, 0, 0), (16, 64, 4, 1, 0), (16, 256, 2, 1, 1),
+                                              (32, 128, 3, 0, 0), (8, 7, 6, 1, 2), (32, 64, 4, 1, 2),
+                                              (64, 64, 0, 1, 2), (64, 33, 4, 0, 1), (5, 64, 4, 1, 2)])
+def test_defer_pass_geometry_and_tableau(K, rb, occ, nt, form):
+    """Whole tableau after 45 pivots equals the eager session's, byte for byte."""
+    m, n, seed = 300, 520, 5
+    prob = dlp.Problem.random(m, n, seed)
+    with dlp.Session(prob, defer=1, check_interval=45) as e:
+        e.run(45)
+        Te = e.tableau()
+        le = e.result().pivot_log
+    with dlp.Session(prob, defer=K, check_interval=45, rows_per_block=rb, nontemporal=nt) as s:
+        s.set_defer_tuning(occ, form)
+        s.run(45)
+        Td = s.tableau()
+        ld = s.result().pivot_log
+    _same_log(ld, le)
+    assert Td.tobytes() == Te.tobytes()
+
+
+def test_defer_retune_between_runs():
+    A, b, c = O.gen_dense(200, 400, 2)
+    ref = O.solve_dense(A, b, c)
+    with dlp.Session(dlp.Problem.dense(A, b, c), defer=16, check_interval=9) as s:
+        for k in range(1000):
+            s.set_tuning(22 if k % 2 else 26, [16, 64, 200][k % 3], k % 2)
+            s.set_defer_tuning([0, 4, 2][k % 3], k % 3)
+            st, _ = s.run(11)
+            if st != L.RUNNING:
+                break
+        res = s.result()
+    _check(res, ref)
+
+
+def test_defer_adalloc_sparse_rows():
+    """Sparse tableau: most rows untouched by most steps (skip rule in the pass)."""
+    p = dlp.Problem.adalloc(200, 200, 1, 0.1, 0.25)
+    M, b, c = O.adalloc_lp(200, 200, 0.1, 0.25)
+    ref = O.solve_dense(M, b, c)
+    _check(dlp.solve(p, defer=16), ref)
+
+
+def test_defer_rejects_bad_settings():
+    A, b, c = O.gen_dense(20, 30, 1)
+    with pytest.raises(L.DLPError):
+        dlp.solve(dlp.Problem.dense(A, b, c), defer=65)
+    with pytest.raises(L.DLPError):
+        dlp.solve(dlp.Problem.dense(A, b, c), defer=8, update_variant=4)   # 1024-column tiles
+    with dlp.Session(dlp.Problem.dense(A, b, c), defer=8) as s:
+        with pytest.raises(L.DLPError):
+            s.step_candidate()
+        with pytest.raises(L.DLPError):
+            s.set_tuning(4, 8, 1)
+
+
+def test_defer_update_stats():
+    with dlp.Session(dlp.Problem.random(400, 600, 7), defer=8, timing=2, check_interval=40) as s:
+        s.run(40)
+        n, ms, k = s.update_stats()
+    assert k == 8 and n == 5 and ms > 0

@@ -231,14 +231,14 @@ def test_update_variants_bit_identical(variant):
     ref = O.solve_dense(A, b, c)
     for rb, nt in ((4, 1), (64, 0)):
         res = dlp.solve(dlp.Problem.dense(A, b, c), update_variant=variant, rows_per_block=rb,
-                        nontemporal=nt)
+                        nontemporal=nt, defer=1)
         _check_equal(res, ref)
 
 
 def test_retune_mid_solve():
     A, b, c = O.gen_dense(200, 400, 1)
     ref = O.solve_dense(A, b, c)
-    with dlp.Session(dlp.Problem.dense(A, b, c), check_interval=8) as s:
+    with dlp.Session(dlp.Problem.dense(A, b, c), check_interval=8, defer=1) as s:
         for k, v in enumerate([4, 0, 6, 2, 5, 7, 1, 3] * 100):
             s.set_tuning(v, 4 + 4 * (k % 5), k % 2)
             st, _ = s.run(16)

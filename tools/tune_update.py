@@ -34,7 +34,7 @@ m, n, seed = W[a.workload]
 sessions = {}
 for al in map(int, a.ld_aligns.split(",")):
     s = dlp.Session(dlp.Problem.random(m, n, seed), timing=1, check_interval=max(a.pivots, 1),
-                    max_pivots=10 ** 7, log_pivots=0, ld_align=al)
+                    max_pivots=10 ** 7, log_pivots=0, ld_align=al, defer=1)
     s.run(3)
     sessions[al] = s
 cfgs = [(al, v, rb, nt) for al in sessions for v in map(int, a.variants.split(","))
