@@ -60,7 +60,7 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(pmc_dir: str, kernel_substr: str = "update_kernel"):
+def pmc_traffic(pmc_dir: str, kernel_substr: str = "update_"):
     """Per-launch HBM bytes of the update kernel from rocprofv3 counter CSVs:
     (2 x FETCH_SIZE + WRITE_SIZE) KiB -> bytes (gfx950 FETCH_SIZE reads 1/2 of a
     wide coalesced stream: MI355X_MICROARCH.md §HBM)."""
@@ -82,11 +82,12 @@ def pmc_traffic(pmc_dir: str, kernel_substr: str = "update_kernel"):
     return (2.0 * sum(fetch) / len(fetch) + sum(write) / len(write)) * 1024.0
 
 
-def committed_traffic(workload: str):
-    """Latest committed PMC summary for this workload (profiles/*/<workload>_update_pmc_traffic.json),
-    produced by tools/gpu_profile.sh on the same kernel; None when absent."""
+def committed_traffic(workload: str, kernel: str):
+    """Latest committed PMC summary for this workload and kernel
+    (profiles/*/<workload>_<kernel>_pmc_traffic.json, kernel = update | pass), produced by
+    tools/gpu_profile.sh + tools/pmc_summary.py on the same kernel; None when absent."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{workload}_update_pmc_traffic.json")))
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{workload}_{kernel}_pmc_traffic.json")))
     if not paths:
         return None, None
     with open(paths[-1]) as f:
@@ -145,7 +146,7 @@ def main():
                        log_pivots=1, defer=args.defer)
     if args.occupancy >= 0 or args.form >= 0:
         if defer_of(sess) > 1:
-            sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 4, args.form)
+            sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 0, args.form)
     st, done = sess.run(args.warmup)
     if done != args.warmup:
         raise SystemExit(f"warm-up ended early: status {st} after {done} pivots")
@@ -179,10 +180,12 @@ def main():
     sess.close()
 
     if rank == 0:
+        ksub = "update_" if defer == 1 else "pass"
         if args.pmc_dir:
-            traffic, traffic_src = pmc_traffic(args.pmc_dir), f"live: {args.pmc_dir}"
+            traffic, traffic_src = pmc_traffic(args.pmc_dir, ksub), f"live: {args.pmc_dir}"
         else:
-            traffic, traffic_src = committed_traffic(args.workload) if world == 1 else (None, None)
+            traffic, traffic_src = (committed_traffic(args.workload, "update" if defer == 1 else "pass")
+                                    if world == 1 else (None, None))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(m, n, seed, args.cpu_pivots, args.cpu_threads)

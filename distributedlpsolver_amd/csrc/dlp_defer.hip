@@ -68,8 +68,8 @@ __global__ __launch_bounds__(kRatioThreads) void ratio_defer_kernel(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
     DevState* st, double* __restrict__ C, int64_t ldc, const double* __restrict__ P,
-    double* __restrict__ rhs, Cand* partials, Cand* cand_out, int nranks, double tol_dj,
-    double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap) {
+    double* __restrict__ rhs, int32_t* __restrict__ nzc, Cand* partials, Cand* cand_out,
+    int nranks, double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap) {
     __shared__ PricePart lds_pp[4];
     __shared__ Cand lds_c[4];
     __shared__ int s_last;
@@ -115,6 +115,7 @@ __global__ __launch_bounds__(kRatioThreads) void ratio_defer_kernel(
                 }
             }
         C[i * ldc + j] = a;
+        if (i < rows) nzc[i] = (j == 0 ? 0 : nzc[i]) + (a != 0.0 ? 1 : 0);   // the pass's row class
         if (i < rows_elig) {
             double r;
             if (j == 0) {
@@ -463,6 +464,217 @@ __global__ __launch_bounds__(256) void pass1_kernel(double* __restrict__ T, int6
     }
 }
 
+// Scalar-coefficient form of the pass (forms 3-5).  The coefficients C[i][l]
+// of a row are the same for every lane, so they are read with scalar loads
+// straight from the C block (uniform address, read-only in this kernel) and
+// enter v_fma_f64 as an SGPR operand with the negate modifier: no LDS traffic
+// per fma, which bounds the LDS-staged forms at large K (one LDS broadcast
+// per one or two fmas).  V doubles per lane (256 V columns per workgroup), U
+// rows per group, P[0..K) in VGPRs.  Row class: nzc[i] = number of nonzero
+// C[i][l] in the block (kept by ratio_defer_kernel), and the block's last
+// pivot step on the row.  Same per-element operations as pass_kernel.
+template <bool NT, int V>
+__device__ inline void ldrow(double (&t)[V], const double* p) {
+    if constexpr (V == 2) {
+        const d2 v = ldv<NT>(p);
+        t[0] = v.x;
+        t[1] = v.y;
+    } else {
+        t[0] = ldv1<NT>(p);
+    }
+}
+template <bool NT, int V>
+__device__ inline void strow(double* p, const double (&t)[V]) {
+    if constexpr (V == 2) {
+        d2 v;
+        v.x = t[0];
+        v.y = t[1];
+        stv<NT>(p, v);
+    } else {
+        stv1<NT>(p, t[0]);
+    }
+}
+
+// The block's coefficients are read-only during the pass: through the constant
+// address space, wave-uniform loads of them are always scalar loads.
+typedef __attribute__((address_space(4))) const double* cdptr;
+
+template <bool NT, int K, int V, int U, bool PART>
+__global__ __launch_bounds__(256) void pass_s_kernel(double* __restrict__ T, int64_t ld,
+                                                     int64_t rows, int64_t width,
+                                                     const DevState* __restrict__ st,
+                                                     const double* __restrict__ C, int64_t ldc,
+                                                     const double* __restrict__ P,
+                                                     const int32_t* __restrict__ nzc, int rb) {
+    __shared__ int32_t cls[1024];
+    const int kb = st->blk;
+    // two launches per pass: the full-block instance (kb == K) and the partial one
+    // (0 < kb < K: a window's last block, or one cut short by termination), so that
+    // neither carries the other's register pressure; exactly one of them runs
+    if (kb == 0 || (PART ? kb == K : kb != K)) return;
+    const int64_t j = (int64_t)blockIdx.x * (256 * V) + threadIdx.x * V;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - V;
+    double pr[K][V];
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        double v[V];
+        ldrow<false, V>(v, P + (int64_t)l * ld + jc);
+#pragma unroll
+        for (int e = 0; e < V; ++e) pr[l][e] = l < kb ? v[e] : 0.0;
+    }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+        const int nz = nzc[i0 + r];
+        int last = -1;
+        for (int l = 0; l < kb; ++l)
+            if (st->pl[l] == (int32_t)(i0 + r)) last = l;
+        cls[r] = last >= 0 ? last : (nz == kb ? kDense : (nz == 0 ? kUntouched : kSparse));
+    }
+    __syncthreads();
+    // dense groups: U rows, every step of the block touches every row.  The next dense
+    // group's rows are loaded before this group's fma chains, so every wave keeps two
+    // groups of HBM loads in flight (vector loads retire in order: vmcnt covers them,
+    // while the coefficients' scalar loads wait on lgkmcnt only).
+    auto dense_at = [&](int r0) {
+        if (r0 + U > nr) return false;
+        bool d = true;
+#pragma unroll
+        for (int u = 0; u < U; ++u) d = d && cls[r0 + u] == kDense;
+        return d;
+    };
+    const double* cbase = C + i0 * ldc;
+    // one dense group: t = rows r0..r0+U-1 (already loaded), all K steps, store.
+    // Coefficients in chunks of LC steps x U rows (16 doubles = 32 SGPRs), double
+    // buffered: scalar loads return out of order, so a chunk is waited for (lgkmcnt(0))
+    // BEFORE the next chunk's loads are issued, and those then land while the current
+    // chunk's fmas run.  sched_barriers keep the compiler from re-merging the two.
+    constexpr int LC = (16 / U) < K ? (16 / U) : K;
+    auto fetch = [&](double (&f)[U][LC], cdptr cb, int l0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int l = 0; l < LC; ++l) f[u][l] = cb[u * ldc + l0 + l];
+    };
+    auto chain = [&](double (&t)[U][V], const double (&f)[U][LC], int l0) {
+#pragma unroll
+        for (int l = 0; l < LC; ++l)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < V; ++e)
+                    t[u][e] = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
+    };
+    // the chunk holding step kb-1 of a partial block: steps >= kb are skipped
+    auto chain_part = [&](double (&t)[U][V], const double (&f)[U][LC], int l0) {
+#pragma unroll
+        for (int l = 0; l < LC; ++l)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    const double v = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
+                    t[u][e] = (l0 + l < kb) ? v : t[u][e];
+                }
+    };
+    auto group = [&](double (&t)[U][V], int r0) {
+        const cdptr cb = (cdptr)(cbase + (int64_t)r0 * ldc);
+        if constexpr (!PART) {
+            double fa[U][LC], fb[U][LC];
+            fetch(fa, cb, 0);
+#pragma unroll
+            for (int l0 = 0; l0 < K; l0 += 2 * LC) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): chunk fa has landed
+                if (l0 + LC < K) fetch(fb, cb, l0 + LC);
+                __builtin_amdgcn_sched_barrier(0);
+                chain(t, fa, l0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (l0 + LC < K) {
+                    __builtin_amdgcn_s_waitcnt(0xC07F);   // chunk fb has landed
+                    if (l0 + 2 * LC < K) fetch(fa, cb, l0 + 2 * LC);
+                    __builtin_amdgcn_sched_barrier(0);
+                    chain(t, fb, l0 + LC);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        } else {   // partial block (the end of a run window): whole chunks, then the rest
+#pragma unroll
+            for (int l0 = 0; l0 < K; l0 += LC) {
+                if (l0 < kb) {
+                    double f[U][LC];
+                    fetch(f, cb, l0);
+                    if (l0 + LC <= kb)
+                        chain(t, f, l0);
+                    else
+                        chain_part(t, f, l0);
+                }
+            }
+        }
+        if (colok)
+#pragma unroll
+            for (int u = 0; u < U; ++u) strow<NT, V>(T + (i0 + r0 + u) * ld + j, t[u]);
+    };
+    auto load = [&](double (&t)[U][V], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) ldrow<NT, V>(t[u], T + (i0 + r0 + u) * ld + jc);
+    };
+    double ta[U][V], tb[U][V];
+    int r = 0;
+    while (r < nr) {
+        if (dense_at(r)) {
+            // a run of dense groups, ping-ponging two register buffers
+            load(ta, r);
+            // The prefetch is unconditional (at the end of a run it re-reads the current
+            // group's rows, an L2 hit), so the in-order vmcnt wait for the group being
+            // computed is the same on every path and leaves the prefetch in flight.
+            while (true) {
+                const bool nb = dense_at(r + U);
+                load(tb, nb ? r + U : r);
+                __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the chains
+                group(ta, r);
+                r += U;
+                if (!nb) break;
+                const bool na = dense_at(r + U);
+                load(ta, na ? r + U : r);
+                __builtin_amdgcn_sched_barrier(0);
+                group(tb, r);
+                r += U;
+                if (!na) break;
+            }
+            continue;
+        }
+        // generic replay, one row (sparse rows, the block's pivot rows, partial blocks): a
+        // runtime loop over the steps with P[l] re-read from L2, so that the unrolled
+        // register copy serves only the dense path
+        const int c = cls[r];
+        if (c != kUntouched) {
+            double* row = T + (i0 + r) * ld;
+            const double* cr = C + (i0 + r) * ldc;
+            double t[V];
+            int l = 0;
+            if (c >= 0) {
+                ldrow<false, V>(t, P + (int64_t)c * ld + jc);
+                l = c + 1;
+            } else {
+                ldrow<NT, V>(t, row + jc);
+            }
+            for (; l < kb; ++l) {
+                const double f = cr[l];
+                if (f != 0.0) {
+                    double pv[V];
+                    ldrow<false, V>(pv, P + (int64_t)l * ld + jc);
+#pragma unroll
+                    for (int e = 0; e < V; ++e) t[e] = __builtin_fma(-f, pv[e], t[e]);
+                }
+            }
+            if (colok) strow<NT, V>(row + j, t);
+        }
+        r += 1;
+    }
+}
+
 __global__ void blk_reset_kernel(DevState* st) {
     if (threadIdx.x == 0) st->blk = 0;
 }
@@ -476,7 +688,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     ratio_defer_kernel<<<nblocks, kRatioThreads, 0, s>>>(
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc,
-        d.P, d.rhs, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap);
+        d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap);
     return hipGetLastError();
 }
 
@@ -502,10 +714,10 @@ hipError_t launch_commit_defer(const Geometry& g, const Defer& d, const DevState
 template <bool NT, int K>
 static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
                        hipStream_t s) {
-    const int cols = d.form == 0 ? kDeferTile : 256;
+    const int cols = (d.form == 0 || d.form == 4) ? kDeferTile : 256;
     const int ntiles = (int)((g.width + cols - 1) / cols);
     const int64_t bands = (g.rows + rb - 1) / rb;
-    size_t dyn = (size_t)K * rb * sizeof(double) + (size_t)rb * sizeof(int32_t);
+    size_t dyn = d.form >= 3 ? 0 : (size_t)K * rb * sizeof(double) + (size_t)rb * sizeof(int32_t);
     if (dyn > 160 * 1024) return hipErrorInvalidValue;
     if (occ > 0) {   // reserve LDS so that at most `occ` workgroups fit on a CU (160 KiB)
         const size_t cap = (size_t)160 * 1024 / occ - 1024;
@@ -519,7 +731,26 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
                                                           d.ldc, d.P, rb);
             else
                 return hipErrorInvalidValue;
-        } else if (d.form == 1)
+        } else if (d.form == 3) {
+            pass_s_kernel<NT, K, 1, 4, false><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
+                                                                     d.C, d.ldc, d.P, d.nzc, rb);
+            pass_s_kernel<NT, K, 1, 4, true><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
+                                                                    d.C, d.ldc, d.P, d.nzc, rb);
+        } else if (d.form == 4) {
+            if constexpr (K <= 32) {
+                pass_s_kernel<NT, K, 2, 2, false><<<grid, 256, dyn, s>>>(
+                    g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
+                    g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+            } else
+                return hipErrorInvalidValue;
+        } else if (d.form == 5) {
+            pass_s_kernel<NT, K, 1, 8, false><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
+                                                                     d.C, d.ldc, d.P, d.nzc, rb);
+            pass_s_kernel<NT, K, 1, 8, true><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
+                                                                    d.C, d.ldc, d.P, d.nzc, rb);
+        }
+        else if (d.form == 1)
             pass1_kernel<NT, K, 2><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st, d.C,
                                                           d.ldc, d.P, rb);
         else

@@ -80,8 +80,11 @@ struct Defer {
     int64_t ldc = 0;       // = K (row `rows` = the objective row's entries)
     double* P = nullptr;   // K x ld: normalised pivot rows
     double* rhs = nullptr; // rows: current RHS column (eager cache)
-    int form = 2;          // pass kernel: 0 = 2 doubles/lane, 1 = 1 double/lane x 2 rows,
-                           // 2 = 1 double/lane x 4 rows (default)
+    int32_t* nzc = nullptr; // rows: nonzero C[i][l] of the block so far (the pass's row class)
+    int form = 3;          // pass kernel, LDS-staged coefficients: 0 = 2 doubles/lane,
+                           // 1 = 1 double/lane x 2 rows, 2 = 1 double/lane x 4 rows;
+                           // scalar-coefficient forms: 3 = 1 double x 4 rows (default),
+                           // 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows
 };
 
 // Launchers (dlp_kernels.hip).  All asynchronous on `stream`.

@@ -107,7 +107,7 @@ struct dlp_session {
     // the last tableau pass, pass geometry; update-kernel launch accounting
     dlp::Defer d;
     int since_flush = 0;
-    int defer_rb = 64, defer_occ = 4;
+    int defer_rb = 64, defer_occ = 0;   // pass band rows (128 when streaming), WG/CU cap
     std::vector<uint8_t> ev_flush;   // per timed slot: a pass ran in it
     int64_t upd_launches = 0;
 };
@@ -197,7 +197,7 @@ void free_session(dlp_session* s) {
     for (auto e : s->ev) (void)hipEventDestroy(e);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     void* dev[] = {s->T, s->colq, s->prow_send, s->partials, s->cand_send, s->cand_recv,
-                   s->pp, s->basis, s->st, s->log, s->d.C, s->d.P, s->d.rhs};
+                   s->pp, s->basis, s->st, s->log, s->d.C, s->d.P, s->d.rhs, s->d.nzc};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
@@ -298,7 +298,8 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     }
     const int tile = dlp::update_tile(opt->update_variant);
     g.ntiles = (int)((s->width + tile - 1) / tile);
-    // deferred rank-k update: auto = 16 pivots per tableau pass; eager when the
+    // deferred rank-k update: auto = 32 pivots per tableau pass on a streaming
+    // (HBM-resident) tableau, 16 on a cache-resident one; eager when the
     // caller drives the exchange itself (dlp_session_step_*) or when the chosen
     // rank-1 variant tiles pricing differently from the deferred kernels
     {
@@ -308,9 +309,13 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
             set_error("defer must be 0 (auto) or 1..64");
             return DLP_ERR_ARG;
         }
-        if (K == 0) K = (host_driven || tile != dlp::kDeferTile) ? 1 : 16;
-        if (K > 1 && (host_driven || tile != dlp::kDeferTile)) {
-            set_error("defer > 1 needs dlp_session_run (not the step API) and a 512-column update variant");
+        if (K == 0) K = (host_driven || tile != dlp::kDeferTile) ? 1 : (s->streaming ? 32 : 16);
+        if (K > 1 && tile != dlp::kDeferTile) {
+            set_error("defer > 1 needs a 512-column update variant");
+            return DLP_ERR_ARG;
+        }
+        if (K > 1 && host_driven && s->general) {
+            set_error("a host-driven (step API) general-LP session is eager: create it with defer = 1");
             return DLP_ERR_ARG;
         }
         s->d.K = K;
@@ -347,9 +352,11 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         HIP_TRY(hipMalloc(&s->d.C, sizeof(double) * s->d.K * (rows_total + 1)));
         HIP_TRY(hipMalloc(&s->d.P, sizeof(double) * s->d.K * s->ld));
         HIP_TRY(hipMalloc(&s->d.rhs, sizeof(double) * (s->rows + 1)));
+        HIP_TRY(hipMalloc(&s->d.nzc, sizeof(int32_t) * (s->rows + 1)));
         HIP_TRY(hipMemsetAsync(s->d.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
         HIP_TRY(hipMemsetAsync(s->d.P, 0, sizeof(double) * s->d.K * s->ld, s->stream));
-        if (opt->rows_per_block > 0) s->defer_rb = std::min(opt->rows_per_block, 1024);
+        s->defer_rb = opt->rows_per_block > 0 ? std::min(opt->rows_per_block, 1024)
+                                              : (s->streaming ? 128 : 64);
     }
     HIP_TRY(hipMemsetAsync(s->prow_send, 0, sizeof(int64_t) * s->ld, s->stream));
 
@@ -1094,14 +1101,50 @@ int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
 // Caller-driven steps.  A general LP's Phase I -> II switch is carried by the
 // same three-step exchange: forced drive-out pivots, then one carry step
 // (its candidate is an empty slot, its "pivot row" the carried objective row).
+// Deferred sessions under the step API: the same kernels as enqueue_pivot_defer,
+// with the two exchanges done by the caller between the calls.
+int step_candidate_defer(dlp_session* s) {
+    const dlp_options& o = s->opt;
+    s->step_kind = dlp_session::STEP_PIVOT;
+    HIP_TRY(dlp::launch_ratio_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
+                                    s->ratio_blocks, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
+                                    o.tol_piv, o.pricing, s->log, s->log_cap, s->stream));
+    return DLP_OK;
+}
+
+int step_select_defer(dlp_session* s) {
+    const dlp_options& o = s->opt;
+    if (s->exchange)
+        HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, o.pricing,
+                                   s->log, s->log_cap, s->stream, false, true));
+    HIP_TRY(dlp::launch_prow_defer(s->g, s->d, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
+                                   s->log_cap, s->exchange ? 2 : 1, s->stream));
+    return DLP_OK;
+}
+
+int step_update_defer(dlp_session* s) {
+    const dlp_options& o = s->opt;
+    if (s->exchange)
+        HIP_TRY(dlp::launch_commit_defer(s->g, s->d, s->st, s->prow_recv, s->pp, o.tol_dj, s->log,
+                                         s->log_cap, s->stream));
+    s->since_flush += 1;
+    s->launched += 1;
+    if (s->since_flush >= s->d.K) CALL_TRY(enqueue_flush(s));
+    return DLP_OK;
+}
+
+// Before anything reads the tableau: apply the pending steps of a deferred block
+// (the step API leaves a partial block pending when the caller stops).
+int flush_pending(dlp_session* s) {
+    if (s->d.K > 1 && s->since_flush > 0) CALL_TRY(enqueue_flush(s));
+    return DLP_OK;
+}
+
 int dlp_session_step_candidate(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
-    if (s->d.K > 1) {
-        set_error("the step API drives eager sessions only: create the session with defer = 1");
-        return DLP_ERR_STATE;
-    }
     HIP_TRY(hipSetDevice(s->device));
     s->step_void = false;
+    if (s->d.K > 1) return step_candidate_defer(s);
     if (s->drive_next < s->drive.size()) {
         s->step_kind = dlp_session::STEP_FORCED;
         return enqueue_forced_candidate(s, s->drive[s->drive_next++]);
@@ -1119,6 +1162,7 @@ int dlp_session_step_select(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
     if (s->step_void) return DLP_OK;
+    if (s->d.K > 1) return step_select_defer(s);
     switch (s->step_kind) {
         case dlp_session::STEP_FORCED: return enqueue_forced_select(s);
         case dlp_session::STEP_CARRY: return enqueue_carry_out(s);
@@ -1132,6 +1176,7 @@ int dlp_session_step_update(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
     if (s->step_void) return DLP_OK;
+    if (s->d.K > 1) return step_update_defer(s);
     if (s->step_kind == dlp_session::STEP_CARRY) {
         CALL_TRY(enqueue_carry_in(s));
         return finish_phase1(s);
@@ -1208,7 +1253,7 @@ int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_bloc
             set_error("a deferred session (defer > 1) needs a 512-column update variant");
             return DLP_ERR_ARG;
         }
-        s->defer_rb = rows_per_block > 0 ? std::min(rows_per_block, 1024) : 64;
+        s->defer_rb = rows_per_block > 0 ? std::min(rows_per_block, 1024) : (s->streaming ? 128 : 64);
     }
     s->opt.update_variant = update_variant;
     s->opt.nontemporal = nontemporal;
@@ -1234,8 +1279,8 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
 }
 
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
-    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 2) return DLP_ERR_ARG;
-    if (form == 0 && s->d.K > 32) {
+    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 5) return DLP_ERR_ARG;
+    if ((form == 0 || form == 4) && s->d.K > 32) {
         set_error("the 2-doubles-per-lane pass holds at most 32 steps");
         return DLP_ERR_ARG;
     }
@@ -1275,6 +1320,7 @@ int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, in
 int dlp_session_tableau(dlp_session* s, double* host) {
     if (!s || !host) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
+    CALL_TRY(flush_pending(s));
     HIP_TRY(hipMemcpyAsync(host, s->T, sizeof(double) * (s->rows + 1) * s->ld,
                            hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1284,6 +1330,7 @@ int dlp_session_tableau(dlp_session* s, double* host) {
 int dlp_session_read_rows(dlp_session* s, int64_t first, int64_t count, double* host) {
     if (!s || !host || first < 0 || count < 0 || first + count > s->rows + 1) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
+    CALL_TRY(flush_pending(s));
     HIP_TRY(hipMemcpyAsync(host, s->T + first * s->ld, sizeof(double) * count * s->ld,
                            hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1292,6 +1339,8 @@ int dlp_session_read_rows(dlp_session* s, int64_t first, int64_t count, double* 
 
 int dlp_session_result(dlp_session* s, dlp_result** out) {
     if (!s || !out) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    CALL_TRY(flush_pending(s));
     auto* r = new (std::nothrow) dlp_result();
     if (!r) return DLP_ERR_OOM;
     int rc = extract_result(s, r);

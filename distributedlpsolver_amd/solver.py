@@ -292,7 +292,8 @@ class Session:
         return n.value, ms.value, k.value
 
     def set_defer_tuning(self, occupancy: int, form: int = -1):
-        """Deferred pass: workgroups/CU cap (0 = none) and form (0 wide, 1/2 narrow x 2/4 rows)."""
+        """Deferred pass: workgroups/CU cap (0 = none) and form (0 wide, 1/2 narrow x 2/4 rows;
+        scalar-coefficient 3 = 1 double x 4 rows, 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows)."""
         L.check(L.lib().dlp_session_set_defer_tuning(self._h, occupancy, form),
                 "dlp_session_set_defer_tuning")
 

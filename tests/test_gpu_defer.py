@@ -53,7 +53,10 @@ def test_defer_degenerate_bland(K, pricing):
 
 @pytest.mark.parametrize("K,rb,occ,nt,form", [(16, 16, 0, 0, 0), (16, 64, 4, 1, 0), (16, 256, 2, 1, 1),
                                               (32, 128, 3, 0, 0), (8, 7, 6, 1, 2), (32, 64, 4, 1, 2),
-                                              (64, 64, 0, 1, 2), (64, 33, 4, 0, 1), (5, 64, 4, 1, 2)])
+                                              (64, 64, 0, 1, 2), (64, 33, 4, 0, 1), (5, 64, 4, 1, 2),
+                                              (16, 64, 0, 1, 3), (32, 37, 4, 0, 3), (64, 64, 2, 1, 3),
+                                              (8, 16, 0, 1, 4), (32, 100, 4, 1, 4), (13, 64, 0, 0, 4),
+                                              (16, 64, 0, 1, 5), (48, 29, 0, 1, 5), (64, 256, 4, 0, 5)])
 def test_defer_pass_geometry_and_tableau(K, rb, occ, nt, form):
     """Whole tableau after 45 pivots equals the eager session's, byte for byte."""
     m, n, seed = 300, 520, 5
@@ -77,7 +80,7 @@ def test_defer_retune_between_runs():
     with dlp.Session(dlp.Problem.dense(A, b, c), defer=16, check_interval=9) as s:
         for k in range(1000):
             s.set_tuning(22 if k % 2 else 26, [16, 64, 200][k % 3], k % 2)
-            s.set_defer_tuning([0, 4, 2][k % 3], k % 3)
+            s.set_defer_tuning([0, 4, 2][k % 3], k % 6)
             st, _ = s.run(11)
             if st != L.RUNNING:
                 break
@@ -85,12 +88,17 @@ def test_defer_retune_between_runs():
     _check(res, ref)
 
 
-def test_defer_adalloc_sparse_rows():
+@pytest.mark.parametrize("form", [2, 3, 4, 5])
+def test_defer_adalloc_sparse_rows(form):
     """Sparse tableau: most rows untouched by most steps (skip rule in the pass)."""
     p = dlp.Problem.adalloc(200, 200, 1, 0.1, 0.25)
     M, b, c = O.adalloc_lp(200, 200, 0.1, 0.25)
     ref = O.solve_dense(M, b, c)
-    _check(dlp.solve(p, defer=16), ref)
+    with dlp.Session(p, defer=16) as s:
+        s.set_defer_tuning(0, form)
+        s.run(10 ** 6)
+        res = s.result()
+    _check(res, ref)
 
 
 def test_defer_rejects_bad_settings():
@@ -101,8 +109,6 @@ def test_defer_rejects_bad_settings():
         dlp.solve(dlp.Problem.dense(A, b, c), defer=8, update_variant=4)   # 1024-column tiles
     with dlp.Session(dlp.Problem.dense(A, b, c), defer=8) as s:
         with pytest.raises(L.DLPError):
-            s.step_candidate()
-        with pytest.raises(L.DLPError):
             s.set_tuning(4, 8, 1)
 
 
@@ -111,3 +117,46 @@ def test_defer_update_stats():
         s.run(40)
         n, ms, k = s.update_stats()
     assert k == 8 and n == 5 and ms > 0
+
+
+@pytest.mark.parametrize("P,K", [(1, 8), (2, 4), (2, 16), (3, 32)])
+def test_defer_step_api_multi_rank_one_gpu(P, K):
+    """The deferred exchange path (ratio -> candidate all-gather -> select ->
+    pivot-row MAX all-reduce -> commit, pass every K pivots) with P row-block
+    sessions on one GPU and the host doing the exchanges: the same pivot log,
+    objective, x and y as the oracle.  This is the device code the RCCL path of
+    bench.py --gpus N runs."""
+    m, n, seed = 150, 170, 4
+    A, b, c = O.gen_dense(m, n, seed)
+    ref = O.solve_dense(A, b, c)
+    prob = dlp.Problem.random(m, n, seed)
+    sess = [dlp.Session(prob, rank=r, nranks=P, defer=K) for r in range(P)]
+    assert all(s.update_stats()[2] == K for s in sess)
+    status = L.RUNNING
+    for _ in range(10_000):
+        cands = np.concatenate([s.step_candidate() for s in sess])
+        st, _ = sess[0].status()
+        if st != L.RUNNING:
+            status = st
+            break
+        sends = [s.step_select(cands) for s in sess]
+        prow = np.max(np.stack(sends), axis=0)
+        for s in sess:
+            s.step_update(prow)
+    assert status == L.OK
+    results = [s.result() for s in sess]
+    for r in results:
+        _same_log(r.pivot_log, ref.pivot_log)
+        assert np.float64(r.objective).tobytes() == np.float64(ref.objective).tobytes()
+        np.testing.assert_array_equal(r.y, ref.y)
+    x = np.sum([r.x for r in results], axis=0)
+    assert x.tobytes() == ref.x.tobytes()
+    # the stacked local tableaus equal the eager single-rank tableau after the same pivots
+    with dlp.Session(prob, defer=1) as e:
+        e.run(10 ** 6)
+        Te = e.tableau()
+    rows = [s.tableau()[:-1] for s in sess]
+    Td = np.concatenate(rows + [sess[0].tableau()[-1:]])
+    assert Td.tobytes() == Te.tobytes()
+    for s in sess:
+        s.close()

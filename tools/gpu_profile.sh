@@ -12,7 +12,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
     python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/trace_bench.json 2> $OUT/trace.err || exit $?
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
-    python3 $R/bench.py --no-cpu-baseline --steps 4 --warmup 1 "$@" > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err || exit $?
+    python3 $R/bench.py --no-cpu-baseline --steps 32 --warmup 16 "$@" > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err || exit $?
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
-    python3 $R/bench.py --no-cpu-baseline --steps 4 --warmup 1 "$@" > $OUT/pmc_write.json 2> $OUT/pmc_write.err || exit $?
+    python3 $R/bench.py --no-cpu-baseline --steps 32 --warmup 16 "$@" > $OUT/pmc_write.json 2> $OUT/pmc_write.err || exit $?
 echo "profile $TAG done"

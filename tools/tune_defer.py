@@ -45,7 +45,7 @@ any_s = next(iter(sess.values()))
 bytes_pass = 16.0 * any_s.rows * (any_s.ncols + 1)
 cfgs = [(K, rb, occ, nt, fm) for K in sess for rb in map(int, a.rbs.split(","))
         for occ in map(int, a.occs.split(",")) for nt in map(int, a.nts.split(","))
-        for fm in map(int, a.forms.split(",")) if not (fm == 0 and K > 32)]
+        for fm in map(int, a.forms.split(",")) if not (fm in (0, 4) and K > 32)]
 res = {c: {"wall": [], "pass": []} for c in cfgs}
 rng = random.Random(0)
 for r in range(a.rounds):
