@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--nontemporal", type=int, default=-1, help="-1 = auto")
     ap.add_argument("--variant", type=int, default=-1, help="update-kernel variant, -1 = auto")
     ap.add_argument("--ld-align", type=int, default=0, help="row alignment (doubles), 0 = auto")
-    ap.add_argument("--timing", type=int, default=2)
+    ap.add_argument("--timing", type=int, default=1,
+                    help="1 = HIP events around the update/pass launches only, 2 = every phase")
     ap.add_argument("--defer", type=int, default=0,
                     help="pivots per tableau pass (1 = eager rank-1 per pivot, 0 = auto)")
     ap.add_argument("--occupancy", type=int, default=-1, help="pass workgroups/CU cap (-1 = default)")
@@ -169,7 +170,7 @@ def main():
     # algorithmic bytes of one launch: one read + one write of every resident element
     # (the deferred pass skips the objective row, kept current by the pivot-row kernel)
     bytes_launch = 16.0 * (rows_local + (1 if defer == 1 else 0)) * N1
-    achieved = bytes_launch / (upd_ms * 1e-3) / 1e9
+    achieved = bytes_launch / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else None   # timing 0: untimed
 
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -207,12 +208,13 @@ def main():
                        "parallelism": f"rowblock{world}", "pricing": "dantzig->bland on degeneracy",
                        "pivots_per_tableau_pass": defer},
             "achieved_hbm_gbs": achieved,
-            "phases_ms_per_pivot": {"ratio": tm[0] / max(nsamp, 1), "exchange": tm[1] / max(nsamp, 1),
-                                    "prow": tm[2] / max(nsamp, 1), "update": tm[3] / max(nsamp, 1)},
+            "phases_ms_per_pivot": ({"ratio": tm[0] / max(nsamp, 1), "exchange": tm[1] / max(nsamp, 1),
+                                     "prow": tm[2] / max(nsamp, 1), "update": tm[3] / max(nsamp, 1)}
+                                    if args.timing >= 2 else None),
             "update_launches": launches,
             "objective_after_window": res.objective,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
+                         "frac": achieved / HBM_PEAK_GBS if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "kernel": (f"rank-1 update variant {variant} (rows/band {rb_used}, "

@@ -395,7 +395,6 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         s->use_rccl = true;
     }
     s->ev_per_pivot = opt->timing == 1 ? 2 : (opt->timing >= 2 ? 5 : 0);
-    if (s->ev_per_pivot && s->d.K > 1) s->ev_per_pivot = 5;   // the pass is timed per slot
     if (s->ev_per_pivot) {
         s->ev.resize((size_t)s->ev_per_pivot * opt->check_interval);
         for (auto& e : s->ev) HIP_TRY(hipEventCreate(&e));
@@ -446,7 +445,9 @@ int enqueue_flush(dlp_session* s) {
 // objective row and pricing), and the pass when the block is full or `last`.
 int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
     const dlp_options& o = s->opt;
-    hipEvent_t* ev = s->ev_per_pivot ? &s->ev[(size_t)slot * s->ev_per_pivot] : nullptr;
+    // timing 2: 5 events per pivot (every phase); timing 1: 2 events around the pass only
+    hipEvent_t* ev = s->ev_per_pivot == 5 ? &s->ev[(size_t)slot * 5] : nullptr;
+    hipEvent_t* evp = s->ev_per_pivot == 2 ? &s->ev[(size_t)slot * 2] : nullptr;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s->stream));
     HIP_TRY(dlp::launch_ratio_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
                                     s->ratio_blocks, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
@@ -470,11 +471,11 @@ int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
     if (ev) HIP_TRY(hipEventRecord(ev[3], s->stream));
     s->since_flush += 1;
     const bool flush = last || s->since_flush >= s->d.K;
+    if (flush && evp) HIP_TRY(hipEventRecord(evp[0], s->stream));
     if (flush) CALL_TRY(enqueue_flush(s));
-    if (ev) {
-        HIP_TRY(hipEventRecord(ev[4], s->stream));
-        s->ev_flush[slot] = flush ? 1 : 0;
-    }
+    if (flush && evp) HIP_TRY(hipEventRecord(evp[1], s->stream));
+    if (ev) HIP_TRY(hipEventRecord(ev[4], s->stream));
+    if (ev || evp) s->ev_flush[slot] = flush ? 1 : 0;
     return DLP_OK;
 }
 
@@ -605,8 +606,11 @@ int poll(dlp_session* s) {
             hipEvent_t* ev = &s->ev[(size_t)k * s->ev_per_pivot];
             float ms = 0.f;
             if (s->ev_per_pivot == 2) {
-                HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
-                s->timings[DLP_PHASE_UPDATE] += ms;
+                // deferred: only slots that ended with a pass recorded their events
+                if (s->d.K <= 1 || s->ev_flush[k]) {
+                    HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+                    s->timings[DLP_PHASE_UPDATE] += ms;
+                }
             } else {
                 for (int ph = 0; ph < 4; ++ph) {
                     HIP_TRY(hipEventElapsedTime(&ms, ev[ph], ev[ph + 1]));
