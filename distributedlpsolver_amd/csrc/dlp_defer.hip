@@ -64,14 +64,14 @@ __device__ inline void stv(double* p, d2 v) {
 // T0[i][q]; C[j][i] = a; the RHS cache advances by step j-1 (or is read from
 // T0 when the block is empty); then the ratio candidate.  The objective row
 // (local index rows) is current in place: C[j][rows] = z_q.
-__global__ __launch_bounds__(kRatioThreads) void ratio_defer_kernel(
+__global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
     DevState* st, double* __restrict__ C, int64_t ldc, const double* __restrict__ P,
     double* __restrict__ rhs, int32_t* __restrict__ nzc, Cand* partials, Cand* cand_out,
     int nranks, double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap) {
-    __shared__ PricePart lds_pp[4];
-    __shared__ Cand lds_c[4];
+    __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
+    __shared__ Cand lds_c[kRatioDeferThreads / 64];
     __shared__ int s_last;
     __shared__ double s_pq[kMaxDefer], s_pn[kMaxDefer];
     __shared__ int32_t s_pl[kMaxDefer];
@@ -681,12 +681,18 @@ __global__ void blk_reset_kernel(DevState* st) {
 
 }  // namespace
 
+int ratio_defer_blocks(const Geometry& g) {
+    return (int)((g.rows + 1 + kRatioDeferThreads - 1) / kRatioDeferThreads);
+}
+
 hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               const PricePart* pp, DevState* st, Cand* partials, int nblocks,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
-    ratio_defer_kernel<<<nblocks, kRatioThreads, 0, s>>>(
+    if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
+    nblocks = ratio_defer_blocks(g);
+    ratio_defer_kernel<<<nblocks, kRatioDeferThreads, 0, s>>>(
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc,
         d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap);
     return hipGetLastError();

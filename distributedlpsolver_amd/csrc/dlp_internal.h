@@ -15,6 +15,7 @@ constexpr int kUpdThreads = 256;
 constexpr int kUpdVec = 2;
 constexpr int kUpdTile = kUpdThreads * kUpdVec;   // doubles per column tile
 constexpr int kRatioThreads = 256;
+constexpr int kRatioDeferThreads = 256;  // deferred ratio test (64 and 512 measured slower)
 constexpr int kProwThreads = 256;
 constexpr int32_t kNoIndex = 0x7fffffff;
 constexpr int kColqPad = 16;   // colq allocated with rows + 1 + kColqPad entries
@@ -114,6 +115,7 @@ hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* bas
                         int nblocks, Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                         int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s);
 int ratio_blocks(const Geometry& g);
+int ratio_defer_blocks(const Geometry& g);
 hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32_t* basis,
                          DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
                          hipStream_t s, bool forced = false, bool track = false);

@@ -64,6 +64,7 @@ struct dlp_session {
     int64_t* prow_recv = nullptr;   // == prow_send when nranks == 1
     dlp::Cand* partials = nullptr;
     int ratio_blocks = 0;
+    int ratio_blocks_max = 0;       // partials capacity (eager or deferred ratio kernel)
     dlp::Cand* cand_send = nullptr;
     dlp::Cand* cand_recv = nullptr;
     dlp::PricePart* pp = nullptr;
@@ -330,6 +331,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     }
     g.T = s->T;
     s->ratio_blocks = dlp::ratio_blocks(g);
+    s->ratio_blocks_max = std::max(s->ratio_blocks, dlp::ratio_defer_blocks(g));
     HIP_TRY(hipMalloc(&s->colq, sizeof(double) * (rows_total + dlp::kColqPad)));
     HIP_TRY(hipMemsetAsync(s->colq, 0, sizeof(double) * (rows_total + dlp::kColqPad), s->stream));
     s->exchange = nranks > 1 || uid != nullptr;
@@ -338,7 +340,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         HIP_TRY(hipMalloc(&s->prow_recv, sizeof(int64_t) * s->ld));
     else
         s->prow_recv = s->prow_send;
-    HIP_TRY(hipMalloc(&s->partials, sizeof(dlp::Cand) * s->ratio_blocks));
+    HIP_TRY(hipMalloc(&s->partials, sizeof(dlp::Cand) * s->ratio_blocks_max));
     HIP_TRY(hipMalloc(&s->cand_send, sizeof(dlp::Cand)));
     HIP_TRY(hipMalloc(&s->cand_recv, sizeof(dlp::Cand) * nranks));
     HIP_TRY(hipMalloc(&s->pp, sizeof(dlp::PricePart) * ((s->ld + 511) / 512)));
@@ -450,7 +452,7 @@ int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
     hipEvent_t* evp = s->ev_per_pivot == 2 ? &s->ev[(size_t)slot * 2] : nullptr;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s->stream));
     HIP_TRY(dlp::launch_ratio_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
-                                    s->ratio_blocks, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
+                                    s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
                                     o.tol_piv, o.pricing, s->log, s->log_cap, s->stream));
     if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
     if (s->exchange) {
@@ -1111,7 +1113,7 @@ int step_candidate_defer(dlp_session* s) {
     const dlp_options& o = s->opt;
     s->step_kind = dlp_session::STEP_PIVOT;
     HIP_TRY(dlp::launch_ratio_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
-                                    s->ratio_blocks, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
+                                    s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
                                     o.tol_piv, o.pricing, s->log, s->log_cap, s->stream));
     return DLP_OK;
 }
