@@ -40,8 +40,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
+    # defaults are whole deferred blocks (K = 32 at C3): a window that ends mid-block pays a
+    # full tableau pass for its last few pivots (run() leaves the tableau current), so a
+    # 200-pivot window measures 7 passes for 6.25 blocks of work
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-pivots", type=int, default=60)

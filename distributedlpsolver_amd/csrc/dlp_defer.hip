@@ -77,6 +77,35 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     __shared__ int32_t s_pl[kMaxDefer];
     if (st->status != DLP_RUNNING) return;
 
+    // Everything that does not depend on q is requested before the pricing reduce,
+    // so those loads are in flight while the partials are combined: the replay
+    // chain's first 8 coefficients (preloading 32 measured slower), the RHS inputs, the basis entry, the step
+    // tables.  Only T0[i][q] and P[l][q] wait for q.
+    const int j = st->blk;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int l = threadIdx.x; l < j; l += blockDim.x) {
+        s_pn[l] = P[(int64_t)l * ld + ncols];
+        s_pl[l] = st->pl[l];
+    }
+    constexpr int kPre = 8;    // C[i][0..kPre), index clamped into the row (so no guard)
+    double f0[kPre];
+    double r_in = 0.0, f_prev = 0.0;
+    int32_t nz_in = 0, bvar = 0;
+    if (i < rows && j > 0) {
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) f0[u] = C[i * ldc + min(u, j - 1)];
+        nz_in = nzc[i];
+    }
+    if (i < rows_elig) {
+        if (j == 0) {
+            r_in = T[i * ld + ncols];
+        } else {
+            r_in = rhs[i];
+            f_prev = C[i * ldc + (j - 1)];
+        }
+        bvar = basis[row_first + i];
+    }
+
     PricePart acc = pp_empty();
     for (int k = threadIdx.x; k < ntiles; k += blockDim.x) pp_combine(acc, pp[k]);
     acc = block_price(acc, lds_pp);
@@ -93,42 +122,50 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
         return;
     }
 
-    const int j = st->blk;
-    for (int l = threadIdx.x; l < j; l += blockDim.x) {
-        s_pq[l] = P[(int64_t)l * ld + q];
-        s_pn[l] = P[(int64_t)l * ld + ncols];
-        s_pl[l] = st->pl[l];
-    }
+    for (int l = threadIdx.x; l < j; l += blockDim.x) s_pq[l] = P[(int64_t)l * ld + q];
     __syncthreads();
 
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     Cand c = cand_empty();
     if (i <= rows) {
         double a = T[i * ld + q];
-        if (i < rows)
-            for (int l = 0; l < j; ++l) {
-                if (i == s_pl[l]) {
-                    a = s_pq[l];
-                } else {
-                    const double f = C[i * ldc + l];
-                    if (f != 0.0) a = __builtin_fma(-f, s_pq[l], a);
+        if (i < rows) {
+            // steps 0..kPre-1 from the preloaded coefficients (unrolled: f0 stays in
+            // registers), then chunks of 8 whose loads are issued back to back
+#pragma unroll
+            for (int l = 0; l < kPre; ++l) {
+                if (l < j) {
+                    if (i == s_pl[l])
+                        a = s_pq[l];
+                    else if (f0[l] != 0.0)
+                        a = __builtin_fma(-f0[l], s_pq[l], a);
                 }
             }
-        C[i * ldc + j] = a;
-        if (i < rows) nzc[i] = (j == 0 ? 0 : nzc[i]) + (a != 0.0 ? 1 : 0);   // the pass's row class
-        if (i < rows_elig) {
-            double r;
-            if (j == 0) {
-                r = T[i * ld + ncols];
-            } else {
-                const int l = j - 1;
-                r = rhs[i];
-                if (i == s_pl[l]) {
-                    r = s_pn[l];
-                } else {
-                    const double f = C[i * ldc + l];
-                    if (f != 0.0) r = __builtin_fma(-f, s_pn[l], r);
+            for (int l0 = kPre; l0 < j; l0 += 8) {
+                double f[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) f[u] = C[i * ldc + min(l0 + u, j - 1)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int l = l0 + u;
+                    if (l < j) {
+                        if (i == s_pl[l])
+                            a = s_pq[l];
+                        else if (f[u] != 0.0)
+                            a = __builtin_fma(-f[u], s_pq[l], a);
+                    }
                 }
+            }
+        }
+        C[i * ldc + j] = a;
+        if (i < rows) nzc[i] = (j == 0 ? 0 : nz_in) + (a != 0.0 ? 1 : 0);   // the pass's row class
+        if (i < rows_elig) {
+            double r = r_in;
+            if (j > 0) {
+                const int l = j - 1;
+                if (i == s_pl[l])
+                    r = s_pn[l];
+                else if (f_prev != 0.0)
+                    r = __builtin_fma(-f_prev, s_pn[l], r);
             }
             rhs[i] = r;
             if (a > tol_piv) {
@@ -136,7 +173,7 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
                 if (!(b > 0.0)) b = 0.0;
                 c.ratio = b / a;
                 c.row = (int32_t)(row_first + i);
-                c.basis_var = basis[row_first + i];
+                c.basis_var = bvar;
                 c.valid = 1;
                 c.pivot = a;
             }
@@ -232,13 +269,22 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     pr.y = 0.0;
     if (pl >= 0 && j < ld) {
         d2 t = *(const d2*)(T + (int64_t)pl * ld + j);
-        for (int l = 0; l < s; ++l) {
-            const d2 pv = *(const d2*)(P + (int64_t)l * ld + j);
-            if (pl == s_pl[l]) {
-                t = pv;
-            } else if (s_cp[l] != 0.0) {
-                t.x = __builtin_fma(-s_cp[l], pv.x, t.x);
-                t.y = __builtin_fma(-s_cp[l], pv.y, t.y);
+        // chunks of 8 pivot rows: loads issued back to back (row index clamped), then applied in order
+        for (int l0 = 0; l0 < s; l0 += 8) {
+            d2 pv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) pv[u] = *(const d2*)(P + (int64_t)min(l0 + u, s - 1) * ld + j);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int l = l0 + u;
+                if (l < s) {
+                    if (pl == s_pl[l]) {
+                        t = pv[u];
+                    } else if (s_cp[l] != 0.0) {
+                        t.x = __builtin_fma(-s_cp[l], pv[u].x, t.x);
+                        t.y = __builtin_fma(-s_cp[l], pv[u].y, t.y);
+                    }
+                }
             }
         }
         const double piv = st->piv;
@@ -500,12 +546,11 @@ __device__ inline void strow(double* p, const double (&t)[V]) {
 typedef __attribute__((address_space(4))) const double* cdptr;
 
 template <bool NT, int K, int V, int U, bool PART>
-__global__ __launch_bounds__(256) void pass_s_kernel(double* __restrict__ T, int64_t ld,
-                                                     int64_t rows, int64_t width,
-                                                     const DevState* __restrict__ st,
-                                                     const double* __restrict__ C, int64_t ldc,
-                                                     const double* __restrict__ P,
-                                                     const int32_t* __restrict__ nzc, int rb) {
+__device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, int64_t rows,
+                                            int64_t width, const DevState* __restrict__ st,
+                                            const double* __restrict__ C, int64_t ldc,
+                                            const double* __restrict__ P,
+                                            const int32_t* __restrict__ nzc, int rb) {
     __shared__ int32_t cls[1024];
     const int kb = st->blk;
     // two launches per pass: the full-block instance (kb == K) and the partial one
@@ -519,7 +564,8 @@ __global__ __launch_bounds__(256) void pass_s_kernel(double* __restrict__ T, int
 #pragma unroll
     for (int l = 0; l < K; ++l) {
         double v[V];
-        ldrow<false, V>(v, P + (int64_t)l * ld + jc);
+        // rows l >= kb are not used (and need not exist: P holds d.K <= K rows)
+        ldrow<false, V>(v, P + (int64_t)(l < kb ? l : 0) * ld + jc);
 #pragma unroll
         for (int e = 0; e < V; ++e) pr[l][e] = l < kb ? v[e] : 0.0;
     }
@@ -673,6 +719,16 @@ __global__ __launch_bounds__(256) void pass_s_kernel(double* __restrict__ T, int
         }
         r += 1;
     }
+}
+
+template <bool NT, int K, int V, int U, bool PART>
+__global__ __launch_bounds__(256) void pass_s_kernel(double* __restrict__ T, int64_t ld,
+                                                     int64_t rows, int64_t width,
+                                                     const DevState* __restrict__ st,
+                                                     const double* __restrict__ C, int64_t ldc,
+                                                     const double* __restrict__ P,
+                                                     const int32_t* __restrict__ nzc, int rb) {
+    pass_s_body<NT, K, V, U, PART>(T, ld, rows, width, st, C, ldc, P, nzc, rb);
 }
 
 __global__ void blk_reset_kernel(DevState* st) {

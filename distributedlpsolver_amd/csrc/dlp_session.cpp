@@ -352,11 +352,14 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     if (s->d.K > 1) {
         s->d.ldc = s->d.K;
         HIP_TRY(hipMalloc(&s->d.C, sizeof(double) * s->d.K * (rows_total + 1)));
-        HIP_TRY(hipMalloc(&s->d.P, sizeof(double) * s->d.K * s->ld));
+        // P is sized for the pass template's block (K rounded up to 4/8/16/32/64), so a
+        // kernel instance never addresses past it, whatever the session's K
+        const int64_t kt = s->d.K <= 4 ? 4 : s->d.K <= 8 ? 8 : s->d.K <= 16 ? 16 : s->d.K <= 32 ? 32 : 64;
+        HIP_TRY(hipMalloc(&s->d.P, sizeof(double) * kt * s->ld));
         HIP_TRY(hipMalloc(&s->d.rhs, sizeof(double) * (s->rows + 1)));
         HIP_TRY(hipMalloc(&s->d.nzc, sizeof(int32_t) * (s->rows + 1)));
         HIP_TRY(hipMemsetAsync(s->d.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
-        HIP_TRY(hipMemsetAsync(s->d.P, 0, sizeof(double) * s->d.K * s->ld, s->stream));
+        HIP_TRY(hipMemsetAsync(s->d.P, 0, sizeof(double) * kt * s->ld, s->stream));
         s->defer_rb = opt->rows_per_block > 0 ? std::min(opt->rows_per_block, 1024)
                                               : (s->streaming ? 128 : 64);
     }

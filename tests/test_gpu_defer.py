@@ -56,7 +56,9 @@ def test_defer_degenerate_bland(K, pricing):
                                               (64, 64, 0, 1, 2), (64, 33, 4, 0, 1), (5, 64, 4, 1, 2),
                                               (16, 64, 0, 1, 3), (32, 37, 4, 0, 3), (64, 64, 2, 1, 3),
                                               (8, 16, 0, 1, 4), (32, 100, 4, 1, 4), (13, 64, 0, 0, 4),
-                                              (16, 64, 0, 1, 5), (48, 29, 0, 1, 5), (64, 256, 4, 0, 5)])
+                                              (16, 64, 0, 1, 5), (48, 29, 0, 1, 5), (64, 256, 4, 0, 5),
+                                              (48, 64, 0, 1, 3), (24, 128, 0, 0, 3), (40, 64, 0, 1, 5),
+                                              (7, 64, 4, 1, 3)])
 def test_defer_pass_geometry_and_tableau(K, rb, occ, nt, form):
     """Whole tableau after 45 pivots equals the eager session's, byte for byte."""
     m, n, seed = 300, 520, 5
