@@ -361,7 +361,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         HIP_TRY(hipMemsetAsync(s->d.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
         HIP_TRY(hipMemsetAsync(s->d.P, 0, sizeof(double) * kt * s->ld, s->stream));
         s->defer_rb = opt->rows_per_block > 0 ? std::min(opt->rows_per_block, 1024)
-                                              : (s->streaming ? 128 : 64);
+                                              : (s->streaming ? 256 : 64);
     }
     HIP_TRY(hipMemsetAsync(s->prow_send, 0, sizeof(int64_t) * s->ld, s->stream));
 
@@ -1262,7 +1262,7 @@ int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_bloc
             set_error("a deferred session (defer > 1) needs a 512-column update variant");
             return DLP_ERR_ARG;
         }
-        s->defer_rb = rows_per_block > 0 ? std::min(rows_per_block, 1024) : (s->streaming ? 128 : 64);
+        s->defer_rb = rows_per_block > 0 ? std::min(rows_per_block, 1024) : (s->streaming ? 256 : 64);
     }
     s->opt.update_variant = update_variant;
     s->opt.nontemporal = nontemporal;
