@@ -15,7 +15,7 @@ constexpr int kUpdThreads = 256;
 constexpr int kUpdVec = 2;
 constexpr int kUpdTile = kUpdThreads * kUpdVec;   // doubles per column tile
 constexpr int kRatioThreads = 256;
-constexpr int kRatioDeferThreads = 256;  // deferred ratio test (64 and 512 measured slower)
+constexpr int kRatioDeferThreads = 256;  // deferred ratio test (64, 128 and 512 measured slower)
 constexpr int kProwThreads = 256;
 constexpr int32_t kNoIndex = 0x7fffffff;
 constexpr int kColqPad = 16;   // colq allocated with rows + 1 + kColqPad entries
