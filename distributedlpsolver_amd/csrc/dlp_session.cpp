@@ -300,7 +300,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     const int tile = dlp::update_tile(opt->update_variant);
     g.ntiles = (int)((s->width + tile - 1) / tile);
     // deferred rank-k update: auto = 32 pivots per tableau pass on a streaming
-    // (HBM-resident) tableau, 16 on a cache-resident one; eager when the
+    // (HBM-resident) tableau, 16 on a cache-resident one, eager on a tiny one; eager when the
     // caller drives the exchange itself (dlp_session_step_*) or when the chosen
     // rank-1 variant tiles pricing differently from the deferred kernels
     {
@@ -310,7 +310,13 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
             set_error("defer must be 0 (auto) or 1..64");
             return DLP_ERR_ARG;
         }
-        if (K == 0) K = (host_driven || tile != dlp::kDeferTile) ? 1 : (s->streaming ? 32 : 16);
+        // a tableau under 32 MiB stays eager: its rank-1 update is a few-µs launch, and
+        // the replayed ratio / pivot-row kernels cost more than the passes they save
+        // (C4 256x512: 14.2 µs/pivot eager vs 19.0 at K = 16; 1024x1024: 18.0 vs 20.8;
+        // C2 4096x8192, 268 MB: K = 16 is 2.3x eager; profiles/r01j/tune_small_defer.txt)
+        const bool tiny = (double)(s->rows + 1) * (double)s->width * 8.0 < (double)(32ll << 20);
+        if (K == 0)
+            K = (host_driven || tile != dlp::kDeferTile || tiny) ? 1 : (s->streaming ? 32 : 16);
         if (K > 1 && tile != dlp::kDeferTile) {
             set_error("defer > 1 needs a 512-column update variant");
             return DLP_ERR_ARG;

@@ -138,7 +138,8 @@ typedef struct dlp_options {
                                 -tol_feas * (1 + max_i b'_i) (default 1e-9) */
     int32_t defer;           /* pivots per tableau pass (deferred rank-k update, results
                                 bit-identical to rank-1): 1 = eager rank-1 per pivot, 2..64 =
-                                block size, 0 = auto (default: 16; eager for sessions driven
+                                block size, 0 = auto (default: 32 on a tableau > 1 GiB, 16
+                                from 32 MiB, eager below 32 MiB and for sessions driven
                                 through dlp_session_step_*) */
     int32_t pad2_;
 } dlp_options;
