@@ -79,8 +79,9 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
 
     // Everything that does not depend on q is requested before the pricing reduce,
     // so those loads are in flight while the partials are combined: the replay
-    // chain's first 8 coefficients (preloading 32 measured slower), the RHS inputs, the basis entry, the step
-    // tables.  Only T0[i][q] and P[l][q] wait for q.
+    // chain's first 8 coefficients (preloading 32 measured slower), the RHS
+    // inputs, the basis entry, the step tables.  Only T0[i][q] and P[l][q] wait
+    // for q.
     const int j = st->blk;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int l = threadIdx.x; l < j; l += blockDim.x) {
