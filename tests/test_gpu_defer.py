@@ -162,3 +162,11 @@ def test_defer_step_api_multi_rank_one_gpu(P, K):
     assert Td.tobytes() == Te.tobytes()
     for s in sess:
         s.close()
+
+
+def test_auto_block_size_policy():
+    """defer = 0 (auto): eager under 32 MiB of tableau, K = 16 up to 1 GiB."""
+    with dlp.Session(dlp.Problem.random(256, 512, 4, degenerate=True)) as s:
+        assert s.update_stats()[2] == 1
+    with dlp.Session(dlp.Problem.random(2048, 2048, 2)) as s:   # 2049 x 4097 doubles = 67 MB
+        assert s.update_stats()[2] == 16
