@@ -222,7 +222,7 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "kernel": (f"rank-1 update variant {variant} (rows/band {rb_used}, "
                                     f"nt {nt_used}, ld {ld_used})" if defer == 1 else
-                                    f"rank-{defer} tableau pass pass_kernel (rows/band {rb_used}, "
+                                    f"rank-{defer} tableau pass pass_s_kernel (rows/band {rb_used}, "
                                     f"nt {nt_used}, ld {ld_used}): {defer} pivots per launch"),
                          "launch_ms": upd_ms},
             "cpu_baseline": cpu,
