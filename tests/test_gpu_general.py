@@ -44,9 +44,10 @@ def _check(res, ref, x_too=True):
 
 @pytest.mark.parametrize("cs", CASES, ids=[c["name"] for c in CASES])
 @pytest.mark.parametrize("pricing", [0, 1])
-def test_general_fixtures_bit_identical(cs, pricing):
+@pytest.mark.parametrize("defer", [0, 16])  # 0 = auto: eager below 32 MiB
+def test_general_fixtures_bit_identical(cs, pricing, defer):
     lp = fixture_lp(cs)
-    res = dlp.solve(dlp.Problem.general(*lp_arrays(lp)), pricing=pricing)
+    res = dlp.solve(dlp.Problem.general(*lp_arrays(lp)), pricing=pricing, defer=defer)
     ref = O.solve_general(lp, pricing=pricing)
     _check(res, ref)
     if ref.status == 0 and "highs" in cs and cs["highs"]["status"] == 0:
@@ -56,10 +57,11 @@ def test_general_fixtures_bit_identical(cs, pricing):
 
 @pytest.mark.parametrize("m,n,seed,sense,frac_eq", [(120, 160, 301, 1, 0.2), (200, 150, 302, -1, 0.3),
                                                     (300, 420, 303, 1, 0.1)])
-def test_general_random_larger(m, n, seed, sense, frac_eq):
+@pytest.mark.parametrize("defer", [0, 16])  # 0 = auto: eager below 32 MiB
+def test_general_random_larger(m, n, seed, sense, frac_eq, defer):
     cs = random_general("r", m, n, seed, sense=sense, c0=0.5, frac_eq=frac_eq)
     lp = fixture_lp(cs)
-    res = dlp.solve(dlp.Problem.general(*lp_arrays(lp)))
+    res = dlp.solve(dlp.Problem.general(*lp_arrays(lp)), defer=defer)
     ref = O.solve_general(lp, nthreads=8)
     assert ref.status == 0 and ref.phase1_pivots > 0
     _check(res, ref)
@@ -131,25 +133,28 @@ def test_general_multi_rank_sessions_one_gpu(P, name):
 
 
 @pytest.mark.parametrize("name", ["lpgen_2d_20x20_eq", "network_flow", "enzo_c_infeasible"])
-def test_general_rccl_exchange_single_rank(name):
+@pytest.mark.parametrize("defer", [0, 16])  # 0 = auto: eager below 32 MiB
+def test_general_rccl_exchange_single_rank(name, defer):
     cs = next(c for c in CASES if c["name"] == name)
     lp = fixture_lp(cs)
     ref = O.solve_general(lp)
     with dlp.Session(dlp.Problem.general(*lp_arrays(lp)), rank=0, nranks=1,
-                     rccl_id=dlp.comm_unique_id(), timing=2, check_interval=5) as s:
+                     rccl_id=dlp.comm_unique_id(), timing=2, check_interval=5,
+                     defer=defer) as s:
         st, _ = s.run(10 ** 6)
         res = s.result()
     assert st == ref.status
     _check(res, ref)
 
 
-def test_general_resume_across_runs():
+@pytest.mark.parametrize("defer", [0, 8])
+def test_general_resume_across_runs(defer):
     """dlp_session_run in small slices (the Phase I end, the drive-out and the
     switch land in different calls) equals one solve."""
     cs = next(c for c in CASES if c["name"] == "random_40x60_max")
     lp = fixture_lp(cs)
     ref = O.solve_general(lp)
-    with dlp.Session(dlp.Problem.general(*lp_arrays(lp)), check_interval=3) as s:
+    with dlp.Session(dlp.Problem.general(*lp_arrays(lp)), check_interval=3, defer=defer) as s:
         st = L.RUNNING
         while st == L.RUNNING:
             st, _ = s.run(4)

@@ -45,9 +45,10 @@ def _check_equal(res, ref):
 
 @pytest.mark.parametrize("kat", load_golden("kat.json"), ids=lambda k: k["name"])
 @pytest.mark.parametrize("pricing", [0, 1])
-def test_kat(kat, pricing):
+@pytest.mark.parametrize("defer", [0, 16])  # 0 = auto: eager below 32 MiB
+def test_kat(kat, pricing, defer):
     A, b, c = np.array(kat["A"]), np.array(kat["b"]), np.array(kat["c"])
-    res, ref = _solve_both(A, b, c, pricing=pricing)
+    res, ref = _solve_both(A, b, c, pricing=pricing, defer=defer)
     _check_equal(res, ref)
     assert res.status == kat.get("expected_status", 0)
     if "expected_x" in kat:
@@ -56,11 +57,12 @@ def test_kat(kat, pricing):
 
 @pytest.mark.parametrize("case", [c for c in load_golden("generated.json")],
                          ids=lambda c: c["name"])
-def test_generated_host_input(case):
+@pytest.mark.parametrize("defer", [0, 16])  # 0 = auto: eager below 32 MiB
+def test_generated_host_input(case, defer):
     """Host-supplied dense LPs (C1, C4 degenerate): bit-identical to the oracle,
     objective within 1e-9 of HiGHS."""
     A, b, c = O.gen_dense(case["m"], case["n"], case["seed"], case["degenerate"])
-    res, ref = _solve_both(A, b, c)
+    res, ref = _solve_both(A, b, c, defer=defer)
     _check_equal(res, ref)
     hi = case["highs"]["objective"]
     assert abs(res.objective - hi) <= 1e-9 * abs(hi)
@@ -106,10 +108,11 @@ def test_launch_options_do_not_change_results(opts):
     _check_equal(res, ref)
 
 
-def test_pivot_limit_and_resume():
+@pytest.mark.parametrize("defer", [0, 8])
+def test_pivot_limit_and_resume(defer):
     A, b, c = O.gen_dense(120, 150, 9)
     ref = O.solve_dense(A, b, c)
-    with dlp.Session(dlp.Problem.dense(A, b, c), check_interval=16) as s:
+    with dlp.Session(dlp.Problem.dense(A, b, c), check_interval=16, defer=defer) as s:
         st, done = s.run(50)
         assert st == L.RUNNING and done == 50
         st, done2 = s.run(10 ** 6)
@@ -118,17 +121,19 @@ def test_pivot_limit_and_resume():
     _check_equal(res, ref)
 
 
-def test_max_pivots_reports_limit():
+@pytest.mark.parametrize("defer", [0, 8])
+def test_max_pivots_reports_limit(defer):
     A, b, c = O.gen_dense(120, 150, 9)
-    res = dlp.solve(dlp.Problem.dense(A, b, c), max_pivots=20, check_interval=8)
+    res = dlp.solve(dlp.Problem.dense(A, b, c), max_pivots=20, check_interval=8, defer=defer)
     assert res.status == L.PIVOT_LIMIT and res.num_pivots == 20
     ref = O.solve_dense(A, b, c, max_pivots=20)
     _same_log(res.pivot_log, ref.pivot_log)
 
 
-def test_unbounded():
+@pytest.mark.parametrize("defer", [0, 4])
+def test_unbounded(defer):
     A = np.array([[-1.0, 1.0], [1.0, -2.0]])
-    res, ref = _solve_both(A, np.array([1.0, 2.0]), np.array([1.0, 1.0]))
+    res, ref = _solve_both(A, np.array([1.0, 2.0]), np.array([1.0, 1.0]), defer=defer)
     assert res.status == ref.status == L.UNBOUNDED
     _same_log(res.pivot_log, ref.pivot_log)
 
@@ -178,13 +183,16 @@ def test_multi_rank_sessions_one_gpu(P):
         s.close()
 
 
-def test_rccl_exchange_path_single_rank():
-    """The RCCL exchange path (all-gather + select kernel + MAX all-reduce) on a
-    1-rank communicator gives the same log as the fused single-GPU path."""
+@pytest.mark.parametrize("defer", [0, 1, 16, 32])
+def test_rccl_exchange_path_single_rank(defer):
+    """The RCCL exchange path (all-gather + select kernel + MAX all-reduce; with
+    defer > 1 also the commit kernel and the rank-K pass, as bench.py --gpus N
+    runs it) on a 1-rank communicator gives the same log as the oracle."""
     A, b, c = O.gen_dense(200, 400, 1)
     ref = O.solve_dense(A, b, c)
     with dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1,
-                     rccl_id=dlp.comm_unique_id(), timing=2) as s:
+                     rccl_id=dlp.comm_unique_id(), timing=2, defer=defer) as s:
+        assert s.update_stats()[2] == (defer or 1)
         st, done = s.run(10 ** 6)
         res = s.result()
     assert st == L.OK
@@ -192,11 +200,12 @@ def test_rccl_exchange_path_single_rank():
 
 
 @pytest.mark.parametrize("A_,I_", [(2, 10), (100, 100), (200, 200)])
-def test_adalloc_bridge(A_, I_):
+@pytest.mark.parametrize("defer", [0, 16])  # 0 = auto: eager below 32 MiB
+def test_adalloc_bridge(A_, I_, defer):
     """f1: the reference's own generated instance solved exactly on the GPU."""
     rec = [r for r in load_golden("adalloc.json") if (r["A"], r["I"]) == (A_, I_)][0]
     p = dlp.Problem.adalloc(A_, I_, 1, rec["sparsity"], rec["scaling"])
-    res = dlp.solve(p)
+    res = dlp.solve(p, defer=defer)
     M, b, c = O.adalloc_lp(A_, I_, rec["sparsity"], rec["scaling"])
     ref = O.solve_dense(M, b, c)
     _check_equal(res, ref)
