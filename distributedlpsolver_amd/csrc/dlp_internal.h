@@ -84,7 +84,7 @@ struct Defer {
     int32_t* nzc = nullptr; // rows: nonzero C[i][l] of the block so far (the pass's row class)
     int form = 3;          // pass kernel, LDS-staged coefficients: 0 = 2 doubles/lane,
                            // 1 = 1 double/lane x 2 rows, 2 = 1 double/lane x 4 rows;
-                           // scalar-coefficient forms: 3 = 1 double x 4 rows (default),
+                           // scalar-coefficient forms: 3 = 1 double x 4 rows (default; 4 at K = 32 streaming),
                            // 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows
 };
 

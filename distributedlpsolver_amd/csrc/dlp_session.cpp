@@ -327,6 +327,10 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         }
         s->d.K = K;
         s->opt.defer = K;
+        // pass form: 2 doubles x 2 rows per lane at K = 32 on a streaming tableau (C3: 6.31
+        // vs 6.39 ms per pass, 4,494 vs 4,441 pivots/s, profiles/r01k/bench_ab_form*.json);
+        // 1 double x 4 rows elsewhere (K = 16: form 3 6.1 ms vs form 4 6.4, r01g)
+        s->d.form = (K == 32 && s->streaming) ? 4 : 3;
     }
     g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block : auto_rows_per_block(s);
     g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
