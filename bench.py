@@ -1,27 +1,41 @@
 #!/usr/bin/env python3
-"""Benchmark: simplex pivots/s + achieved HBM GB/s of the rank-1 update on a
+"""Benchmark: simplex pivots/s + achieved HBM GB/s of the tableau update on a
 dense fp64 tableau (BASELINE.json metric), 1/2/4/8 MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2]
+    python bench.py [--gpus N] [--steps S] [--warmup W] [--workload c3|c2]
+                    [--step-unit block|pivot]
 
-A "step" is one simplex pivot (pricing + ratio test + pivot-row exchange +
-rank-1 elimination) of ONE LP whose tableau is resident in HBM, row-block
-partitioned over the N ranks (launched by torch.distributed.run for N > 1,
-one process per GPU, exchange over RCCL inside libdlp).  The LP is fixed as N
+What is timed: pivots of ONE LP whose tableau is resident in HBM, row-block
+partitioned over the N ranks (launched by torch.distributed.run for N > 1, one
+process per GPU, exchange over RCCL inside libdlp).  The LP is fixed as N
 grows, so scaling is strong.  Default workload C3: m = n = 32768 (N = 65536,
 17.2 GB tableau), generated on the device (synthetic, seed 3 = config id).
 
-Rank 0 prints ONE JSON line.  The roofline object prices the update kernel:
-algorithmic bytes per launch = 16 (m_local + 1)(N + 1) (one read + one write of
-every resident tableau element) over its mean launch time from
-HIP events on the session stream.  cpu_baseline (rank 0, N = 1 only) is the
-in-repo CPU oracle (same pivot rule) on a bounded sample of the same workload.
+A "step" is one pass of the hot path over the tableau.  The update is the
+deferred rank-K form: K pivots are selected (pricing, ratio
+test, pivot-row exchange) on replayed views of the resident tableau, then ONE
+HBM pass applies all K to every element, bit-identical to K rank-1 updates.
+So with --step-unit block (default) a step = K pivots + their tableau pass
+(K = 32 at C3), and S steps time S*K pivots, every one of them fully applied
+(a window never ends with pivots pending).  With --step-unit pivot a step is
+one pivot, and the window's last pass covers only its last partial block
+(DESIGN.md §6 explains the difference).  `value` is pivots/s either way.
+
+Rank 0 prints ONE JSON line.  roofline prices the tableau pass: algorithmic
+bytes per launch = 16 * rows_local * (N + 1) (one read + one write of every
+constraint element) over its mean launch time from HIP events
+on the session stream.  `traffic` is the committed rocprofv3 PMC summary of the
+same kernel at the same geometry (profiles/, tools/pmc_summary.py), or null
+when none matches.  cpu_baseline (rank 0, N = 1 only) is the in-repo CPU
+oracle (same pivot rule, test infrastructure) on a bounded sample of the same
+LP: all host threads available to this process, then 1 thread.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -40,15 +54,16 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults are whole deferred blocks (K = 32 at C3): a window that ends mid-block pays a
-    # full tableau pass for its last few pivots (run() leaves the tableau current), so a
-    # 200-pivot window measures 7 passes for 6.25 blocks of work
-    ap.add_argument("--steps", type=int, default=256)
-    ap.add_argument("--warmup", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--step-unit", default="block", choices=("block", "pivot"),
+                    help="block: a step is K pivots + one rank-K tableau pass; pivot: one pivot")
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-pivots", type=int, default=60)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU baseline: time budget of each of the two oracle windows")
+    ap.add_argument("--no-pivot-window", action="store_true",
+                    help="skip the extra --step-unit pivot window reported beside the main figure")
     ap.add_argument("--rows-per-block", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=-1, help="-1 = auto")
     ap.add_argument("--variant", type=int, default=-1, help="update-kernel variant, -1 = auto")
@@ -64,7 +79,7 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(pmc_dir: str, kernel_substr: str = "update_"):
+def pmc_traffic(pmc_dir: str, kernel_substr: str):
     """Per-launch HBM bytes of the update kernel from rocprofv3 counter CSVs:
     (2 x FETCH_SIZE + WRITE_SIZE) KiB -> bytes (gfx950 FETCH_SIZE reads 1/2 of a
     wide coalesced stream: MI355X_MICROARCH.md §HBM)."""
@@ -86,31 +101,69 @@ def pmc_traffic(pmc_dir: str, kernel_substr: str = "update_"):
     return (2.0 * sum(fetch) / len(fetch) + sum(write) / len(write)) * 1024.0
 
 
-def committed_traffic(workload: str, kernel: str):
-    """Latest committed PMC summary for this workload and kernel
-    (profiles/*/<workload>_<kernel>_pmc_traffic.json, kernel = update | pass), produced by
-    tools/gpu_profile.sh + tools/pmc_summary.py on the same kernel; None when absent."""
+def committed_traffic(key: dict):
+    """The committed PMC summary (profiles/r*/*_pmc_traffic.json, written by
+    tools/pmc_summary.py) whose recorded geometry equals this run's `key`
+    (workload, kernel kind, K, form, band rows, nt, ld); (None, None) when none
+    matches, so a summary of another kernel or geometry is never reported."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{workload}_{kernel}_pmc_traffic.json")))
-    if not paths:
+    hits = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r*", "*_pmc_traffic.json")):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        geo = d.get("geometry")
+        if isinstance(geo, dict) and all(geo.get(k) == v for k, v in key.items()) \
+                and d.get("traffic_bytes_per_launch"):
+            hits.append((os.path.relpath(path, ROOT), d["traffic_bytes_per_launch"]))
+    if not hits:
         return None, None
-    with open(paths[-1]) as f:
-        d = json.load(f)
-    return d.get("traffic_bytes_per_launch"), os.path.relpath(paths[-1], ROOT)
+    src, val = sorted(hits)[-1]
+    return val, src
 
 
-def cpu_baseline(m, n, seed, k, threads):
+def cpu_info():
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, avail
+
+
+def cpu_baseline(m, n, seed, budget_s):
+    """The in-repo C++ oracle (same pivot rule, OpenMP over rows; test
+    infrastructure: the CPU comparator only) on the same LP: all threads this
+    process may use (capped by OMP_NUM_THREADS when the box sets it), then 1."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py  # test infrastructure: the CPU comparator only
-    secs, done, gen = oracle_py.bench_pivots(m, n, seed, 1, k, threads)
-    return {"value": done / secs, "unit": "pivots/s", "cores": threads, "kind": "port",
-            "sample": f"in-repo C++ oracle (same pivot rule, OpenMP over rows), same LP "
-                      f"{m}x{n} seed {seed}: 1 warm-up + {done} timed pivots in {secs:.2f} s "
-                      f"(host tableau generation {gen:.1f} s not timed)"}
-
-
-def defer_of(sess) -> int:
-    return sess.update_stats()[2]
+    model, nproc, avail = cpu_info()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = avail if not (omp and omp.isdigit() and int(omp) > 0) else min(avail, int(omp))
+    (s_all, k_all), (s_one, k_one) = None, None
+    runs, gen = oracle_py.bench_windows(m, n, seed, [(threads, 100000, budget_s), (1, 100000, budget_s)],
+                                        gen_threads=threads)
+    (s_all, k_all), (s_one, k_one) = runs
+    where = (f"{model}; os.cpu_count() = {nproc}, {avail} usable by this process"
+             + (f", OMP_NUM_THREADS = {omp}" if omp else ""))
+    return {"value": k_all / s_all, "unit": "pivots/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "nproc": nproc, "cpus_usable": avail,
+            "sample": (f"in-repo C++ oracle (same pivot rule, eager rank-1, OpenMP over rows) on the same "
+                       f"LP {m}x{n} seed {seed}: 1 warm-up pivot, then {k_all} pivots in {s_all:.2f} s on "
+                       f"{threads} threads, then {k_one} pivots in {s_one:.2f} s on 1 thread ({where}); "
+                       f"host tableau generation {gen:.1f} s not timed"),
+            "single_thread": {"value": k_one / s_one, "unit": "pivots/s", "cores": 1,
+                              "pivots": k_one, "seconds": s_one}}
 
 
 def main():
@@ -142,58 +195,90 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    sess = dlp.Session(dlp.Problem.random(m, n, seed), rank=rank, nranks=world, rccl_id=rccl_id,
-                       device=local, check_interval=max(args.steps, args.warmup, 1),
-                       timing=args.timing, nontemporal=args.nontemporal,
-                       update_variant=args.variant, ld_align=args.ld_align,
-                       rows_per_block=args.rows_per_block, max_pivots=args.warmup + args.steps + 1,
-                       log_pivots=1, defer=args.defer)
+    prob = dlp.Problem.random(m, n, seed)
+    # K is fixed by the session (auto: 32 on a streaming tableau); the pivot budget
+    # leaves room for the widest window and the extra pivot window
+    sess = dlp.Session(prob, rank=rank, nranks=world, rccl_id=rccl_id, device=local,
+                       check_interval=64 * max(args.steps, args.warmup, 1), timing=args.timing,
+                       nontemporal=args.nontemporal, update_variant=args.variant,
+                       ld_align=args.ld_align, rows_per_block=args.rows_per_block,
+                       max_pivots=64 * (args.warmup + args.steps) + args.steps + 2, log_pivots=1,
+                       defer=args.defer)
     if args.occupancy >= 0 or args.form >= 0:
-        if defer_of(sess) > 1:
+        if sess.update_stats()[2] > 1:
             sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 0, args.form)
-    st, done = sess.run(args.warmup)
-    if done != args.warmup:
+    K = sess.update_stats()[2]
+    per_step = K if args.step_unit == "block" else 1
+    warm, timed = args.warmup * per_step, args.steps * per_step
+
+    st, done = sess.run(warm)
+    if done != warm:
         raise SystemExit(f"warm-up ended early: status {st} after {done} pivots")
     sess.reset_timings()
 
     barrier_sync()
     t0 = time.perf_counter()
-    st, done = sess.run(args.steps)
+    st, done = sess.run(timed)
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    if done != args.steps:
+    if done != timed:
         raise SystemExit(f"timed window ended early: status {st} after {done} pivots")
 
     tm, nsamp = sess.timings()
-    launches, upd_total_ms, defer = sess.update_stats()
+    launches, upd_total_ms, _ = sess.update_stats()
     variant, rb_used, nt_used = sess.get_tuning()
+    form = sess.defer_form() if K > 1 else None
     ld_used = sess.ld
     rows_local, N1 = sess.rows, sess.ncols + 1
-    upd_ms = upd_total_ms / max(launches, 1)   # per update-kernel launch (rank-1, or rank-k pass)
+    upd_ms = upd_total_ms / max(launches, 1)   # per update-kernel launch (rank-1, or rank-K pass)
     # algorithmic bytes of one launch: one read + one write of every resident element
     # (the deferred pass skips the objective row, kept current by the pivot-row kernel)
-    bytes_launch = 16.0 * (rows_local + (1 if defer == 1 else 0)) * N1
+    bytes_launch = 16.0 * (rows_local + (1 if K == 1 else 0)) * N1
     achieved = bytes_launch / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else None   # timing 0: untimed
+    obj_after = None
+
+    # the same LP continues: a --step-unit pivot window of args.steps pivots beside the main
+    # figure (its last pass covers a partial block), timed the same way
+    pw = None
+    if not args.no_pivot_window and args.step_unit == "block" and K > 1:
+        barrier_sync()
+        t1 = time.perf_counter()
+        st, done = sess.run(args.steps)
+        barrier_sync()
+        pw_el = time.perf_counter() - t1
+        if done == args.steps:
+            pw = {"pivots": args.steps, "seconds": pw_el, "passes": -(-args.steps // K)}
 
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        import torch as _t
+        t = _t.tensor([elapsed, pw["seconds"] if pw else 0.0], dtype=_t.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
+        if pw:
+            pw["seconds"] = float(t[1].item())
+    if pw:
+        pw["pivots_per_s"] = pw["pivots"] / pw["seconds"]
 
     res = sess.result()
+    obj_after = res.objective
     sess.close()
 
     if rank == 0:
-        ksub = "update_" if defer == 1 else "pass"
+        kind = "update" if K == 1 else "pass"
+        ksub = "update_" if K == 1 else "pass"
+        geo = {"workload": args.workload, "kernel": kind, "K": K, "form": form,
+               "rows_per_block": rb_used, "nontemporal": nt_used, "ld": ld_used,
+               "rows_local": rows_local}
         if args.pmc_dir:
             traffic, traffic_src = pmc_traffic(args.pmc_dir, ksub), f"live: {args.pmc_dir}"
+        elif world == 1:
+            traffic, traffic_src = committed_traffic(geo)
         else:
-            traffic, traffic_src = (committed_traffic(args.workload, "update" if defer == 1 else "pass")
-                                    if world == 1 else (None, None))
+            traffic, traffic_src = None, None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(m, n, seed, args.cpu_pivots, args.cpu_threads)
-        value = args.steps / elapsed
+            cpu = cpu_baseline(m, n, seed, args.cpu_seconds)
+        value = timed / elapsed
         line = {
             "metric": "simplex pivots/s (dense fp64 tableau, rank-1 update HBM roofline)",
             "value": value,
@@ -207,23 +292,30 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (device-generated splitmix64 dense LP, seed = config id)",
-            "config": {"workload": desc, "m": m, "n": n, "N": m + n, "ld": ld_used, "seed": seed, "rows_per_rank": rows_local,
-                       "parallelism": f"rowblock{world}", "pricing": "dantzig->bland on degeneracy",
-                       "pivots_per_tableau_pass": defer},
+            "config": {"workload": desc, "m": m, "n": n, "N": m + n, "ld": ld_used, "seed": seed,
+                       "rows_per_rank": rows_local, "parallelism": f"rowblock{world}",
+                       "pricing": "dantzig->bland on degeneracy", "pivots_per_tableau_pass": K,
+                       "step": (f"{per_step} pivots + their rank-{K} tableau pass" if per_step > 1
+                                else "one pivot")},
+            "pivots_timed": timed,
+            "pivots_per_step": per_step,
+            "K": K,
+            "passes_in_window": launches,
             "achieved_hbm_gbs": achieved,
             "phases_ms_per_pivot": ({"ratio": tm[0] / max(nsamp, 1), "exchange": tm[1] / max(nsamp, 1),
                                      "prow": tm[2] / max(nsamp, 1), "update": tm[3] / max(nsamp, 1)}
                                     if args.timing >= 2 else None),
             "update_launches": launches,
-            "objective_after_window": res.objective,
+            "pivot_step_window": pw,
+            "objective_after_run": obj_after,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "kernel": (f"rank-1 update variant {variant} (rows/band {rb_used}, "
-                                    f"nt {nt_used}, ld {ld_used})" if defer == 1 else
-                                    f"rank-{defer} tableau pass pass_s_kernel (rows/band {rb_used}, "
-                                    f"nt {nt_used}, ld {ld_used}): {defer} pivots per launch"),
+                                    f"nt {nt_used}, ld {ld_used})" if K == 1 else
+                                    f"rank-{K} tableau pass, form {form} (rows/band {rb_used}, "
+                                    f"nt {nt_used}, ld {ld_used}): {K} pivots per launch"),
                          "launch_ms": upd_ms},
             "cpu_baseline": cpu,
         }

@@ -783,7 +783,10 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
     size_t dyn = d.form >= 3 ? 0 : (size_t)K * rb * sizeof(double) + (size_t)rb * sizeof(int32_t);
     if (dyn > 160 * 1024) return hipErrorInvalidValue;
     if (occ > 0) {   // reserve LDS so that at most `occ` workgroups fit on a CU (160 KiB)
-        const size_t cap = (size_t)160 * 1024 / occ - 1024;
+        // the kernel's static LDS counts against the same 160 KiB: cls[1024] (forms 3-5),
+        // s_pl[K] (forms 0-2)
+        const size_t stat = d.form >= 3 ? 1024 * sizeof(int32_t) : K * sizeof(int32_t);
+        const size_t cap = (size_t)160 * 1024 / occ - stat;
         if (dyn < cap) dyn = cap;
     }
     const dim3 grid(ntiles, (unsigned)bands);

@@ -634,6 +634,20 @@ int poll(dlp_session* s) {
             }
             s->upd_launches += (s->d.K > 1) ? s->ev_flush[k] : 1;
         }
+        // deferred, solve ended inside the window: the pass that applied the last real
+        // pivots ran in a later slot (the window's closing one), fold that one too
+        if (s->d.K > 1 && s->ev_per_pivot == 2 && real > 0 && real < s->ev_pending &&
+            !s->ev_flush[real - 1]) {
+            for (int64_t k = real; k < s->ev_pending; ++k) {
+                if (!s->ev_flush[k]) continue;
+                hipEvent_t* ev = &s->ev[(size_t)k * 2];
+                float ms = 0.f;
+                HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+                s->timings[DLP_PHASE_UPDATE] += ms;
+                s->upd_launches += 1;
+                break;
+            }
+        }
         s->nsamples += real;
     }
     s->ev_pending = 0;
@@ -1163,7 +1177,10 @@ int dlp_session_step_candidate(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
     s->step_void = false;
-    if (s->d.K > 1) return step_candidate_defer(s);
+    // the Phase I -> II switch (drive-out pivots, carried row) runs on the eager
+    // kernels in every session, as in dlp_session_run: apply a pending deferred
+    // block first, since a forced pivot reads its row from the tableau
+    if (s->drive_next < s->drive.size() || s->carry_pending) CALL_TRY(flush_pending(s));
     if (s->drive_next < s->drive.size()) {
         s->step_kind = dlp_session::STEP_FORCED;
         return enqueue_forced_candidate(s, s->drive[s->drive_next++]);
@@ -1173,6 +1190,7 @@ int dlp_session_step_candidate(dlp_session* s) {
         HIP_TRY(hipMemsetAsync(s->cand_send, 0, sizeof(dlp::Cand), s->stream));
         return DLP_OK;
     }
+    if (s->d.K > 1) return step_candidate_defer(s);
     s->step_kind = dlp_session::STEP_PIVOT;
     return enqueue_candidate(s);
 }
@@ -1181,12 +1199,12 @@ int dlp_session_step_select(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
     if (s->step_void) return DLP_OK;
-    if (s->d.K > 1) return step_select_defer(s);
     switch (s->step_kind) {
         case dlp_session::STEP_FORCED: return enqueue_forced_select(s);
         case dlp_session::STEP_CARRY: return enqueue_carry_out(s);
         default: break;
     }
+    if (s->d.K > 1) return step_select_defer(s);
     CALL_TRY(enqueue_select(s));
     return enqueue_prow(s);
 }
@@ -1195,11 +1213,11 @@ int dlp_session_step_update(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
     if (s->step_void) return DLP_OK;
-    if (s->d.K > 1) return step_update_defer(s);
     if (s->step_kind == dlp_session::STEP_CARRY) {
         CALL_TRY(enqueue_carry_in(s));
         return finish_phase1(s);
     }
+    if (s->d.K > 1 && s->step_kind == dlp_session::STEP_PIVOT) return step_update_defer(s);
     CALL_TRY(enqueue_update(s));
     s->launched += 1;
     return DLP_OK;
@@ -1307,6 +1325,14 @@ int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
     if (form >= 0) s->d.form = form;
     if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
     if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
+    return DLP_OK;
+}
+
+int dlp_session_get_defer_tuning(dlp_session* s, int* occupancy, int* form, int* K) {
+    if (!s) return DLP_ERR_ARG;
+    if (occupancy) *occupancy = s->defer_occ;
+    if (form) *form = s->d.K > 1 ? s->d.form : -1;
+    if (K) *K = s->d.K;
     return DLP_OK;
 }
 

@@ -297,6 +297,16 @@ class Session:
         L.check(L.lib().dlp_session_set_defer_tuning(self._h, occupancy, form),
                 "dlp_session_set_defer_tuning")
 
+    def get_defer_tuning(self) -> tuple[int, int, int]:
+        """(pass workgroups/CU cap, pass form (-1 when eager), pivots per pass K)."""
+        occ, form, k = C.c_int(), C.c_int(), C.c_int()
+        L.check(L.lib().dlp_session_get_defer_tuning(self._h, C.byref(occ), C.byref(form), C.byref(k)),
+                "dlp_session_get_defer_tuning")
+        return occ.value, form.value, k.value
+
+    def defer_form(self) -> int:
+        return self.get_defer_tuning()[1]
+
     def reset_timings(self):
         L.check(L.lib().dlp_session_reset_timings(self._h), "dlp_session_reset_timings")
 

@@ -139,8 +139,10 @@ typedef struct dlp_options {
     int32_t defer;           /* pivots per tableau pass (deferred rank-k update, results
                                 bit-identical to rank-1): 1 = eager rank-1 per pivot, 2..64 =
                                 block size, 0 = auto (default: 32 on a tableau > 1 GiB, 16
-                                from 32 MiB, eager below 32 MiB and for sessions driven
-                                through dlp_session_step_*) */
+                                from 32 MiB, eager below 32 MiB and for multi-rank sessions
+                                without an RCCL id, whose exchange the caller drives
+                                through dlp_session_step_*; a single-rank session driven
+                                through the step API keeps the size-based choice) */
     int32_t pad2_;
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
@@ -278,10 +280,17 @@ int dlp_session_reset_timings(dlp_session* s);
 int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_block, int nontemporal);
 int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_block, int* nontemporal);
 /* Deferred sessions: workgroups per CU allowed for the tableau pass (LDS
- * reservation; 0 = no cap, default 4) and its form (0 = 2 doubles per lane,
- * K <= 32; 1 / 2 = 1 double per lane, 2 / 4 rows per iteration (default 2);
- * -1 = keep).  rows_per_block (set_tuning) is the pass's row band. */
+ * reservation; 0 = no cap, the default) and its form (-1 = keep):
+ *   LDS-staged coefficients: 0 = 2 doubles per lane (K <= 32), 1 / 2 = 1 double
+ *   per lane x 2 / 4 rows per iteration;
+ *   scalar-load coefficients: 3 = 1 double x 4 rows, 4 = 2 doubles x 2 rows
+ *   (K <= 32), 5 = 1 double x 8 rows.
+ * Default: 4 at K = 32 on a tableau > 1 GiB, else 3.  rows_per_block
+ * (set_tuning) is the pass's row band.  Results are bit-identical for every
+ * setting. */
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
+/* Current deferred-pass settings (K = 1: form -1). */
+int dlp_session_get_defer_tuning(dlp_session* s, int* occupancy, int* form, int* K);
 int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,
                      int64_t* ncols);
 /* Copy the local tableau (rows_local+1 rows x ld, objective last) to the host. */

@@ -446,4 +446,39 @@ int oracle_bench_pivots(int kind, int64_t m, int64_t n, uint64_t seed, int64_t w
     return 0;
 }
 
+// bench.py cpu_baseline: one generated LP (gen_threads), one warm-up pivot, then
+// nrun consecutive timed windows on the same tableau, window r with threads[r]
+// OpenMP threads, each ending after max_k[r] pivots or once budget_s[r] seconds
+// have passed (checked after every pivot).  secs[r] / done[r] per window.
+int oracle_bench_windows(int kind, int64_t m, int64_t n, uint64_t seed, int32_t gen_threads,
+                         int nrun, const int32_t* threads, const int64_t* max_k,
+                         const double* budget_s, double* secs, int64_t* done,
+                         double* gen_seconds) {
+    using clk = std::chrono::steady_clock;
+    oracle_opts o{};
+    o.pricing = 0; o.tol_dj = 1e-9; o.tol_piv = 1e-9; o.max_pivots = 1 << 30;
+    o.nthreads = gen_threads;
+    Tab t;
+    auto g0 = clk::now();
+    tab_init(t, m, n, 0, m, &o);
+    if (oracle_gen_tableau(kind, m, n, seed, 0, m, t.ld, t.T.data(), gen_threads) != 0) return -1;
+    if (gen_seconds) *gen_seconds = std::chrono::duration<double>(clk::now() - g0).count();
+    if (pivot_once(t) != 4) return -6;
+    for (int r = 0; r < nrun; ++r) {
+        t.nthreads = threads[r] > 0 ? threads[r] : 1;
+        auto t0 = clk::now();
+        int64_t cnt = 0;
+        double el = 0.0;
+        while (cnt < max_k[r]) {
+            if (pivot_once(t) != 4) break;
+            ++cnt;
+            el = std::chrono::duration<double>(clk::now() - t0).count();
+            if (el >= budget_s[r]) break;
+        }
+        secs[r] = el;
+        done[r] = cnt;
+    }
+    return 0;
+}
+
 }  // extern "C"

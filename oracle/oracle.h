@@ -115,6 +115,13 @@ double oracle_sum_fixed(const double* x, int64_t n);
 /* CPU baseline: generate the tableau, do `warmup` pivots, time `k` pivots. */
 int oracle_bench_pivots(int kind, int64_t m, int64_t n, uint64_t seed, int64_t warmup, int64_t k,
                         int32_t nthreads, double* seconds, int64_t* done, double* gen_seconds);
+/* CPU baseline over several thread counts on ONE generated LP: one warm-up
+ * pivot, then nrun consecutive windows (threads[r] threads, at most max_k[r]
+ * pivots or budget_s[r] seconds); secs[r], done[r] per window. */
+int oracle_bench_windows(int kind, int64_t m, int64_t n, uint64_t seed, int32_t gen_threads,
+                         int nrun, const int32_t* threads, const int64_t* max_k,
+                         const double* budget_s, double* secs, int64_t* done,
+                         double* gen_seconds);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/digests.json: oracle digests of long runs at the
+BASELINE.json full sizes, too slow for the oracle inside a GPU test but cheap
+for the GPU to reproduce.  Run in the build container (CPU only):
+
+    python tests/golden/make_digests.py [c2] [c3]
+
+  c2  C2 4096 x 4096 seed 2 (dense family) solved to optimality by the oracle:
+      pivot count, status, sha256 of the pivot log / x / y, objective bits.
+  c3  C3 32768 x 32768 seed 3: the exact pivot sequence of the default
+      bench.py run (5 warm-up + 20 timed blocks of K = 32 pivots, then a
+      20-pivot window = 820 pivots): sha256 of the log, the objective row and
+      sampled constraint rows after those pivots.
+
+The digests hash little-endian fp64 / int32 bytes of the oracle's outputs
+(tests/oracle_py.py), so the GPU side compares bit for bit."""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import oracle_py as O  # noqa: E402
+
+OUT = os.path.join(HERE, "digests.json")
+C3_PIVOTS = 5 * 32 + 20 * 32 + 20
+C3_ROWS = [0, 1, 777, 12345, 20000, 32767]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def c2():
+    m = n = 4096
+    t0 = time.time()
+    A, b, c = O.gen_dense(m, n, 2)
+    r = O.solve_dense(A, b, c, nthreads=os.cpu_count() or 8, log_cap=200_000)
+    return {"m": m, "n": n, "seed": 2, "status": r.status, "num_pivots": int(r.num_pivots),
+            "objective_hex": float(r.objective).hex(), "log_sha256": sha(r.pivot_log),
+            "x_sha256": sha(r.x), "y_sha256": sha(r.y), "basis_sha256": sha(r.basis),
+            "oracle_seconds": time.time() - t0}
+
+
+def c3():
+    m = n = 32768
+    t0 = time.time()
+    rows = np.array(C3_ROWS + [m], np.int64)   # + the objective row
+    log, out, basis = O.run_generated(m, n, 3, C3_PIVOTS, rows, nthreads=os.cpu_count() or 8)
+    w = ((n + m + 1) + 15) // 16 * 16
+    return {"m": m, "n": n, "seed": 3, "pivots": int(len(log)), "log_sha256": sha(log),
+            "log_prefix_sha256": {str(k): sha(log[:k]) for k in (160, 800)},
+            "objective_hex": float(log[-1]["objective"]).hex(),
+            "rows": C3_ROWS, "width": w,
+            "row_sha256": {str(i): sha(out[k, :w]) for k, i in enumerate(C3_ROWS)},
+            "objective_row_sha256": sha(out[-1, :w]), "basis_sha256": sha(basis),
+            "oracle_seconds": time.time() - t0}
+
+
+def main():
+    which = sys.argv[1:] or ["c2", "c3"]
+    d = {}
+    if os.path.exists(OUT):
+        with open(OUT) as f:
+            d = json.load(f)
+    for w in which:
+        d[w] = {"c2": c2, "c3": c3}[w]()
+        with open(OUT, "w") as f:
+            json.dump(d, f, indent=1)
+        print(w, json.dumps(d[w]), flush=True)
+
+
+if __name__ == "__main__":
+    main()

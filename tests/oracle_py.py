@@ -214,6 +214,27 @@ def bench_pivots(m, n, seed, warmup, k, nthreads, degenerate=False):
     return secs.value, done.value, gen.value
 
 
+def bench_windows(m, n, seed, runs, gen_threads, degenerate=False):
+    """runs = [(threads, max_pivots, budget_seconds), ...] on one generated LP
+    (oracle_bench_windows).  Returns ([(seconds, pivots), ...], generation seconds)."""
+    L = lib()
+    if not getattr(L, "_bw_bound", False):
+        L.oracle_bench_windows.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_uint64, C.c_int32,
+                                           C.c_int, _I32, _I64, _D, _D, _I64, _D]
+        L._bw_bound = True
+    thr = np.array([r[0] for r in runs], np.int32)
+    kmax = np.array([r[1] for r in runs], np.int64)
+    bud = np.array([r[2] for r in runs], np.float64)
+    secs = np.zeros(len(runs))
+    done = np.zeros(len(runs), np.int64)
+    gen = C.c_double()
+    rc = L.oracle_bench_windows(1 if degenerate else 0, m, n, seed, gen_threads, len(runs),
+                                thr.ctypes.data_as(_I32), kmax.ctypes.data_as(_I64), _d(bud),
+                                _d(secs), done.ctypes.data_as(_I64), C.byref(gen))
+    assert rc == 0, f"oracle_bench_windows rc={rc}"
+    return [(float(s), int(k)) for s, k in zip(secs, done)], gen.value
+
+
 def mw_run(A, I, sparsity=0.1, scaling=0.25, epsilon=0.01, T=300, tol=1e-18):
     """fp64 MW spec (oracle/oracle_mw.cpp), sort mode.  Returns a dict of per-iteration arrays."""
     L = lib()
