@@ -150,7 +150,6 @@ def cpu_baseline(m, n, seed, budget_s):
     model, nproc, avail = cpu_info()
     omp = os.environ.get("OMP_NUM_THREADS")
     threads = avail if not (omp and omp.isdigit() and int(omp) > 0) else min(avail, int(omp))
-    (s_all, k_all), (s_one, k_one) = None, None
     runs, gen = oracle_py.bench_windows(m, n, seed, [(threads, 100000, budget_s), (1, 100000, budget_s)],
                                         gen_threads=threads)
     (s_all, k_all), (s_one, k_one) = runs
@@ -318,6 +317,7 @@ def main():
                                     f"nt {nt_used}, ld {ld_used}): {K} pivots per launch"),
                          "launch_ms": upd_ms},
             "cpu_baseline": cpu,
+            "geometry": geo,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -56,6 +56,14 @@ def main():
     wr, _ = counter(os.path.join(tag, "pmc_write"), "WRITE_SIZE", sub)
     calls, avg_ns = stats(os.path.join(tag, "trace"), sub)
     d = {"kernel": kname, "trace_working_launches": calls, "trace_avg_ns": avg_ns}
+    # the bench line of the trace pass names the geometry (bench.py's committed_traffic key)
+    try:
+        with open(os.path.join(tag, "trace_bench.json")) as f:
+            line = json.loads(f.read().strip().splitlines()[-1])
+        d["geometry"] = line.get("geometry")
+        d["trace_bench_launch_ms"] = line["roofline"]["launch_ms"]
+    except (OSError, ValueError, KeyError, IndexError):
+        pass
     if fe and wr:
         # the first launch after a retune / the last partial block can differ: report the mean
         rd = 2.0 * sum(fe) / len(fe) * 1024.0
