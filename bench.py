@@ -155,6 +155,9 @@ def cpu_baseline(m, n, seed, budget_s):
     (s_all, k_all), (s_one, k_one) = runs
     where = (f"{model}; os.cpu_count() = {nproc}, {avail} usable by this process"
              + (f", OMP_NUM_THREADS = {omp}" if omp else ""))
+    if not (k_all and s_all and k_one and s_one):
+        raise RuntimeError(f"CPU baseline sample too small: {k_all} pivots in {s_all} s, "
+                           f"{k_one} in {s_one} s (the LP ended inside the sample)")
     return {"value": k_all / s_all, "unit": "pivots/s", "cores": threads, "kind": "port",
             "cpu_model": model, "nproc": nproc, "cpus_usable": avail,
             "sample": (f"in-repo C++ oracle (same pivot rule, eager rank-1, OpenMP over rows) on the same "

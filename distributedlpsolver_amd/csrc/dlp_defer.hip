@@ -732,6 +732,308 @@ __global__ __launch_bounds__(256) void pass_s_kernel(double* __restrict__ T, int
     pass_s_body<NT, K, V, U, PART>(T, ld, rows, width, st, C, ldc, P, nzc, rb);
 }
 
+// The same body held to 3 waves per SIMD (<= 168 VGPRs; form 4 alone takes 170, which
+// allocates 176 and leaves 2 waves per SIMD).
+template <bool NT, int K, int V, int U, bool PART>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void pass_s3_kernel(
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t width, const DevState* __restrict__ st,
+    const double* __restrict__ C, int64_t ldc, const double* __restrict__ P,
+    const int32_t* __restrict__ nzc, int rb) {
+    pass_s_body<NT, K, V, U, PART>(T, ld, rows, width, st, C, ldc, P, nzc, rb);
+}
+
+// Streamed form of the pass (forms 6-9): pass_s_body's per-element operations,
+// with three changes aimed at the HBM stream.
+//  * Work order.  A 1-D grid; workgroup b works on position q of a list of
+//    (tile, band) pairs ordered by groups of kPassBands bands, tile-major inside
+//    a group, and the list is cut into 8 equal contiguous pieces, piece b % 8
+//    going to the workgroups that share b's XCD (blocks are dealt round-robin
+//    over the 8 XCDs: MI355X_MICROARCH.md, workgroup dispatch).  So the
+//    workgroups resident on one XCD at a time share a few tiles' P slices and a
+//    few bands' coefficients in that XCD's L2, instead of every workgroup
+//    fetching both again from the Infinity Cache.  Placement only moves speed.
+//  * Dense groups first.  The band's dense groups (U rows, every step of the
+//    block touches every row) are compacted into a list in LDS and streamed
+//    through a ring of D register buffers: the rows of D-1 groups are in flight
+//    while one group's fma chains run.  Everything else (sparse rows, the
+//    block's pivot rows, rows of partly dense groups) follows, row by row,
+//    through the generic replay.  Rows are independent, so order is free.
+//  * Coefficients.  Scalar loads in chunks of LC steps x U rows, double
+//    buffered, and the next dense group's first chunk is fetched during the
+//    current group's last chunk (full blocks: K / LC is even).
+constexpr int kPassBands = 16;   // bands per group of the work order
+
+// Buffer access to one band of the tableau: the descriptor is built once from
+// wave-uniform values, every lane keeps ONE 32-bit column offset, and the row
+// offset is a scalar (soffset).  aux 2 = nt.
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+template <bool NT, int V>
+__device__ inline void bld(double (&t)[V], __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    if constexpr (V == 2) {
+        const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, NT ? 2 : 0);
+        const d2 v = __builtin_bit_cast(d2, x);
+        t[0] = v.x;
+        t[1] = v.y;
+    } else {
+        const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, NT ? 2 : 0);
+        t[0] = __builtin_bit_cast(double, x);
+    }
+}
+template <bool NT, int V>
+__device__ inline void bst(const double (&t)[V], __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    if constexpr (V == 2) {
+        d2 v;
+        v.x = t[0];
+        v.y = t[1];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs, voff, soff, NT ? 2 : 0);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t[0]), rs, voff, soff, NT ? 2 : 0);
+    }
+}
+
+template <int K, int V, int U>
+struct PassGeo {
+    static constexpr int LC = (16 / U) < K ? (16 / U) : K;   // steps per coefficient chunk
+    static constexpr int NCH = K / LC;                       // chunks per group
+};
+
+template <bool NT, int K, int V, int U, int D, bool PART>
+__global__ __launch_bounds__(256) void pass_r_kernel(double* __restrict__ T, int64_t ld,
+                                                     int64_t rows, int64_t width,
+                                                     const DevState* __restrict__ st,
+                                                     const double* __restrict__ C, int64_t ldc,
+                                                     const double* __restrict__ P,
+                                                     const int32_t* __restrict__ nzc, int rb,
+                                                     int ntiles, int nbands, int order) {
+    static_assert(PassGeo<K, V, U>::NCH % 2 == 0, "the cross-group prefetch needs an even chunk count");
+    __shared__ int32_t cls[1024];
+    __shared__ int16_t dgl[512];
+    __shared__ int32_t s_wtot[4];
+    const int kb = st->blk;
+    if (kb == 0 || (PART ? kb == K : kb != K)) return;
+    // (tile, band) of this workgroup: order 1 = the XCD work order above; order 0 =
+    // tile-fastest over the whole grid (consecutive workgroups stream one row range)
+    const int64_t total = (int64_t)ntiles * nbands;
+    int tile, band;
+    if (order) {
+        const int64_t per = (total + 7) >> 3;
+        const int64_t q = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+        if ((int64_t)(blockIdx.x >> 3) >= per || q >= total) return;
+        const int bgrp = (int)(q / ((int64_t)kPassBands * ntiles));
+        const int rr = (int)(q - (int64_t)bgrp * kPassBands * ntiles);
+        const int nbg = min(kPassBands, nbands - bgrp * kPassBands);
+        tile = rr / nbg;
+        band = bgrp * kPassBands + rr % nbg;
+    } else if (order == 2) {
+        // XCD b % 8 owns a range of ceil(ntiles / 8) column tiles and walks it band by
+        // band: its resident workgroups share those tiles' P slices in its L2, and the
+        // 8 XCDs together sweep whole rows, as the eager update does
+        const int t8 = (ntiles + 7) >> 3;
+        const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+        const int tx0 = x * t8, ntx = min(t8, ntiles - tx0);
+        if (ntx <= 0 || k >= ntx * nbands) return;
+        band = k / ntx;
+        tile = tx0 + k % ntx;
+    } else {
+        if ((int64_t)blockIdx.x >= total) return;
+        band = (int)(blockIdx.x / ntiles);
+        tile = (int)(blockIdx.x - (int64_t)band * ntiles);
+    }
+
+    const int64_t j = (int64_t)tile * (256 * V) + threadIdx.x * V;
+    const int64_t jc = j < width ? j : width - V;
+    double pr[K][V];
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        double v[V];
+        ldrow<false, V>(v, P + (int64_t)(l < kb ? l : 0) * ld + jc);
+#pragma unroll
+        for (int e = 0; e < V; ++e) pr[l][e] = l < kb ? v[e] : 0.0;
+    }
+    const int64_t i0 = (int64_t)band * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+        const int nz = nzc[i0 + r];
+        int last = -1;
+        for (int l = 0; l < kb; ++l)
+            if (st->pl[l] == (int32_t)(i0 + r)) last = l;
+        cls[r] = last >= 0 ? last : (nz == kb ? kDense : (nz == 0 ? kUntouched : kSparse));
+    }
+    __syncthreads();
+    // compact the dense groups into dgl[0..ndg); their rows leave the generic loop
+    const int ng = nr / U;
+    int ndg = 0;
+    for (int base = 0; base < ng; base += 256) {
+        const int g = base + (int)threadIdx.x;
+        bool d = g < ng;
+        if (d)
+#pragma unroll
+            for (int u = 0; u < U; ++u) d = d && cls[g * U + u] == kDense;
+        const uint64_t m = __ballot(d);
+        const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        const int pre = __popcll(m & ((1ull << ln) - 1ull));
+        if (ln == 0) s_wtot[wv] = __popcll(m);
+        __syncthreads();
+        int off = ndg;
+        for (int w = 0; w < wv; ++w) off += s_wtot[w];
+        if (d) {
+            dgl[off + pre] = (int16_t)g;
+#pragma unroll
+            for (int u = 0; u < U; ++u) cls[g * U + u] = kUntouched;
+        }
+        ndg += s_wtot[0] + s_wtot[1] + s_wtot[2] + s_wtot[3];
+        __syncthreads();
+    }
+
+    constexpr int LC = PassGeo<K, V, U>::LC;
+    constexpr int NCH = PassGeo<K, V, U>::NCH;
+    const double* cbase = C + i0 * ldc;
+    auto fetch = [&](double (&f)[U][LC], cdptr cb, int l0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int l = 0; l < LC; ++l) f[u][l] = cb[u * ldc + l0 + l];
+    };
+    auto chain = [&](double (&t)[U][V], const double (&f)[U][LC], int l0) {
+#pragma unroll
+        for (int l = 0; l < LC; ++l)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < V; ++e)
+                    t[u][e] = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
+    };
+    // the chunk holding step kb-1: a uniform branch per step (no per-element selects)
+    auto chain_part = [&](double (&t)[U][V], const double (&f)[U][LC], int l0) {
+#pragma unroll
+        for (int l = 0; l < LC; ++l)
+            if (l0 + l < kb)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int e = 0; e < V; ++e)
+                        t[u][e] = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
+    };
+    auto grow = [&](int g) { return (int)__builtin_amdgcn_readfirstlane(dgl[g]) * U; };
+    // the band through one buffer descriptor (the launcher keeps rb * ld * 8 < 2^31).
+    // Lanes past the last column work on (and store) the last column group: the
+    // same operations on the same inputs give the same bits as its owner lane, so
+    // every store is unconditional (no exec-masked stores for vmcnt to second-guess)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(T + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
+    const int voff = (int)(jc * 8);
+    const int ld8 = (int)(ld * 8);
+    auto load = [&](double (&t)[U][V], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) bld<NT, V>(t[u], rs, voff, (r0 + u) * ld8);
+    };
+    auto store = [&](const double (&t)[U][V], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) bst<NT, V>(t[u], rs, voff, (r0 + u) * ld8);
+    };
+    double fa[U][LC], fb[U][LC];
+    // full block: fa holds chunk 0 of this group on entry and chunk 0 of group rn on exit
+    auto group_full = [&](double (&t)[U][V], int r0, int rn) {
+        const cdptr cb = (cdptr)(cbase + (int64_t)r0 * ldc);
+        const cdptr cn = (cdptr)(cbase + (int64_t)rn * ldc);
+#pragma unroll
+        for (int c = 0; c < NCH; c += 2) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): fa has landed
+            fetch(fb, cb, (c + 1) * LC);
+            __builtin_amdgcn_sched_barrier(0);
+            chain(t, fa, c * LC);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // fb has landed
+            if (c + 2 < NCH)
+                fetch(fa, cb, (c + 2) * LC);
+            else
+                fetch(fa, cn, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            chain(t, fb, (c + 1) * LC);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        store(t, r0);
+    };
+    // partial block: chunks up to step kb-1, the last one masked
+    auto group_part = [&](double (&t)[U][V], int r0) {
+        const cdptr cb = (cdptr)(cbase + (int64_t)r0 * ldc);
+        fetch(fa, cb, 0);
+#pragma unroll
+        for (int c = 0; c < NCH; c += 2) {
+            if (c * LC < kb) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                if ((c + 1) * LC < kb) fetch(fb, cb, (c + 1) * LC);
+                __builtin_amdgcn_sched_barrier(0);
+                if ((c + 1) * LC <= kb)
+                    chain(t, fa, c * LC);
+                else
+                    chain_part(t, fa, c * LC);
+                __builtin_amdgcn_sched_barrier(0);
+                if ((c + 1) * LC < kb) {
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    if ((c + 2) * LC < kb && c + 2 < NCH) fetch(fa, cb, (c + 2) * LC);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if ((c + 2) * LC <= kb)
+                        chain(t, fb, (c + 1) * LC);
+                    else
+                        chain_part(t, fb, (c + 1) * LC);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        store(t, r0);
+    };
+
+    if (ndg > 0) {
+        double buf[D][U][V];
+#pragma unroll
+        for (int b = 0; b < D - 1; ++b) load(buf[b], grow(b < ndg ? b : ndg - 1));
+        if constexpr (!PART) fetch(fa, (cdptr)(cbase + (int64_t)grow(0) * ldc), 0);
+        for (int g0 = 0; g0 < ndg; g0 += D) {
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                const int gi = g0 + b;
+                if (gi < ndg) {
+                    // the ring's next group: rows D-1 groups ahead (clamped: an L2 hit)
+                    const int ga = gi + D - 1 < ndg ? gi + D - 1 : ndg - 1;
+                    load(buf[(b + D - 1) % D], grow(ga));
+                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (!PART)
+                        group_full(buf[b], grow(gi), grow(gi + 1 < ndg ? gi + 1 : gi));
+                    else
+                        group_part(buf[b], grow(gi));
+                }
+            }
+        }
+    }
+    // everything else, row by row (as pass_s_body's generic replay)
+    for (int r = 0; r < nr; ++r) {
+        const int c = cls[r];
+        if (c == kUntouched) continue;
+        const double* cr = C + (i0 + r) * ldc;
+        double t[V];
+        int l = 0;
+        if (c >= 0) {
+            ldrow<false, V>(t, P + (int64_t)c * ld + jc);
+            l = c + 1;
+        } else {
+            bld<NT, V>(t, rs, voff, r * ld8);
+        }
+        for (; l < kb; ++l) {
+            const double f = cr[l];
+            if (f != 0.0) {
+                double pv[V];
+                ldrow<false, V>(pv, P + (int64_t)l * ld + jc);
+#pragma unroll
+                for (int e = 0; e < V; ++e) t[e] = __builtin_fma(-f, pv[e], t[e]);
+            }
+        }
+        bst<NT, V>(t, rs, voff, r * ld8);
+    }
+}
+
 __global__ void blk_reset_kernel(DevState* st) {
     if (threadIdx.x == 0) st->blk = 0;
 }
@@ -774,49 +1076,108 @@ hipError_t launch_commit_defer(const Geometry& g, const Defer& d, const DevState
     return hipGetLastError();
 }
 
+template <bool NT, int K, int V, int U, int D>
+static void launch_pass_r(const Geometry& g, const Defer& d, DevState* st, int rb, size_t dyn,
+                          int order, hipStream_t s) {
+    const int ntiles = (int)((g.width + 256 * V - 1) / (256 * V));
+    const int nbands = (int)((g.rows + rb - 1) / rb);
+    const int64_t total = (int64_t)ntiles * nbands;
+    const int64_t t8 = (ntiles + 7) / 8;
+    const dim3 grid((unsigned)(order == 1 ? 8 * ((total + 7) / 8) : order == 2 ? 8 * t8 * nbands : total));
+    pass_r_kernel<NT, K, V, U, D, false><<<grid, 256, dyn, s>>>(
+        g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb, ntiles, nbands, order);
+    pass_r_kernel<NT, K, V, U, D, true><<<grid, 256, dyn, s>>>(
+        g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb, ntiles, nbands, order);
+}
+
 template <bool NT, int K>
 static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
                        hipStream_t s) {
-    const int cols = (d.form == 0 || d.form == 4) ? kDeferTile : 256;
+    if (d.form >= 6 && d.form != 14 && d.form != 15 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31)) {
+        // streamed forms (K >= 16, a band within one 2 GiB buffer descriptor; else form 3)
+        if constexpr (K >= 16) {
+            if ((d.form == 6 || d.form == 7 || d.form == 10 || d.form == 11 || d.form == 16 ||
+                 d.form == 17) && K > 32)
+                return hipErrorInvalidValue;
+            size_t dyn = 0;
+            if (occ > 0) {   // static LDS: cls[1024], dgl[512], s_wtot[4]
+                const size_t stat = 1024 * sizeof(int32_t) + 512 * sizeof(int16_t) + 16;
+                dyn = (size_t)160 * 1024 / occ - stat;
+            }
+            if (g.rows > 0) {
+                // forms 6-9: XCD work order by band groups; 10-13: the same with the
+                // tile-fastest order; 16-19: XCD work order by tile ranges
+                const int order = d.form <= 9 ? 1 : d.form <= 13 ? 0 : 2;
+                const int f = d.form <= 9 ? d.form : d.form <= 13 ? d.form - 4 : d.form - 10;
+                if (f == 6) {
+                    if constexpr (K <= 32) launch_pass_r<NT, K, 2, 2, 4>(g, d, st, rb, dyn, order, s);
+                } else if (f == 7) {
+                    if constexpr (K <= 32) launch_pass_r<NT, K, 2, 2, 2>(g, d, st, rb, dyn, order, s);
+                } else if (f == 8) {
+                    launch_pass_r<NT, K, 1, 4, 4>(g, d, st, rb, dyn, order, s);
+                } else {
+                    launch_pass_r<NT, K, 1, 4, 2>(g, d, st, rb, dyn, order, s);
+                }
+            }
+            blk_reset_kernel<<<1, 64, 0, s>>>(st);
+            return hipGetLastError();
+        }
+    }
+    // streamed forms need K >= 16 (an even number of coefficient chunks): form 3 below
+    const int form = (d.form >= 6 && d.form != 14 && d.form != 15) ? 3 : d.form;
+    const int cols = (form == 0 || form == 4 || form >= 14) ? kDeferTile : 256;
     const int ntiles = (int)((g.width + cols - 1) / cols);
     const int64_t bands = (g.rows + rb - 1) / rb;
-    size_t dyn = d.form >= 3 ? 0 : (size_t)K * rb * sizeof(double) + (size_t)rb * sizeof(int32_t);
+    size_t dyn = form >= 3 ? 0 : (size_t)K * rb * sizeof(double) + (size_t)rb * sizeof(int32_t);
     if (dyn > 160 * 1024) return hipErrorInvalidValue;
     if (occ > 0) {   // reserve LDS so that at most `occ` workgroups fit on a CU (160 KiB)
         // the kernel's static LDS counts against the same 160 KiB: cls[1024] (forms 3-5),
         // s_pl[K] (forms 0-2)
-        const size_t stat = d.form >= 3 ? 1024 * sizeof(int32_t) : K * sizeof(int32_t);
+        const size_t stat = form >= 14 ? 1024 * sizeof(int32_t) + 512 * sizeof(int16_t) + 16
+                            : form >= 3 ? 1024 * sizeof(int32_t) : K * sizeof(int32_t);
         const size_t cap = (size_t)160 * 1024 / occ - stat;
         if (dyn < cap) dyn = cap;
     }
     const dim3 grid(ntiles, (unsigned)bands);
     if (g.rows > 0) {
-        if (d.form == 0) {
+        if (form == 0) {
             if constexpr (K <= 32)   // 2 doubles per lane: P[0..K) in 4K VGPRs
                 pass_kernel<NT, K><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st, d.C,
                                                           d.ldc, d.P, rb);
             else
                 return hipErrorInvalidValue;
-        } else if (d.form == 3) {
+        } else if (form == 3) {
             pass_s_kernel<NT, K, 1, 4, false><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
                                                                      d.C, d.ldc, d.P, d.nzc, rb);
             pass_s_kernel<NT, K, 1, 4, true><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
                                                                     d.C, d.ldc, d.P, d.nzc, rb);
-        } else if (d.form == 4) {
+        } else if (form == 4 || form == 14 || form == 15) {
             if constexpr (K <= 32) {
-                pass_s_kernel<NT, K, 2, 2, false><<<grid, 256, dyn, s>>>(
-                    g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
-                pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
-                    g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                if (form == 15)
+                    pass_s3_kernel<NT, K, 2, 2, false><<<grid, 256, dyn, s>>>(
+                        g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                else
+                    pass_s_kernel<NT, K, 2, 2, false><<<grid, 256, dyn, s>>>(
+                        g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                if (form >= 14 && K >= 16 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31)) {
+                    // partial block through the streamed kernel's partial instance
+                    const int nb = (int)bands;
+                    if constexpr (K >= 16)
+                        pass_r_kernel<NT, K, 2, 2, 4, true><<<dim3((unsigned)(ntiles * bands)), 256, dyn, s>>>(
+                            g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb, ntiles, nb, 0);
+                } else {
+                    pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
+                        g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                }
             } else
                 return hipErrorInvalidValue;
-        } else if (d.form == 5) {
+        } else if (form == 5) {
             pass_s_kernel<NT, K, 1, 8, false><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
                                                                      d.C, d.ldc, d.P, d.nzc, rb);
             pass_s_kernel<NT, K, 1, 8, true><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
                                                                     d.C, d.ldc, d.P, d.nzc, rb);
         }
-        else if (d.form == 1)
+        else if (form == 1)
             pass1_kernel<NT, K, 2><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st, d.C,
                                                           d.ldc, d.P, rb);
         else

@@ -327,10 +327,13 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         }
         s->d.K = K;
         s->opt.defer = K;
-        // pass form: 2 doubles x 2 rows per lane at K = 32 on a streaming tableau (C3: 6.31
-        // vs 6.39 ms per pass, 4,494 vs 4,441 pivots/s, profiles/r01k/bench_ab_form*.json);
-        // 1 double x 4 rows elsewhere (K = 16: form 3 6.1 ms vs form 4 6.4, r01g)
-        s->d.form = (K == 32 && s->streaming) ? 4 : 3;
+        // pass form 14: 2 doubles x 2 rows per lane for full blocks (form 4), the streamed
+        // kernel's partial instance for a window's last block (C3: full pass 6.30 ms; a
+        // 20-pivot partial pass 7.56 ms vs 12.7 ms with form 4's own partial instance,
+        // profiles/r02/tune_c3_k32_window20.txt), at K = 32 on a streaming tableau and K = 16
+        // on a cache-resident one (C2: pass 0.116 vs 0.128 ms for form 3, tune_c2.txt);
+        // 1 double x 4 rows elsewhere (K = 16 streaming: form 3 6.1 ms vs form 4 6.4, r01g)
+        s->d.form = ((K == 32 && s->streaming) || (K == 16 && !s->streaming)) ? 14 : 3;
     }
     g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block : auto_rows_per_block(s);
     g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
@@ -1316,8 +1319,10 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
 }
 
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
-    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 5) return DLP_ERR_ARG;
-    if ((form == 0 || form == 4) && s->d.K > 32) {
+    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 19) return DLP_ERR_ARG;
+    if ((form == 0 || form == 4 || form == 6 || form == 7 || form == 10 || form == 11 || form == 14 ||
+         form == 15 || form == 16 || form == 17) &&
+        s->d.K > 32) {
         set_error("the 2-doubles-per-lane pass holds at most 32 steps");
         return DLP_ERR_ARG;
     }

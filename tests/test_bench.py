@@ -11,7 +11,7 @@ import bench  # noqa: E402
 
 
 def test_cpu_baseline_small():
-    cb = bench.cpu_baseline(64, 64, 3, 0.2)
+    cb = bench.cpu_baseline(1500, 1500, 3, 0.2)
     assert cb["unit"] == "pivots/s" and cb["kind"] == "port"
     assert cb["value"] > 0 and cb["single_thread"]["value"] > 0
     assert cb["cores"] >= 1 and cb["single_thread"]["cores"] == 1

@@ -58,7 +58,17 @@ def test_defer_degenerate_bland(K, pricing):
                                               (8, 16, 0, 1, 4), (32, 100, 4, 1, 4), (13, 64, 0, 0, 4),
                                               (16, 64, 0, 1, 5), (48, 29, 0, 1, 5), (64, 256, 4, 0, 5),
                                               (48, 64, 0, 1, 3), (24, 128, 0, 0, 3), (40, 64, 0, 1, 5),
-                                              (7, 64, 4, 1, 3)])
+                                              (7, 64, 4, 1, 3),
+                                              # streamed forms 6-9 (K < 16 runs form 3; K = 24 / 48
+                                              # run the partial-block instance of the next template)
+                                              (16, 64, 0, 1, 6), (32, 256, 0, 1, 6), (32, 100, 0, 0, 7),
+                                              (24, 64, 4, 1, 7), (16, 37, 0, 1, 8), (32, 64, 2, 0, 8),
+                                              (64, 128, 0, 1, 9), (48, 64, 0, 1, 9), (8, 64, 0, 1, 6),
+                                              (64, 1024, 0, 1, 8), (32, 64, 0, 1, 10), (16, 64, 4, 0, 11),
+                                              (64, 64, 0, 1, 12), (32, 37, 0, 1, 13),
+                                              (32, 256, 0, 1, 14), (16, 64, 0, 0, 14), (8, 64, 0, 1, 14),
+                                              (32, 256, 0, 1, 15), (24, 64, 0, 0, 15), (32, 16, 4, 1, 16),
+                                              (16, 64, 0, 0, 17), (64, 32, 0, 1, 18), (32, 8, 0, 1, 19)])
 def test_defer_pass_geometry_and_tableau(K, rb, occ, nt, form):
     """Whole tableau after 45 pivots equals the eager session's, byte for byte."""
     m, n, seed = 300, 520, 5
@@ -76,13 +86,37 @@ def test_defer_pass_geometry_and_tableau(K, rb, occ, nt, form):
     assert Td.tobytes() == Te.tobytes()
 
 
+@pytest.mark.parametrize("form,K,rb", [(6, 32, 64), (7, 16, 64), (8, 32, 128), (9, 64, 64), (10, 32, 64),
+                                       (13, 64, 128), (16, 32, 16), (17, 32, 64), (18, 64, 32)])
+def test_defer_streamed_forms_many_bands(form, K, rb):
+    """Streamed pass forms on 47-94 bands (the work order's band groups of 16,
+    the last one partial, and 12-24 column tiles): 2 full blocks and a partial
+    one, whole tableau byte-equal to the eager session's."""
+    m = n = 3000
+    k = 2 * K + 7
+    prob = dlp.Problem.random(m, n, 11)
+    with dlp.Session(prob, defer=1, check_interval=k) as e:
+        e.run(k)
+        Te = e.tableau()
+        le = e.result().pivot_log
+    with dlp.Session(prob, defer=K, check_interval=K, rows_per_block=rb) as s:
+        s.set_defer_tuning(0, form)
+        done = 0
+        while done < k:
+            done += s.run(min(K, k - done))[1]
+        Td = s.tableau()
+        ld = s.result().pivot_log
+    _same_log(ld, le)
+    assert Td.tobytes() == Te.tobytes()
+
+
 def test_defer_retune_between_runs():
     A, b, c = O.gen_dense(200, 400, 2)
     ref = O.solve_dense(A, b, c)
     with dlp.Session(dlp.Problem.dense(A, b, c), defer=16, check_interval=9) as s:
         for k in range(1000):
             s.set_tuning(22 if k % 2 else 26, [16, 64, 200][k % 3], k % 2)
-            s.set_defer_tuning([0, 4, 2][k % 3], k % 6)
+            s.set_defer_tuning([0, 4, 2][k % 3], k % 20)
             st, _ = s.run(11)
             if st != L.RUNNING:
                 break
@@ -90,7 +124,7 @@ def test_defer_retune_between_runs():
     _check(res, ref)
 
 
-@pytest.mark.parametrize("form", [2, 3, 4, 5])
+@pytest.mark.parametrize("form", [2, 3, 4, 5, 6, 8])
 def test_defer_adalloc_sparse_rows(form):
     """Sparse tableau: most rows untouched by most steps (skip rule in the pass)."""
     p = dlp.Problem.adalloc(200, 200, 1, 0.1, 0.25)

@@ -31,6 +31,8 @@ ap.add_argument("--forms", default="2")
 ap.add_argument("--blocks", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--timing", type=int, default=2)
+ap.add_argument("--window", type=int, default=0,
+                help="pivots per timed window (0 = blocks x K); < K times one partial-block pass")
 ap.add_argument("--out", default=None)
 a = ap.parse_args()
 m, n, seed = W[a.workload]
@@ -59,12 +61,13 @@ for r in range(a.rounds):
         s.run(K)   # first window after a retune (graph rebuild) is not timed
         s.reset_timings()
         s.status()
+        win = a.window or K * a.blocks
         t0 = time.perf_counter()
-        s.run(K * a.blocks)
+        s.run(win)
         s.status()
         dt = time.perf_counter() - t0
         nl, ms, _ = s.update_stats()
-        res[c]["wall"].append(dt * 1e3 / (K * a.blocks))
+        res[c]["wall"].append(dt * 1e3 / win)
         if nl:
             res[c]["pass"].append(ms / nl)
     print(f"round {r} done", flush=True)
