@@ -140,6 +140,7 @@ SIGNATURES = [
     ("dlp_session_reset_timings", C.c_int, [_P]),
     ("dlp_session_update_stats", C.c_int, [_P, C.POINTER(_I64), _DP, C.POINTER(C.c_int)]),
     ("dlp_session_set_defer_tuning", C.c_int, [_P, C.c_int, C.c_int]),
+    ("dlp_session_set_fused_pivot", C.c_int, [_P, C.c_int]),
     ("dlp_session_get_defer_tuning", C.c_int,
      [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dlp_session_set_tuning", C.c_int, [_P, C.c_int, C.c_int, C.c_int]),

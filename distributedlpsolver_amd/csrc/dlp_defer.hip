@@ -30,6 +30,9 @@ namespace {
 
 #include "dlp_device.h"
 
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+
 template <bool NT>
 __device__ inline d2 ldv(const double* p) {
     if constexpr (NT)
@@ -64,46 +67,57 @@ __device__ inline void stv(double* p, d2 v) {
 // T0[i][q]; C[j][i] = a; the RHS cache advances by step j-1 (or is read from
 // T0 when the block is empty); then the ratio candidate.  The objective row
 // (local index rows) is current in place: C[j][rows] = z_q.
-__global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
+//
+// Latency, not bytes, sets this kernel's time, so everything that does not
+// depend on q is requested before the pricing reduce: the lane's whole replay
+// chain of coefficients (from Cc, the column-major copy of C, so each load is
+// one coalesced 512-B wave access), the RHS inputs, the basis entry, the step
+// tables.  Only T0[i][q] and P[l][q] wait for q.  The workgroup partials are
+// handed to the last-arriving workgroup without fences: write-through (sc1)
+// stores drained by vmcnt(0) before the ticket add, sc1 loads after it
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first table row).
+constexpr int kAuxSc1 = 16;   // buffer-op cache policy: sc1 (write-through store / L2 load)
+
+// Fused single-rank pivot (pivot_defer_kernel): the workgroup that ends the ratio
+// phase (the last arriver, or block 0 when nothing prices in) publishes the
+// selection to the pivot-row workgroups of the same launch: st->zq, then an
+// agent release and the flag st->go.
+__device__ inline void release_go(DevState* st) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&st->go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int KMAX, bool FUSED>
+__device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
-    DevState* st, double* __restrict__ C, int64_t ldc, const double* __restrict__ P,
-    double* __restrict__ rhs, int32_t* __restrict__ nzc, Cand* partials, Cand* cand_out,
-    int nranks, double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap) {
+    DevState* st, double* __restrict__ C, int64_t ldc, double* __restrict__ Cc, int64_t ldcc,
+    const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
+    Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
+    dlp_pivot* log, int64_t log_cap, int nblocks) {
     __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
     __shared__ Cand lds_c[kRatioDeferThreads / 64];
     __shared__ int s_last;
-    __shared__ double s_pq[kMaxDefer], s_pn[kMaxDefer];
-    __shared__ int32_t s_pl[kMaxDefer];
+    __shared__ double s_pq[KMAX], s_pn[KMAX];
+    __shared__ int32_t s_pl[KMAX];
     if (st->status != DLP_RUNNING) return;
 
-    // Everything that does not depend on q is requested before the pricing reduce,
-    // so those loads are in flight while the partials are combined: the replay
-    // chain's first 8 coefficients (preloading 32 measured slower), the RHS
-    // inputs, the basis entry, the step tables.  Only T0[i][q] and P[l][q] wait
-    // for q.
     const int j = st->blk;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int l = threadIdx.x; l < j; l += blockDim.x) {
         s_pn[l] = P[(int64_t)l * ld + ncols];
         s_pl[l] = st->pl[l];
     }
-    constexpr int kPre = 8;    // C[i][0..kPre), index clamped into the row (so no guard)
-    double f0[kPre];
-    double r_in = 0.0, f_prev = 0.0;
-    int32_t nz_in = 0, bvar = 0;
-    if (i < rows && j > 0) {
+    const int64_t ic = i < rows ? i : rows;   // clamped: loads need no guard
+    double f[KMAX];
 #pragma unroll
-        for (int u = 0; u < kPre; ++u) f0[u] = C[i * ldc + min(u, j - 1)];
-        nz_in = nzc[i];
-    }
+    for (int l = 0; l < KMAX; ++l) f[l] = (l < j) ? Cc[(int64_t)l * ldcc + ic] : 0.0;
+    double r_in = 0.0;
+    int32_t nz_in = 0, bvar = 0;
+    if (i < rows && j > 0) nz_in = nzc[i];
     if (i < rows_elig) {
-        if (j == 0) {
-            r_in = T[i * ld + ncols];
-        } else {
-            r_in = rhs[i];
-            f_prev = C[i * ldc + (j - 1)];
-        }
+        r_in = j == 0 ? T[i * ld + ncols] : rhs[i];
         bvar = basis[row_first + i];
     }
 
@@ -119,6 +133,7 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->q = -1;
             st->status = DLP_OK;
+            if constexpr (FUSED) release_go(st);
         }
         return;
     }
@@ -130,43 +145,30 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     if (i <= rows) {
         double a = T[i * ld + q];
         if (i < rows) {
-            // steps 0..kPre-1 from the preloaded coefficients (unrolled: f0 stays in
-            // registers), then chunks of 8 whose loads are issued back to back
 #pragma unroll
-            for (int l = 0; l < kPre; ++l) {
+            for (int l = 0; l < KMAX; ++l) {
                 if (l < j) {
                     if (i == s_pl[l])
                         a = s_pq[l];
-                    else if (f0[l] != 0.0)
-                        a = __builtin_fma(-f0[l], s_pq[l], a);
-                }
-            }
-            for (int l0 = kPre; l0 < j; l0 += 8) {
-                double f[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) f[u] = C[i * ldc + min(l0 + u, j - 1)];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int l = l0 + u;
-                    if (l < j) {
-                        if (i == s_pl[l])
-                            a = s_pq[l];
-                        else if (f[u] != 0.0)
-                            a = __builtin_fma(-f[u], s_pq[l], a);
-                    }
+                    else if (f[l] != 0.0)
+                        a = __builtin_fma(-f[l], s_pq[l], a);
                 }
             }
         }
         C[i * ldc + j] = a;
+        Cc[(int64_t)j * ldcc + i] = a;
         if (i < rows) nzc[i] = (j == 0 ? 0 : nz_in) + (a != 0.0 ? 1 : 0);   // the pass's row class
         if (i < rows_elig) {
             double r = r_in;
             if (j > 0) {
                 const int l = j - 1;
+                double fp = 0.0;   // f[j-1], selected without dynamic register indexing
+#pragma unroll
+                for (int u = 0; u < KMAX; ++u) fp = (u == l) ? f[u] : fp;
                 if (i == s_pl[l])
                     r = s_pn[l];
-                else if (f_prev != 0.0)
-                    r = __builtin_fma(-f_prev, s_pn[l], r);
+                else if (fp != 0.0)
+                    r = __builtin_fma(-fp, s_pn[l], r);
             }
             rhs[i] = r;
             if (a > tol_piv) {
@@ -182,24 +184,26 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     }
     c = block_cand(c, lds_c);
 
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)partials, (short)0, (int)(nblocks * sizeof(Cand)), 0x00020000);
     if (threadIdx.x == 0) {
-        partials[blockIdx.x] = c;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const u4v* cv = (const u4v*)&c;
+        __builtin_amdgcn_raw_buffer_store_b128(cv[0], prs, (int)(blockIdx.x * sizeof(Cand)), 0, kAuxSc1);
+        __builtin_amdgcn_raw_buffer_store_b128(cv[1], prs, (int)(blockIdx.x * sizeof(Cand)) + 16, 0,
+                                               kAuxSc1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev =
             __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (prev == gridDim.x - 1);
+        s_last = (prev == (unsigned)nblocks - 1);
     }
     __syncthreads();
     if (!s_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
     Cand best = cand_empty();
-    for (int k = threadIdx.x; k < (int)gridDim.x; k += blockDim.x) {
-        const Cand o = partials[k];
+    for (int k = threadIdx.x; k < nblocks; k += blockDim.x) {
+        Cand o;
+        u4v* ov = (u4v*)&o;
+        ov[0] = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(k * sizeof(Cand)), 0, kAuxSc1);
+        ov[1] = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(k * sizeof(Cand)) + 16, 0, kAuxSc1);
         if (cand_better(o, best)) best = o;
     }
     best = block_cand(best, lds_c);
@@ -210,7 +214,24 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
             do_select(st, best, q, basis, row_first, rows, pricing, log, log_cap, true);
         else
             cand_out[0] = best;
+        if constexpr (FUSED) {
+            st->zq = T[rows * ld + q];   // the objective row is current; nobody writes it yet
+            release_go(st);
+        }
     }
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
+    const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
+    int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
+    DevState* st, double* __restrict__ C, int64_t ldc, double* __restrict__ Cc, int64_t ldcc,
+    const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
+    Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
+    dlp_pivot* log, int64_t log_cap) {
+    ratio_defer_body<KMAX, false>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
+                                  ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
+                                  tol_piv, pricing, log, log_cap, (int)gridDim.x);
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
@@ -323,6 +344,123 @@ __global__ __launch_bounds__(256) void commit_defer_kernel(
     if (j < ld) pr = *(const d2*)(bits + j);
     commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
                lds_pp);
+}
+
+// Single rank: ratio test, selection and pivot row in ONE launch (saves a kernel
+// boundary per pivot, and the pivot-row workgroups load the block's P rows while
+// the ratio phase runs).  Blocks [0, nrat) run ratio_defer_body; blocks
+// [nrat, nrat + nprow) are pivot-row workgroups, one 512-column tile each, which
+// wait for st->go (bounded spin: a stall turns into DLP_ERR_HIP, never a hang),
+// then replay T0[p] exactly as prow_defer_kernel and commit it (commit_row, with
+// z_q from st->zq).  The last pivot-row workgroup to finish resets go and its
+// ticket for the next launch.  Every block of the grid is resident at once
+// (<= 2 * 129 workgroups of 256 threads at C3 against 8 per CU), and blocks are
+// dispatched in index order, so the ratio blocks always run.
+template <int KMAX>
+__global__ __launch_bounds__(256) void pivot_defer_kernel(
+    double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
+    int64_t nprice, int64_t row_first, int32_t* basis, PricePart* pp, int ntiles, DevState* st,
+    double* __restrict__ C, int64_t ldc, double* __restrict__ Cc, int64_t ldcc,
+    double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc, Cand* partials,
+    int nrat, double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap) {
+    if ((int)blockIdx.x < nrat) {
+        ratio_defer_body<KMAX, true>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st,
+                                     C, ldc, Cc, ldcc, P, rhs, nzc, partials, nullptr, 1, tol_dj,
+                                     tol_piv, pricing, log, log_cap, nrat);
+        return;
+    }
+    __shared__ PricePart lds_pp[4];
+    __shared__ double s_cp[KMAX];
+    __shared__ int32_t s_pl[KMAX];
+    __shared__ int s_ok;
+    if (st->status != DLP_RUNNING) return;   // the same answer in every block of this launch
+    const int tile = (int)blockIdx.x - nrat;
+    const int64_t j = ((int64_t)tile * blockDim.x + threadIdx.x) * 2;
+    const int64_t jc = j < ld ? j : ld - 2;
+    // the block's earlier pivot rows at this lane's columns, before the wait (blk may
+    // already be one past them if this block starts late: that row is not used)
+    const int s0 = min(st->blk, KMAX);
+    d2 pv[KMAX];
+#pragma unroll
+    for (int l = 0; l < KMAX; ++l)
+        if (l < s0) pv[l] = *(const d2*)(P + (int64_t)l * ld + jc);
+    if (threadIdx.x == 0) {
+        int ok = 0;
+        for (int it = 0; it < (1 << 24); ++it) {
+            if (__hip_atomic_load(&st->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                ok = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_ok = ok;
+    }
+    __syncthreads();
+    const bool run = s_ok && st->status == DLP_RUNNING;
+    if (!s_ok && threadIdx.x == 0) st->status = DLP_ERR_HIP;
+    if (run) {
+        const int s = st->blk - 1;
+        const int32_t pl = st->p_local;
+        for (int l = threadIdx.x; l < s; l += blockDim.x) {
+            s_cp[l] = C[(int64_t)pl * ldc + l];
+            s_pl[l] = st->pl[l];
+        }
+        __syncthreads();
+        d2 pr;
+        pr.x = 0.0;
+        pr.y = 0.0;
+        if (j < ld) {
+            d2 t = *(const d2*)(T + (int64_t)pl * ld + j);
+#pragma unroll
+            for (int l = 0; l < KMAX; ++l) {
+                if (l < s) {
+                    const d2 v = l < s0 ? pv[l] : *(const d2*)(P + (int64_t)l * ld + j);
+                    if (pl == s_pl[l]) {
+                        t = v;
+                    } else if (s_cp[l] != 0.0) {
+                        t.x = __builtin_fma(-s_cp[l], v.x, t.x);
+                        t.y = __builtin_fma(-s_cp[l], v.y, t.y);
+                    }
+                }
+            }
+            const double piv = st->piv;
+            pr.x = t.x / piv;
+            pr.y = t.y / piv;
+        }
+        // commit_row with z_q from the state (C[rows][s] is another block's store)
+        const int64_t width = (ncols + 16) & ~(int64_t)15;
+        if (j < ld) *(d2*)(P + (int64_t)s * ld + j) = pr;
+        const double zq = st->zq;
+        PricePart acc = pp_empty();
+        if (j < width) {
+            double* zp = T + rows * ld + j;
+            d2 z = *(const d2*)zp;
+            if (zq != 0.0) {
+                z.x = __builtin_fma(-zq, pr.x, z.x);
+                z.y = __builtin_fma(-zq, pr.y, z.y);
+                *(d2*)zp = z;
+            }
+            price_pair(acc, z.x, z.y, j, nprice, tol_dj);
+            if (log && j <= ncols && ncols < j + 2) {
+                const int64_t k = st->npivots - 1;
+                if (k >= 0 && k < log_cap) log[k].objective = (ncols == j) ? z.x : z.y;
+            }
+        }
+        acc = block_price(acc, lds_pp);
+        if (threadIdx.x == 0) pp[tile] = acc;
+    }
+    // the last pivot-row block to finish re-arms the flag for the next launch
+    if (threadIdx.x == 0) {
+        const int nprow = (int)gridDim.x - nrat;
+        const unsigned prev =
+            __hip_atomic_fetch_add(&st->ticket2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == (unsigned)nprow - 1) {
+            __hip_atomic_store(&st->go, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&st->ticket2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // The tableau pass.  Workgroup (tile, band): 512 columns (2 doubles per lane,
@@ -614,48 +752,52 @@ __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, 
                 for (int e = 0; e < V; ++e)
                     t[u][e] = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
     };
-    // the chunk holding step kb-1 of a partial block: steps >= kb are skipped
+    // the chunk holding step kb-1 of a partial block: steps >= kb are skipped by a
+    // uniform branch per step (per-element selects cost this instance ~85 VGPRs)
     auto chain_part = [&](double (&t)[U][V], const double (&f)[U][LC], int l0) {
 #pragma unroll
         for (int l = 0; l < LC; ++l)
+            if (l0 + l < kb)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int e = 0; e < V; ++e)
+                        t[u][e] = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
+    };
+    // a partial block runs the full-block code: chunks past step kb-1 are skipped, and in
+    // the chunk holding it the coefficients of steps >= kb are zeroed (scalar selects).
+    // With P[l] = +0 for l >= kb (above) such a step is fma(-(+0), +0, t) = t + (-0) = t
+    // for every t, so the result is exactly that of the kb real steps.
+    auto mask = [&](double (&f)[U][LC], int l0) {
+        if constexpr (PART) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    const double v = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
-                    t[u][e] = (l0 + l < kb) ? v : t[u][e];
-                }
+                for (int l = 0; l < LC; ++l) f[u][l] = (l0 + l < kb) ? f[u][l] : 0.0;
+        }
     };
     auto group = [&](double (&t)[U][V], int r0) {
         const cdptr cb = (cdptr)(cbase + (int64_t)r0 * ldc);
-        if constexpr (!PART) {
+        {
             double fa[U][LC], fb[U][LC];
             fetch(fa, cb, 0);
 #pragma unroll
             for (int l0 = 0; l0 < K; l0 += 2 * LC) {
+                if (PART && l0 >= kb) break;
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): chunk fa has landed
-                if (l0 + LC < K) fetch(fb, cb, l0 + LC);
+                const bool nb = l0 + LC < K && (!PART || l0 + LC < kb);
+                if (nb) fetch(fb, cb, l0 + LC);
+                mask(fa, l0);
                 __builtin_amdgcn_sched_barrier(0);
                 chain(t, fa, l0);
                 __builtin_amdgcn_sched_barrier(0);
-                if (l0 + LC < K) {
+                if (nb) {
                     __builtin_amdgcn_s_waitcnt(0xC07F);   // chunk fb has landed
-                    if (l0 + 2 * LC < K) fetch(fa, cb, l0 + 2 * LC);
+                    if (l0 + 2 * LC < K && (!PART || l0 + 2 * LC < kb)) fetch(fa, cb, l0 + 2 * LC);
+                    mask(fb, l0 + LC);
                     __builtin_amdgcn_sched_barrier(0);
                     chain(t, fb, l0 + LC);
                     __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        } else {   // partial block (the end of a run window): whole chunks, then the rest
-#pragma unroll
-            for (int l0 = 0; l0 < K; l0 += LC) {
-                if (l0 < kb) {
-                    double f[U][LC];
-                    fetch(f, cb, l0);
-                    if (l0 + LC <= kb)
-                        chain(t, f, l0);
-                    else
-                        chain_part(t, f, l0);
                 }
             }
         }
@@ -766,8 +908,6 @@ constexpr int kPassBands = 16;   // bands per group of the work order
 // Buffer access to one band of the tableau: the descriptor is built once from
 // wave-uniform values, every lane keeps ONE 32-bit column offset, and the row
 // offset is a scalar (soffset).  aux 2 = nt.
-typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-typedef unsigned int u2v __attribute__((ext_vector_type(2)));
 template <bool NT, int V>
 __device__ inline void bld(double (&t)[V], __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
     if constexpr (V == 2) {
@@ -1051,10 +1191,51 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
     nblocks = ratio_defer_blocks(g);
-    ratio_defer_kernel<<<nblocks, kRatioDeferThreads, 0, s>>>(
-        g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc,
-        d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap);
+#define DLP_RATIO_DEFER(KM)                                                                      \
+    ratio_defer_kernel<KM><<<nblocks, kRatioDeferThreads, 0, s>>>(                               \
+        g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, \
+        d.Cc, d.ldcc, d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing,   \
+        log, log_cap)
+    if (d.K <= 8)
+        DLP_RATIO_DEFER(8);
+    else if (d.K <= 16)
+        DLP_RATIO_DEFER(16);
+    else if (d.K <= 32)
+        DLP_RATIO_DEFER(32);
+    else
+        DLP_RATIO_DEFER(64);
+#undef DLP_RATIO_DEFER
     return hipGetLastError();
+}
+
+hipError_t launch_pivot_defer(const Geometry& g, const Defer& d, int32_t* basis, PricePart* pp,
+                              DevState* st, Cand* partials, int nblocks, double tol_dj,
+                              double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
+                              hipStream_t s) {
+    const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
+    if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
+    const int nrat = ratio_defer_blocks(g);
+    const int nprow = (int)((g.ld + kDeferTile - 1) / kDeferTile);
+    // every block resident at once (the pivot-row blocks wait on the ratio blocks): the
+    // caller keeps the grid within 2 blocks per CU (fused_pivot_fits); K <= 32
+    if (d.K > 32) return hipErrorInvalidValue;
+#define DLP_PIVOT_DEFER(KM)                                                                       \
+    pivot_defer_kernel<KM><<<nrat + nprow, 256, 0, s>>>(                                          \
+        g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.nprice, g.row_first, basis, pp, ntiles, st,    \
+        d.C, d.ldc, d.Cc, d.ldcc, d.P, d.rhs, d.nzc, partials, nrat, tol_dj, tol_piv, pricing,    \
+        log, log_cap)
+    if (d.K <= 8)
+        DLP_PIVOT_DEFER(8);
+    else if (d.K <= 16)
+        DLP_PIVOT_DEFER(16);
+    else
+        DLP_PIVOT_DEFER(32);
+#undef DLP_PIVOT_DEFER
+    return hipGetLastError();
+}
+
+int fused_pivot_blocks(const Geometry& g) {
+    return ratio_defer_blocks(g) + (int)((g.ld + kDeferTile - 1) / kDeferTile);
 }
 
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,

@@ -3,8 +3,10 @@
 #include "distributed_solver/instance.h"
 
 #include <algorithm>
+#include <fstream>
 #include <iostream>
 #include <stdexcept>
+#include <string>
 #include <vector>
 
 namespace distributed_solver {
@@ -92,8 +94,61 @@ void Instance::ReportGraphTopology() {
 // R/instance.cpp:154-165: one (current, average) pair per bid.
 void Instance::BuildPrimals() {
     solution_.assign(num_advertisers_, {});
-    for (int a = 0; a < num_advertisers_; ++a)
+    for (int a = 0; a < num_advertisers_ && a < (int)bids_matrix_.size(); ++a)
         for (const auto& kv : bids_matrix_[a]) solution_[a][kv.first] = {0.0L, 0.0L};
+}
+
+// R/instance.cpp:143-152, in long double as there.
+void Instance::UpdateAvgPrimal(int t, std::vector<PrimalRow>* solution) {
+    for (auto& row : *solution)
+        for (auto& kv : row)
+            kv.second.second = (long double)(t - 1) / t * kv.second.second +
+                               (long double)1 / t * kv.second.first;
+}
+
+// R/instance.cpp:167-176.
+void Instance::ResetCurrentPrimal(std::vector<PrimalRow>* sol) {
+    for (auto& row : *sol)
+        for (auto& kv : row) kv.second.first = 0.0;
+}
+
+// The file name of the reference's commented-out writer (R/instance.cpp:63).
+std::string Instance::CsvName(const std::string& handle) const {
+    return handle + std::to_string(num_advertisers_) + "x" + std::to_string(num_impressions_) + "x" +
+           std::to_string(num_slots_) + "x" + std::to_string(bid_sparsity_) + ".csv";
+}
+
+static void write_bid_rows(std::ofstream& file,
+                           const std::vector<std::unordered_map<int, long double>>& bids) {
+    for (const auto& adv : bids) {
+        std::vector<std::pair<int, long double>> row(adv.begin(), adv.end());
+        std::sort(row.begin(), row.end());
+        std::string line;
+        for (const auto& kv : row) line += std::to_string(kv.first) + "," + std::to_string(kv.second) + ",";
+        file << line << "\n";
+    }
+}
+
+// R/instance.cpp:59-86 (its file operations are comments there; done here).
+void Instance::WriteInstanceToCSV(std::string file_name_handle) {
+    const std::string name = CsvName(file_name_handle);
+    if (verbose) std::cout << file_name_handle + "\n" << "Writing instance " + name + "\n";
+    std::ofstream file(name);
+    if (!file) throw std::runtime_error("WriteInstanceToCSV: cannot open " + name);
+    write_bid_rows(file, bids_matrix_);
+}
+
+// R/instance.cpp:88-115: srand(1) bids, written as one shard.
+void Instance::GenerateAndWriteInstance(std::string file_name_handle) {
+    const bool v = verbose;
+    verbose = false;
+    GenerateInstance();
+    verbose = v;
+    const std::string name = CsvName(file_name_handle) + "@0";
+    if (verbose) std::cout << "Writing instance " + name + "\n";
+    std::ofstream file(name);
+    if (!file) throw std::runtime_error("GenerateAndWriteInstance: cannot open " + name);
+    write_bid_rows(file, bids_matrix_);
 }
 
 int Instance::RunSimplex(const dlp_options& options) {

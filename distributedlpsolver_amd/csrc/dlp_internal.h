@@ -57,6 +57,12 @@ struct alignas(16) DevState {
     int32_t blk;       // deferred mode: pivots selected since the last tableau pass
     uint32_t pad[2];
     int32_t pl[kMaxDefer];   // deferred mode: local pivot row of block step l (-1 elsewhere)
+    double zq;         // fused deferred pivot: objective-row entry of the entering column
+    double pad2[15];
+    // fused deferred pivot, on a 128-B line of their own (polled by the pivot-row blocks)
+    uint32_t go;       // selection published to the pivot-row blocks
+    uint32_t ticket2;  // last pivot-row block re-arms `go`
+    uint32_t pad3[30];
 };
 
 // Candidate order: valid first, then smaller ratio, then smaller basis index.
@@ -79,6 +85,8 @@ struct Defer {
     int K = 1;             // block size (1 = eager path, no deferral)
     double* C = nullptr;   // (rows+1) x K row-major: C[i*ldc + l] = T_l[i][q_l]
     int64_t ldc = 0;       // = K (row `rows` = the objective row's entries)
+    double* Cc = nullptr;  // K x ldcc column-major copy of C: Cc[l*ldcc + i] (the ratio
+    int64_t ldcc = 0;      // kernel's replay loads, coalesced); ldcc = round64(rows + 1)
     double* P = nullptr;   // K x ld: normalised pivot rows
     double* rhs = nullptr; // rows: current RHS column (eager cache)
     int32_t* nzc = nullptr; // rows: nonzero C[i][l] of the block so far (the pass's row class)
@@ -137,6 +145,13 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               const PricePart* pp, DevState* st, Cand* partials, int nblocks,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s);
+// nranks == 1: ratio test + selection + pivot row + objective row + pricing in ONE launch
+// (K <= 32; grid of fused_pivot_blocks(g), all of which must be resident at once).
+int fused_pivot_blocks(const Geometry& g);
+hipError_t launch_pivot_defer(const Geometry& g, const Defer& d, int32_t* basis, PricePart* pp,
+                              DevState* st, Cand* partials, int nblocks, double tol_dj,
+                              double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
+                              hipStream_t s);
 // nranks == 1: P[s] + objective row + pricing partials + log in one pass;
 // nranks > 1: the owner's replayed pivot-row bits (others INT64_MIN) to prow_bits.
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,

@@ -75,6 +75,10 @@ struct dlp_session {
     dlp::DevState* host_st = nullptr;   // pinned
     ncclComm_t comm = nullptr;
     bool use_rccl = false;
+    // deferred, single rank: one launch for ratio + selection + pivot row (opt-in: measured
+    // equal to two launches, C2 24.7 vs 25.0 us/pivot, profiles/r02c/tune_*_fused.txt)
+    bool fuse_pivot = false;
+    bool fuse_fits = false;   // ... when K <= 32 and the grid fits 2 blocks per CU
     bool exchange = false;          // candidate all-gather + prow all-reduce path
     int64_t launched = 0;
     int status = DLP_RUNNING;
@@ -198,7 +202,7 @@ void free_session(dlp_session* s) {
     for (auto e : s->ev) (void)hipEventDestroy(e);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     void* dev[] = {s->T, s->colq, s->prow_send, s->partials, s->cand_send, s->cand_recv,
-                   s->pp, s->basis, s->st, s->log, s->d.C, s->d.P, s->d.rhs, s->d.nzc};
+                   s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc, s->d.P, s->d.rhs, s->d.nzc};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
@@ -344,6 +348,12 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     }
     g.T = s->T;
     s->ratio_blocks = dlp::ratio_blocks(g);
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess)
+            cus = 0;
+        s->fuse_fits = s->d.K > 1 && s->d.K <= 32 && dlp::fused_pivot_blocks(g) <= 2 * cus;
+    }
     s->ratio_blocks_max = std::max(s->ratio_blocks, dlp::ratio_defer_blocks(g));
     HIP_TRY(hipMalloc(&s->colq, sizeof(double) * (rows_total + dlp::kColqPad)));
     HIP_TRY(hipMemsetAsync(s->colq, 0, sizeof(double) * (rows_total + dlp::kColqPad), s->stream));
@@ -365,6 +375,9 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     if (s->d.K > 1) {
         s->d.ldc = s->d.K;
         HIP_TRY(hipMalloc(&s->d.C, sizeof(double) * s->d.K * (rows_total + 1)));
+        s->d.ldcc = (rows_total + 1 + 63) / 64 * 64;
+        HIP_TRY(hipMalloc(&s->d.Cc, sizeof(double) * s->d.K * s->d.ldcc));
+        HIP_TRY(hipMemsetAsync(s->d.Cc, 0, sizeof(double) * s->d.K * s->d.ldcc, s->stream));
         // P is sized for the pass template's block (K rounded up to 4/8/16/32/64), so a
         // kernel instance never addresses past it, whatever the session's K
         const int64_t kt = s->d.K <= 4 ? 4 : s->d.K <= 8 ? 8 : s->d.K <= 16 ? 16 : s->d.K <= 32 ? 32 : 64;
@@ -467,6 +480,12 @@ int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
     hipEvent_t* ev = s->ev_per_pivot == 5 ? &s->ev[(size_t)slot * 5] : nullptr;
     hipEvent_t* evp = s->ev_per_pivot == 2 ? &s->ev[(size_t)slot * 2] : nullptr;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s->stream));
+    if (!s->exchange && s->fuse_pivot && s->fuse_fits && !ev) {
+        // single rank: ratio test, selection and pivot row in one launch
+        HIP_TRY(dlp::launch_pivot_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
+                                        s->ratio_blocks_max, o.tol_dj, o.tol_piv, o.pricing, s->log,
+                                        s->log_cap, s->stream));
+    } else {
     HIP_TRY(dlp::launch_ratio_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
                                     s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
                                     o.tol_piv, o.pricing, s->log, s->log_cap, s->stream));
@@ -485,6 +504,7 @@ int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
                                s->comm, s->stream));
         HIP_TRY(dlp::launch_commit_defer(s->g, s->d, s->st, s->prow_recv, s->pp, o.tol_dj, s->log,
                                          s->log_cap, s->stream));
+    }
     }
     if (ev) HIP_TRY(hipEventRecord(ev[3], s->stream));
     s->since_flush += 1;
@@ -1328,6 +1348,14 @@ int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
     }
     s->defer_occ = occupancy;
     if (form >= 0) s->d.form = form;
+    if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
+    if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
+    return DLP_OK;
+}
+
+int dlp_session_set_fused_pivot(dlp_session* s, int on) {
+    if (!s || on < 0 || on > 1) return DLP_ERR_ARG;
+    s->fuse_pivot = on != 0;
     if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
     if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
     return DLP_OK;

@@ -291,6 +291,11 @@ class Session:
                 "dlp_session_update_stats")
         return n.value, ms.value, k.value
 
+    def set_fused_pivot(self, on: bool = True):
+        """Deferred single-rank sessions: ratio test + selection + pivot row as one launch."""
+        L.check(L.lib().dlp_session_set_fused_pivot(self._h, 1 if on else 0),
+                "dlp_session_set_fused_pivot")
+
     def set_defer_tuning(self, occupancy: int, form: int = -1):
         """Deferred pass: workgroups/CU cap (0 = none) and form (0 wide, 1/2 narrow x 2/4 rows;
         scalar-coefficient 3 = 1 double x 4 rows, 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows)."""

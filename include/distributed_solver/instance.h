@@ -21,6 +21,11 @@
 
 namespace distributed_solver {
 
+// One advertiser's primal entries: impression -> (current x, running-average x),
+// the element type of the reference's solution_ (R/instance.h:34, a
+// __gnu_cxx::hash_map there).
+typedef std::unordered_map<int, std::pair<long double, long double>> PrimalRow;
+
 class Instance {
   public:
     // R/instance.h:41-42.  num_slots must be 1 (every reference scenario).
@@ -37,6 +42,16 @@ class Instance {
     void GenerateInstance();
     // R/instance.cpp:136-141 (called by the constructor, as in the reference).
     void SetBudgets();
+    // R/instance.h:47-48.  The reference's bodies have every file operation
+    // commented out (R/instance.cpp:59-115); these write what those comments
+    // describe: <handle>AxIxSxSPARSITY.csv, one line per advertiser of
+    // "impression,bid," pairs (impressions ascending, std::to_string formatting).
+    // GenerateAndWriteInstance draws the bids as GenerateInstance does and
+    // writes the one shard <name>.csv@0 (the reference's shard count is an
+    // uninitialised member, R/instance.h:26).  Both return nothing and print as
+    // the reference prints; a file that cannot be opened throws.
+    void WriteInstanceToCSV(std::string file_name_handle);
+    void GenerateAndWriteInstance(std::string file_name_handle);
 
     // R/instance.h:52-53.  The reference's MW loop on the GPU (dlp_mw_*, sort
     // mode, fp64 spec of DESIGN.md §9); prints the reference's per-iteration
@@ -48,6 +63,15 @@ class Instance {
                                   long double numerical_accuracy_tolerance, bool binary,
                                   long double scale, int intervals);
 
+    // R/instance.h:55-57 (statics over a caller's solution vector, as the MW
+    // loop uses them, R/allocation_mw.cpp:287-291; and BuildPrimals, public in
+    // the reference): running average x_avg = (t-1)/t x_avg + 1/t x
+    // (R/instance.cpp:143-152); one (0, 0) pair per bid (R/instance.cpp:154-165);
+    // current x := 0 (R/instance.cpp:167-176).
+    static void UpdateAvgPrimal(int t, std::vector<PrimalRow>* solution);
+    void BuildPrimals();
+    static void ResetCurrentPrimal(std::vector<PrimalRow>* sol);
+
     // Added entry: solve the same LP EXACTLY with the dense-tableau simplex;
     // returns a dlp status; Solution() pairs are then (x*, x*).
     int RunSimplex(const dlp_options& options);
@@ -55,10 +79,7 @@ class Instance {
 
     // Results.  Solution()[a][i] = (current x_ai, averaged x_ai) as in the
     // reference's solution_ (both equal the exact optimum here).
-    const std::vector<std::unordered_map<int, std::pair<long double, long double>>>& Solution()
-        const {
-        return solution_;
-    }
+    const std::vector<PrimalRow>& Solution() const { return solution_; }
     long double DualValue() const { return dual_value_; }
     long double MaxInfeasibility() const;   // max_a (sum_i b_ai x_ai - B_a)/B_a, cf. R/allocation_mw.cpp:205-232
     long double Revenue() const;            // sum b_ai x_ai, cf. R/allocation_mw.cpp:235-251
@@ -71,15 +92,15 @@ class Instance {
     bool verbose = true;        // print as the reference does
 
   private:
-    void BuildPrimals();
     void ReportGraphTopology();
+    std::string CsvName(const std::string& handle) const;
 
     int num_advertisers_, num_impressions_, num_slots_;
     long double bid_sparsity_, epsilon_, scaling_factor_, numerical_accuracy_tolerance_;
     std::vector<long double> budgets_;
     std::vector<std::unordered_map<int, long double>> bids_matrix_;
     std::vector<std::unordered_map<int, long double>> transpose_bids_matrix_;
-    std::vector<std::unordered_map<int, std::pair<long double, long double>>> solution_;
+    std::vector<PrimalRow> solution_;
     dlp_problem* problem_ = nullptr;
     long double dual_value_ = 0;
     std::vector<dlp_mw_iter> mw_log_;

@@ -284,11 +284,23 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
  *   LDS-staged coefficients: 0 = 2 doubles per lane (K <= 32), 1 / 2 = 1 double
  *   per lane x 2 / 4 rows per iteration;
  *   scalar-load coefficients: 3 = 1 double x 4 rows, 4 = 2 doubles x 2 rows
- *   (K <= 32), 5 = 1 double x 8 rows.
- * Default: 4 at K = 32 on a tableau > 1 GiB, else 3.  rows_per_block
- * (set_tuning) is the pass's row band.  Results are bit-identical for every
- * setting. */
+ *   (K <= 32), 5 = 1 double x 8 rows;
+ *   streamed (buffer ops, dense-group ring; K < 16 runs form 3): 6-9 = XCD
+ *   band-group order, 10-13 = tile-fastest order, 16-19 = XCD tile-range order,
+ *   each as {2 doubles x 2 rows, ring 4 (K <= 32); 2 x 2, ring 2 (K <= 32);
+ *   1 x 4, ring 4; 1 x 4, ring 2};
+ *   14 = form 4 for full blocks + the streamed partial-block kernel (K <= 32),
+ *   15 = the same with the full-block kernel held to 3 waves per SIMD.
+ * Default: 14 at K = 32 on a tableau > 1 GiB and at K = 16 below, else 3.
+ * rows_per_block (set_tuning) is the pass's row band.  Results are
+ * bit-identical for every setting. */
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
+/* Deferred single-rank sessions (K <= 32): run the ratio test, the selection
+ * and the pivot row as one fused launch per pivot (1) or as two launches (0,
+ * the default: the in-launch hand-off costs what the kernel boundary does).
+ * Bit-identical either way; timing >= 2 (per-phase events) always uses two
+ * launches. */
+int dlp_session_set_fused_pivot(dlp_session* s, int on);
 /* Current deferred-pass settings (K = 1: form -1). */
 int dlp_session_get_defer_tuning(dlp_session* s, int* occupancy, int* form, int* K);
 int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,

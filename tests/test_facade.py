@@ -33,6 +33,35 @@ def test_topology_matches_reference_binary(driver):
     assert out.startswith("Generated instance")
 
 
+def test_rest_of_the_reference_surface(tmp_path):
+    """WriteInstanceToCSV / GenerateAndWriteInstance (R/instance.h:47-48) write
+    the reference's commented-out CSV (one line per advertiser, its bids);
+    UpdateAvgPrimal / ResetCurrentPrimal / BuildPrimals (R/instance.h:55-57)."""
+    exe = os.path.join(ROOT, "build", "facade_surface")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "facade_surface.cpp"),
+                    "-L", os.path.join(ROOT, "distributedlpsolver_amd"), "-ldlp",
+                    f"-Wl,-rpath,{os.path.join(ROOT, 'distributedlpsolver_amd')}", "-o", exe],
+                   check=True)
+    handle = str(tmp_path / "inst_")
+    out = subprocess.run([exe, "100", "100", "0.1", handle], capture_output=True, text=True,
+                         check=True).stdout
+    assert "check avg 1 reset 1" in out
+    name = f"{handle}100x100x1x0.100000.csv"
+    for path in (name, name + "@0"):
+        with open(path) as f:
+            lines = f.read().splitlines()
+        assert len(lines) == 100
+        nnz = sum(len(line.rstrip(",").split(",")) // 2 for line in lines if line)
+        m = re.search(r"check pairs (\d+)", out)
+        assert nnz == int(m.group(1))
+        for line in lines[:5]:
+            vals = line.rstrip(",").split(",")
+            imps = [int(v) for v in vals[0::2]]
+            assert imps == sorted(imps) and all(0 <= i < 100 for i in imps)
+            assert all(0.0 < float(v) <= 1.0 + 1e-6 for v in vals[1::2])
+
+
 _LINE = r"status (\S+) pivots (\d+) objective (\S+) revenue (\S+) max_infeasibility (\S+)"
 
 

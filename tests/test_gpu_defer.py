@@ -110,6 +110,30 @@ def test_defer_streamed_forms_many_bands(form, K, rb):
     assert Td.tobytes() == Te.tobytes()
 
 
+@pytest.mark.parametrize("K", [8, 16, 32])
+@pytest.mark.parametrize("fused", [False, True])
+def test_fused_pivot_toggle(K, fused):
+    """Ratio test + selection + pivot row in one launch (default for single-rank
+    deferred sessions) or in two: both bit-identical to the oracle, incl. the
+    optimal stop inside a window (the fused launch's early release)."""
+    A, b, c = O.gen_dense(200, 400, 4)
+    ref = O.solve_dense(A, b, c)
+    with dlp.Session(dlp.Problem.dense(A, b, c), defer=K, check_interval=37) as s:
+        s.set_fused_pivot(fused)
+        s.run(10 ** 6)
+        res = s.result()
+    _check(res, ref)
+
+
+def test_fused_pivot_unbounded():
+    A = np.array([[1.0, -1.0], [-1.0, 0.0]])
+    b = np.array([1.0, 0.0])
+    c = np.array([1.0, 1.0])
+    with dlp.Session(dlp.Problem.dense(A, b, c), defer=8) as s:
+        st, _ = s.run(100)
+        assert st == L.UNBOUNDED
+
+
 def test_defer_retune_between_runs():
     A, b, c = O.gen_dense(200, 400, 2)
     ref = O.solve_dense(A, b, c)

@@ -28,6 +28,7 @@ ap.add_argument("--rbs", default="32,64,128")
 ap.add_argument("--occs", default="0,2,4")
 ap.add_argument("--nts", default="1")
 ap.add_argument("--forms", default="2")
+ap.add_argument("--fused", default="1", help="fused single-rank pivot launch: 0, 1 or 0,1")
 ap.add_argument("--blocks", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--timing", type=int, default=2)
@@ -45,19 +46,21 @@ for K in map(int, a.ks.split(",")):
     print(f"session K={K} ready", flush=True)
 any_s = next(iter(sess.values()))
 bytes_pass = 16.0 * any_s.rows * (any_s.ncols + 1)
-cfgs = [(K, rb, occ, nt, fm) for K in sess for rb in map(int, a.rbs.split(","))
+cfgs = [(K, rb, occ, nt, fm, fu) for K in sess for rb in map(int, a.rbs.split(","))
         for occ in map(int, a.occs.split(",")) for nt in map(int, a.nts.split(","))
-        for fm in map(int, a.forms.split(",")) if not (fm in (0, 4) and K > 32)]
+        for fm in map(int, a.forms.split(",")) for fu in map(int, a.fused.split(","))
+        if not (fm in (0, 4, 6, 7, 10, 11, 14, 15, 16, 17) and K > 32)]
 res = {c: {"wall": [], "pass": []} for c in cfgs}
 rng = random.Random(0)
 for r in range(a.rounds):
     order = cfgs[:]
     rng.shuffle(order)
     for c in order:
-        K, rb, occ, nt, fm = c
+        K, rb, occ, nt, fm, fu = c
         s = sess[K]
         s.set_tuning(22, rb, nt)
         s.set_defer_tuning(occ, fm)
+        s.set_fused_pivot(bool(fu))
         s.run(K)   # first window after a retune (graph rebuild) is not timed
         s.reset_timings()
         s.status()
@@ -75,13 +78,13 @@ rows = []
 for c, v in res.items():
     w = statistics.median(v["wall"])
     p = statistics.median(v["pass"]) if v["pass"] else float("nan")
-    rows.append(dict(K=c[0], rows_per_block=c[1], occupancy=c[2], nontemporal=c[3], form=c[4],
+    rows.append(dict(K=c[0], rows_per_block=c[1], occupancy=c[2], nontemporal=c[3], form=c[4], fused=c[5],
                      ms_per_pivot=w, pivots_per_s=1e3 / w, pass_ms=p,
                      pass_gbs=bytes_pass / p / 1e6 if p == p else None))
 rows.sort(key=lambda d: d["ms_per_pivot"])
 for d in rows:
     print(f"K={d['K']:2d} rb={d['rows_per_block']:4d} occ={d['occupancy']} nt={d['nontemporal']} "
-          f"form={d['form']}  "
+          f"form={d['form']} fused={d['fused']}  "
           f"{d['ms_per_pivot']:.4f} ms/pivot  {d['pivots_per_s']:.0f} pivots/s  "
           f"pass {d['pass_ms']:.3f} ms  {d['pass_gbs'] or 0:.0f} GB/s")
 if a.out:
