@@ -51,7 +51,7 @@ class Options(C.Structure):
         ("pad_", C.c_int32),
         ("tol_feas", C.c_double),
         ("defer", C.c_int32),
-        ("pad2_", C.c_int32),
+        ("n_gpus", C.c_int32),
     ]
 
 
@@ -151,6 +151,7 @@ SIGNATURES = [
     ("dlp_session_tableau", C.c_int, [_P, _DP]),
     ("dlp_session_read_rows", C.c_int, [_P, _I64, _I64, _DP]),
     ("dlp_session_result", C.c_int, [_P, C.POINTER(_P)]),
+    ("dlp_sessions_result", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(_P)]),
     ("dlp_session_free", None, [_P]),
     ("dlp_mw_options_default", None, [C.POINTER(MWOptions)]),
     ("dlp_mw_create", C.c_int, [_P, C.POINTER(MWOptions), C.POINTER(_P)]),

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dlp_host.h"
@@ -116,6 +117,8 @@ struct dlp_session {
     std::vector<uint8_t> ev_flush;   // per timed slot: a pass ran in it
     int64_t upd_launches = 0;
 };
+
+extern "C" int flush_pending(dlp_session* s);   // defined with the C entry points
 
 namespace {
 
@@ -225,8 +228,12 @@ int validate_options(const dlp_options* o) {
     return DLP_OK;
 }
 
+// comm_in: a communicator made by the caller (dlp_solve's in-process multi-device
+// path, ncclCommInitAll); the session then owns it.  uid: a unique id shared by
+// P processes (ncclCommInitRank here).  Either one means the RCCL exchange.
 int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int nranks,
-                 const void* uid, dlp_session* s) {
+                 const void* uid, dlp_session* s, ncclComm_t comm_in = nullptr) {
+    const bool rccl = uid != nullptr || comm_in != nullptr;
     s->opt = *opt;
     s->device = opt->device;
     s->rank = rank;
@@ -308,7 +315,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     // caller drives the exchange itself (dlp_session_step_*) or when the chosen
     // rank-1 variant tiles pricing differently from the deferred kernels
     {
-        const bool host_driven = (nranks > 1 || uid != nullptr) && uid == nullptr;
+        const bool host_driven = nranks > 1 && !rccl;
         int K = opt->defer;
         if (K < 0 || K > dlp::kMaxDefer) {
             set_error("defer must be 0 (auto) or 1..64");
@@ -331,13 +338,13 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         }
         s->d.K = K;
         s->opt.defer = K;
-        // pass form 14: 2 doubles x 2 rows per lane for full blocks (form 4), the streamed
-        // kernel's partial instance for a window's last block (C3: full pass 6.30 ms; a
-        // 20-pivot partial pass 7.56 ms vs 12.7 ms with form 4's own partial instance,
-        // profiles/r02/tune_c3_k32_window20.txt), at K = 32 on a streaming tableau and K = 16
-        // on a cache-resident one (C2: pass 0.116 vs 0.128 ms for form 3, tune_c2.txt);
-        // 1 double x 4 rows elsewhere (K = 16 streaming: form 3 6.1 ms vs form 4 6.4, r01g)
-        s->d.form = ((K == 32 && s->streaming) || (K == 16 && !s->streaming)) ? 14 : 3;
+        // pass form 4 (2 doubles x 2 rows per lane; a window's partial last block runs the
+        // full-block code with zeroed coefficients: C3 20-pivot partial pass 6.93 ms vs a
+        // 6.30 ms full pass, 7.58 for the streamed kernel's (form 14), 12.7 before,
+        // profiles/r02c/) at K = 32 on a streaming tableau and K = 16 on a cache-resident one
+        // (C2: pass 0.116 vs 0.128 ms for form 3, profiles/r02b/tune_c2_forms.txt); 1 double
+        // x 4 rows elsewhere (K = 16 streaming: form 3 6.1 ms vs form 4 6.4, r01g)
+        s->d.form = ((K == 32 && s->streaming) || (K == 16 && !s->streaming)) ? 4 : 3;
     }
     g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block : auto_rows_per_block(s);
     g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
@@ -357,7 +364,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     s->ratio_blocks_max = std::max(s->ratio_blocks, dlp::ratio_defer_blocks(g));
     HIP_TRY(hipMalloc(&s->colq, sizeof(double) * (rows_total + dlp::kColqPad)));
     HIP_TRY(hipMemsetAsync(s->colq, 0, sizeof(double) * (rows_total + dlp::kColqPad), s->stream));
-    s->exchange = nranks > 1 || uid != nullptr;
+    s->exchange = nranks > 1 || rccl;
     HIP_TRY(hipMalloc(&s->prow_send, sizeof(int64_t) * s->ld));
     if (s->exchange)
         HIP_TRY(hipMalloc(&s->prow_recv, sizeof(int64_t) * s->ld));
@@ -419,7 +426,10 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     HIP_TRY(dlp::launch_price_init(g, s->pp, opt->tol_dj, opt->update_variant, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
 
-    if (uid) {
+    if (comm_in) {
+        s->comm = comm_in;
+        s->use_rccl = true;
+    } else if (uid) {
         ncclUniqueId id;
         std::memcpy(&id, uid, sizeof(id));
         NCCL_TRY(ncclCommInitRank(&s->comm, nranks, id, rank));
@@ -701,15 +711,15 @@ int run_window_graph(dlp_session* s, int64_t chunk) {
 // Before Phase II has started (infeasible, or a pivot limit in Phase I) the
 // objective is NaN and y is zero; x is the current (Phase I) point.
 int general_result(dlp_session* s, const std::vector<double>& z, const std::vector<double>& rhs,
-                   dlp_result* r) {
+                   dlp_result* r, int64_t row_first, int64_t rows_elig) {
     const dlp::StdForm& f = s->prob_dims.sf;
     const int64_t mu = s->prob_dims.m, nu = s->prob_dims.n;
     r->m = mu;
     r->n = nu;
     r->phase1_pivots = s->phase == 1 ? s->npivots : s->phase1_pivots;
     std::vector<double> xs(f.ns, 0.0);
-    for (int64_t il = 0; il < s->g.rows_elig; ++il) {
-        const int32_t v = r->basis[s->row_first + il];
+    for (int64_t il = 0; il < rows_elig; ++il) {
+        const int32_t v = r->basis[row_first + il];
         if (v < f.ns) xs[v] = rhs[il];
     }
     r->x.resize(nu);
@@ -736,7 +746,24 @@ int general_result(dlp_session* s, const std::vector<double>& z, const std::vect
     return DLP_OK;
 }
 
-int extract_result(dlp_session* s, dlp_result* r) {
+// The RHS column entries of this rank's ratio-eligible rows (the values of their
+// basic variables).
+int local_rhs(dlp_session* s, std::vector<double>& rhs) {
+    HIP_TRY(hipSetDevice(s->device));
+    rhs.assign(s->g.rows_elig, 0.0);
+    if (s->g.rows_elig > 0) {
+        HIP_TRY(dlp::launch_gather_column(s->T, s->ld, s->rows, s->N, s->colq, s->stream));
+        HIP_TRY(hipMemcpyAsync(rhs.data(), s->colq, sizeof(double) * s->g.rows_elig,
+                               hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
+    return DLP_OK;
+}
+
+// rhs_all != NULL: the eligible rows of EVERY rank in global row order (an
+// in-process row-block solve), so x covers all basic variables; else this
+// rank's rows only.
+int extract_result(dlp_session* s, dlp_result* r, const std::vector<double>* rhs_all = nullptr) {
     HIP_TRY(hipSetDevice(s->device));
     CALL_TRY(poll(s));
     r->m = s->m;
@@ -761,17 +788,125 @@ int extract_result(dlp_session* s, dlp_result* r) {
                                hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) r->timings[ph] = s->timings[ph];
-    const int64_t rows_elig = s->g.rows_elig;
-    if (s->general) return general_result(s, z, rhs, r);
+    const std::vector<double>& rh = rhs_all ? *rhs_all : rhs;
+    const int64_t rows_elig = rhs_all ? (int64_t)rhs_all->size() : s->g.rows_elig;
+    const int64_t row_first = rhs_all ? 0 : s->row_first;
+    if (s->general) return general_result(s, z, rh, r, row_first, rows_elig);
     r->objective = z[s->N];
     r->x.assign(s->n, 0.0);
     for (int64_t il = 0; il < rows_elig; ++il) {
-        const int32_t v = r->basis[s->row_first + il];
-        if (v < s->n) r->x[v] = rhs[il];
+        const int32_t v = r->basis[row_first + il];
+        if (v < s->n) r->x[v] = rh[il];
     }
     r->y.resize(s->m);
     for (int64_t i = 0; i < s->m; ++i) r->y[i] = z[s->n + i];
     return DLP_OK;
+}
+
+// One result for a row-block solve whose P rank sessions live in this process:
+// rank 0's objective row, basis and log (replicated on every rank) and every
+// rank's eligible RHS rows, concatenated in global row order.
+int merge_result(dlp_session* const* ss, int P, dlp_result* r) {
+    for (int k = 0; k < P; ++k) CALL_TRY(flush_pending(ss[k]));   // the RHS must be current
+    std::vector<std::pair<int64_t, int>> order;
+    for (int k = 0; k < P; ++k) order.push_back({ss[k]->row_first, k});
+    std::sort(order.begin(), order.end());
+    std::vector<double> all;
+    int64_t next = 0;
+    for (const auto& o : order) {
+        dlp_session* sk = ss[o.second];
+        if (sk->row_first != next) {
+            set_error("rank sessions do not tile the rows");
+            return DLP_ERR_ARG;
+        }
+        std::vector<double> loc;
+        CALL_TRY(local_rhs(sk, loc));
+        all.insert(all.end(), loc.begin(), loc.end());
+        next += sk->rows;
+    }
+    return extract_result(ss[order[0].second], r, &all);
+}
+
+// dlp_solve on n_gpus devices of this process: one RCCL communicator over
+// devices [device, device + P) (ncclCommInitAll, so a failed start cannot
+// leave a rank waiting), one host thread per device creating, running and
+// reading its rank ("single process, one host thread per
+// device").  The ranks advance in lockstep through the collectives.
+int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_result** out) {
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (o.device < 0 || o.device + P > ndev) {
+        set_error("n_gpus = " + std::to_string(P) + " from device " + std::to_string(o.device) +
+                  " exceeds the " + std::to_string(ndev) + " visible devices");
+        return DLP_ERR_NODEVICE;
+    }
+    std::vector<int> devs(P);
+    for (int r = 0; r < P; ++r) devs[r] = o.device + r;
+    std::vector<ncclComm_t> comms(P, nullptr);
+    NCCL_TRY(ncclCommInitAll(comms.data(), P, devs.data()));
+    std::vector<dlp_session*> ss(P, nullptr);
+    std::vector<int> rc(P, DLP_OK);
+    std::vector<std::string> err(P);
+    auto on_ranks = [&](auto&& fn) {
+        std::vector<std::thread> th;
+        for (int r = 0; r < P; ++r)
+            th.emplace_back([&, r] {
+                rc[r] = fn(r);
+                if (rc[r] < 0) err[r] = dlp_last_error();
+            });
+        for (auto& t : th) t.join();
+        for (int r = 0; r < P; ++r)
+            if (rc[r] < 0) {
+                set_error("rank " + std::to_string(r) + ": " + err[r]);
+                return rc[r];
+            }
+        return DLP_OK;
+    };
+    int res = on_ranks([&](int r) {
+        dlp_options orr = o;
+        orr.device = devs[r];
+        orr.n_gpus = 0;
+        auto* s = new (std::nothrow) dlp_session();
+        if (!s) return DLP_ERR_OOM;
+        int k = DLP_OK;
+        try {
+            k = session_init(prob, &orr, r, P, nullptr, s, comms[r]);
+        } catch (const std::exception& e) {
+            set_error(std::string("session_init: ") + e.what());
+            k = DLP_ERR_OOM;
+        }
+        if (k != DLP_OK) {
+            if (s->comm == comms[r]) s->comm = nullptr;   // freed below with the others
+            free_session(s);
+            return k;
+        }
+        comms[r] = nullptr;   // the session owns it now
+        ss[r] = s;
+        return DLP_OK;
+    });
+    if (res == DLP_OK) {
+        res = on_ranks([&](int r) {
+            int64_t done = 0;
+            return dlp_session_run(ss[r], o.max_pivots, &done);
+        });
+    }
+    if (res == DLP_OK) {
+        auto* r = new (std::nothrow) dlp_result();
+        if (!r) {
+            res = DLP_ERR_OOM;
+        } else {
+            res = merge_result(ss.data(), P, r);
+            if (res == DLP_OK)
+                *out = r;
+            else
+                delete r;
+        }
+    }
+    for (auto* s : ss)
+        if (s) free_session(s);
+    for (auto c : comms)
+        if (c) (void)ncclCommDestroy(c);
+    return res;
 }
 
 }  // namespace
@@ -1432,12 +1567,39 @@ int dlp_session_result(dlp_session* s, dlp_result** out) {
 
 void dlp_session_free(dlp_session* s) { free_session(s); }
 
+int dlp_sessions_result(dlp_session* const* ranks, int nranks, dlp_result** out) {
+    if (!ranks || nranks <= 0 || !out) return DLP_ERR_ARG;
+    for (int k = 0; k < nranks; ++k)
+        if (!ranks[k] || ranks[k]->nranks != nranks) {
+            set_error("dlp_sessions_result: every rank session of the solve, once each");
+            return DLP_ERR_ARG;
+        }
+    auto* r = new (std::nothrow) dlp_result();
+    if (!r) return DLP_ERR_OOM;
+    const int rc = merge_result(ranks, nranks, r);
+    if (rc != DLP_OK) {
+        delete r;
+        return rc;
+    }
+    *out = r;
+    return DLP_OK;
+}
+
 int dlp_solve(const dlp_problem* prob, const dlp_options* opt, dlp_result** out) {
     dlp_options o;
     if (opt)
         o = *opt;
     else
         dlp_options_default(&o);
+    if (!prob || !out) return DLP_ERR_ARG;
+    if (o.n_gpus < 0) {
+        set_error("n_gpus must be >= 0");
+        return DLP_ERR_ARG;
+    }
+    if (o.n_gpus >= 1) {
+        CALL_TRY(validate_options(&o));
+        return solve_in_process(prob, o, o.n_gpus, out);
+    }
     dlp_session* s = nullptr;
     CALL_TRY(dlp_session_create(prob, &o, &s));
     int64_t done = 0;

@@ -204,7 +204,8 @@ def options(**kw) -> L.Options:
 
 
 def solve(problem: Problem, **opts) -> Result:
-    """One-shot single-GPU solve (dlp_solve)."""
+    """One-shot solve (dlp_solve): one GPU, or n_gpus=N devices of this process
+    (row-block partition, one host thread + one RCCL rank per device)."""
     o = options(**opts)
     h = C.c_void_p()
     L.check(L.lib().dlp_solve(problem._h, C.byref(o), C.byref(h)), "dlp_solve")
@@ -330,6 +331,16 @@ class Session:
         h = C.c_void_p()
         L.check(L.lib().dlp_session_result(self._h, C.byref(h)), "dlp_session_result")
         return _result_from_handle(h, self.problem.m, self.problem.n)
+
+    @staticmethod
+    def merged_result(sessions) -> Result:
+        """One result for the rank sessions of a row-block solve that all live in
+        this process (dlp_sessions_result): x covers every basic variable."""
+        arr = (C.c_void_p * len(sessions))(*[s._h for s in sessions])
+        h = C.c_void_p()
+        L.check(L.lib().dlp_sessions_result(arr, len(sessions), C.byref(h)), "dlp_sessions_result")
+        p = sessions[0].problem
+        return _result_from_handle(h, p.m, p.n)
 
     def close(self):
         if self._h:

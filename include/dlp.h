@@ -143,7 +143,12 @@ typedef struct dlp_options {
                                 without an RCCL id, whose exchange the caller drives
                                 through dlp_session_step_*; a single-rank session driven
                                 through the step API keeps the size-based choice) */
-    int32_t pad2_;
+    int32_t n_gpus;          /* dlp_solve only: 0 (default) = one GPU, no communicator;
+                                N >= 1 = a row-block solve on devices [device, device+N) of
+                                this process: one host thread and one RCCL communicator
+                                rank per device (ncclCommInitAll); N = 1 runs that path on
+                                a 1-rank communicator.  Sessions ignore it (one process per
+                                GPU: dlp_session_create_rank). */
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
  * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;
@@ -239,7 +244,7 @@ int dlp_problem_adalloc_bids(const dlp_problem* prob, int64_t* nnz, int32_t* adv
                              int32_t* imp, double* bid);
 void dlp_problem_free(dlp_problem* prob);
 
-/* ---- one-shot solve (single GPU) ---------------------------------------- */
+/* ---- one-shot solve (one GPU, or opt->n_gpus GPUs of this process) -------- */
 int dlp_solve(const dlp_problem* prob, const dlp_options* opt, dlp_result** out);
 
 /* ---- sessions: tableau resident in HBM ---------------------------------- */
@@ -291,7 +296,7 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
  *   1 x 4, ring 4; 1 x 4, ring 2};
  *   14 = form 4 for full blocks + the streamed partial-block kernel (K <= 32),
  *   15 = the same with the full-block kernel held to 3 waves per SIMD.
- * Default: 14 at K = 32 on a tableau > 1 GiB and at K = 16 below, else 3.
+ * Default: 4 at K = 32 on a tableau > 1 GiB and at K = 16 below, else 3.
  * rows_per_block (set_tuning) is the pass's row band.  Results are
  * bit-identical for every setting. */
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
@@ -310,6 +315,10 @@ int dlp_session_tableau(dlp_session* s, double* host);
 /* Copy local rows [first, first+count) (row rows_local = objective) to the host. */
 int dlp_session_read_rows(dlp_session* s, int64_t first, int64_t count, double* host);
 int dlp_session_result(dlp_session* s, dlp_result** out);
+/* One result for a row-block solve whose rank sessions all live in this
+ * process (any order): x covers every basic variable (a single rank's
+ * dlp_session_result covers its own rows only). */
+int dlp_sessions_result(dlp_session* const* ranks, int nranks, dlp_result** out);
 void dlp_session_free(dlp_session* s);
 
 /* ---- batched small LPs ------------------

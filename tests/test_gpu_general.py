@@ -128,8 +128,20 @@ def test_general_multi_rank_sessions_one_gpu(P, name):
         assert r.basis.tobytes() == ref.basis.tobytes()
     x = np.sum([r.x for r in results], axis=0) - (P - 1) * _x_base(lp)
     np.testing.assert_allclose(x, ref.x, rtol=0, atol=1e-12 * (1 + np.abs(ref.x).max()))
+    # the in-process merge maps every rank's basic rows back to user variables: bit-exact
+    merged = dlp.Session.merged_result(sess)
+    _check(merged, ref)
     for s in sess:
         s.close()
+
+
+@pytest.mark.parametrize("name", ["lpgen_2d_20x20_eq", "enzo_c_infeasible", "random_60x100"])
+def test_general_solve_n_gpus_in_process(name):
+    cs = next(c for c in CASES if c["name"] == name)
+    lp = fixture_lp(cs)
+    ref = O.solve_general(lp)
+    res = dlp.solve(dlp.Problem.general(*lp_arrays(lp)), n_gpus=1)
+    _check(res, ref)
 
 
 @pytest.mark.parametrize("name", ["lpgen_2d_20x20_eq", "network_flow", "enzo_c_infeasible"])

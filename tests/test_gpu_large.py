@@ -85,7 +85,7 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K):
         occ, form, K = s.get_defer_tuning()
         assert K == want_K
         if K == 32:
-            assert form == 14 and s.get_tuning()[1] == 256   # the bench's pass (form 4 body)
+            assert form == 4 and s.get_tuning()[1] == 256   # the bench's pass
         done = 0
         while done < k:
             st, d = s.run(min(ci, k - done))
@@ -112,8 +112,8 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K):
 
 def test_c3_full_blocks_bit_exact():
     """C3 at the bench geometry: 2 full K = 32 blocks through the full-block
-    pass instance (form 14 = form 4's body, 256-row bands, ld 66048, nt), then
-    an 8-pivot tail through the partial-block instance (the streamed kernel)."""
+    pass instance (form 4, 256-row bands, ld 66048, nt), then an 8-pivot
+    tail through the partial-block instance."""
     _full_blocks_vs_oracle(32768, 32768, 3, 72, 64, 32)
 
 

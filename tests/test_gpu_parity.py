@@ -179,8 +179,24 @@ def test_multi_rank_sessions_one_gpu(P):
         np.testing.assert_array_equal(r.y, ref.y)
     x = np.sum([r.x for r in results], axis=0)   # each basic row lives on one rank
     assert x.tobytes() == ref.x.tobytes()
+    # the in-process merge (dlp_sessions_result), ranks in any order
+    merged = dlp.Session.merged_result(sess[::-1])
+    assert merged.x.tobytes() == ref.x.tobytes() and merged.y.tobytes() == ref.y.tobytes()
+    _same_log(merged.pivot_log, ref.pivot_log)
     for s in sess:
         s.close()
+
+
+@pytest.mark.parametrize("defer", [0, 1, 16])
+def test_solve_n_gpus_in_process(defer):
+    """dlp_solve with n_gpus = 1: the in-process multi-device path (ncclCommInitAll,
+    one host thread per device, RCCL exchange, merged result) on this box's GPU."""
+    A, b, c = O.gen_dense(200, 400, 1)
+    ref = O.solve_dense(A, b, c)
+    res = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, defer=defer)
+    _check_equal(res, ref)
+    with pytest.raises(L.DLPError):
+        dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=dlp.device_count() + 1)
 
 
 @pytest.mark.parametrize("defer", [0, 1, 16, 32])
