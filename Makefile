@@ -11,7 +11,7 @@ HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinc
              -Wall -Wno-unused-function
 LIBDLP    := $(PKG)/libdlp.so
 OBJS      := build/dlp_kernels.o build/dlp_batched.o build/dlp_mw.o build/dlp_session.o build/dlp_adalloc.o \
-             build/dlp_instance.o build/dlp_general.o build/dlp_defer.o
+             build/dlp_instance.o build/dlp_general.o build/dlp_defer.o build/dlp_cluster.o
 
 all: $(LIBDLP) oracle tools
 

@@ -48,7 +48,7 @@ class Options(C.Structure):
         ("use_graph", C.c_int32),
         ("update_variant", C.c_int32),
         ("ld_align", C.c_int32),
-        ("pad_", C.c_int32),
+        ("small_lp", C.c_int32),
         ("tol_feas", C.c_double),
         ("defer", C.c_int32),
         ("n_gpus", C.c_int32),

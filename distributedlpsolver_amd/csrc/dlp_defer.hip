@@ -752,18 +752,6 @@ __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, 
                 for (int e = 0; e < V; ++e)
                     t[u][e] = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
     };
-    // the chunk holding step kb-1 of a partial block: steps >= kb are skipped by a
-    // uniform branch per step (per-element selects cost this instance ~85 VGPRs)
-    auto chain_part = [&](double (&t)[U][V], const double (&f)[U][LC], int l0) {
-#pragma unroll
-        for (int l = 0; l < LC; ++l)
-            if (l0 + l < kb)
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int e = 0; e < V; ++e)
-                        t[u][e] = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
-    };
     // a partial block runs the full-block code: chunks past step kb-1 are skipped, and in
     // the chunk holding it the coefficients of steps >= kb are zeroed (scalar selects).
     // With P[l] = +0 for l >= kb (above) such a step is fma(-(+0), +0, t) = t + (-0) = t

@@ -169,6 +169,16 @@ hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits
 hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,
                          const DevState* st, PricePart* pp, double tol_dj, dlp_pivot* log,
                          int64_t log_cap, bool nontemporal, int variant, hipStream_t s);
+// Small LPs: the tableau in the LDS of nwg workgroups (cluster_plan; 0 = does not
+// fit), `max_pivots` pivots of the eager rule per launch (dlp_cluster.hip).
+size_t cluster_lds_bytes(int64_t m, int cw);
+int cluster_plan(int64_t m, int64_t N, int max_wg, int* cw_out);
+int64_t cluster_gstride(int64_t m);
+int64_t cluster_granules(int64_t m, int nwg);   // uint64 hand-off words of a launch
+hipError_t launch_cluster(const Geometry& g, int64_t m, int64_t n, int nwg, int cw, DevState* st,
+                          int32_t* basis, dlp_pivot* log, int64_t log_cap, uint64_t* gran,
+                          int64_t max_pivots, int pricing, double tol_dj, double tol_piv,
+                          hipStream_t s, uint64_t* stamps = nullptr);
 // Synthetic tableau rows [row_first, row_first+rows) + objective row, on device.
 hipError_t launch_generate(const Geometry& g, int kind, int64_t m, int64_t n, uint64_t seed,
                            hipStream_t s);

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -80,6 +81,10 @@ struct dlp_session {
     // equal to two launches, C2 24.7 vs 25.0 us/pivot, profiles/r02c/tune_*_fused.txt)
     bool fuse_pivot = false;
     bool fuse_fits = false;   // ... when K <= 32 and the grid fits 2 blocks per CU
+    // small LPs: the whole window in one launch, tableau in the LDS of cl_wg workgroups
+    bool cluster = false;
+    int cl_wg = 0, cl_cw = 0;
+    uint64_t* cl_gran = nullptr;   // hand-off granules of the cluster launch
     bool exchange = false;          // candidate all-gather + prow all-reduce path
     int64_t launched = 0;
     int status = DLP_RUNNING;
@@ -205,7 +210,8 @@ void free_session(dlp_session* s) {
     for (auto e : s->ev) (void)hipEventDestroy(e);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     void* dev[] = {s->T, s->colq, s->prow_send, s->partials, s->cand_send, s->cand_recv,
-                   s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc, s->d.P, s->d.rhs, s->d.nzc};
+                   s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc, s->d.P, s->d.rhs, s->d.nzc,
+                   s->cl_gran};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
@@ -326,8 +332,31 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         // (C4 256x512: 14.2 µs/pivot eager vs 19.0 at K = 16; 1024x1024: 18.0 vs 20.8;
         // C2 4096x8192, 268 MB: K = 16 is 2.3x eager; profiles/r01j/tune_small_defer.txt)
         const bool tiny = (double)(s->rows + 1) * (double)s->width * 8.0 < (double)(32ll << 20);
+        // small LPs (auto: tiny, default kernels; or forced by small_lp = 1): one launch per
+        // window with the tableau in LDS, when it fits the CUs' LDS (dlp_cluster.hip)
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess)
+            cus = 0;
+        if (!s->general && nranks == 1 && !rccl && s->m < (1 << 30) && s->N < (1 << 30) &&
+            (opt->small_lp == 1 ||
+             (opt->small_lp == 0 && K == 0 && tiny && opt->update_variant < 0))) {
+            s->cl_wg = dlp::cluster_plan(s->m, s->N, cus, &s->cl_cw);
+            // tuning only: DLP_CLUSTER_WG=G forces the workgroup count (if the slices fit)
+            if (const char* e = std::getenv("DLP_CLUSTER_WG")) {
+                const int gw = std::atoi(e);
+                const int cw = gw > 0 ? (int)((s->N + gw) / gw) : 0;
+                if (gw > 0 && gw <= cus && (int64_t)(gw - 1) * cw < s->N + 1 &&
+                    dlp::cluster_lds_bytes(s->m, cw) <= 160 * 1024 - 1024) {
+                    s->cl_wg = gw;
+                    s->cl_cw = cw;
+                }
+            }
+            s->cluster = s->cl_wg > 0;
+        }
         if (K == 0)
-            K = (host_driven || tile != dlp::kDeferTile || tiny) ? 1 : (s->streaming ? 32 : 16);
+            K = (host_driven || tile != dlp::kDeferTile || tiny || s->cluster) ? 1
+                                                                             : (s->streaming ? 32 : 16);
+        if (s->cluster && K != 1) s->cluster = false;
         if (K > 1 && tile != dlp::kDeferTile) {
             set_error("defer > 1 needs a 512-column update variant");
             return DLP_ERR_ARG;
@@ -354,6 +383,9 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         return DLP_ERR_OOM;
     }
     g.T = s->T;
+    if (s->cluster) {
+        HIP_TRY(hipMalloc(&s->cl_gran, sizeof(uint64_t) * dlp::cluster_granules(s->m, s->cl_wg)));
+    }
     s->ratio_blocks = dlp::ratio_blocks(g);
     {
         int cus = 0;
@@ -527,6 +559,42 @@ int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
     return DLP_OK;
 }
 
+// Small LPs: `count` pivots in one launch, the tableau in LDS; the HBM tableau,
+// basis, log and state are current afterwards, and the pricing partials are
+// rebuilt so that the multi-kernel path (the step API) can continue from it.
+int enqueue_cluster(dlp_session* s, int64_t count) {
+    const dlp_options& o = s->opt;
+    hipEvent_t* ev = s->ev_per_pivot ? &s->ev[0] : nullptr;
+    if (ev)
+        for (int k = 0; k < s->ev_per_pivot - 1; ++k) HIP_TRY(hipEventRecord(ev[k], s->stream));
+    // diagnostic: DLP_CLUSTER_STAMPS=<file> dumps s_memtime per phase of the first 64 pivots
+    // of the first window (tools only; never set in a timed run)
+    static const char* stamp_path = std::getenv("DLP_CLUSTER_STAMPS");
+    uint64_t* stamps = nullptr;
+    if (stamp_path) {
+        HIP_TRY(hipMalloc(&stamps, sizeof(uint64_t) * 16 * 64 * s->cl_wg));
+        HIP_TRY(hipMemsetAsync(stamps, 0, sizeof(uint64_t) * 16 * 64 * s->cl_wg, s->stream));
+    }
+    HIP_TRY(dlp::launch_cluster(s->g, s->m, s->n, s->cl_wg, s->cl_cw, s->st, s->basis, s->log,
+                                s->log_cap, s->cl_gran, count, o.pricing, o.tol_dj, o.tol_piv,
+                                s->stream, stamps));
+    if (stamps) {
+        std::vector<uint64_t> h(16 * 64 * s->cl_wg);
+        HIP_TRY(hipMemcpyAsync(h.data(), stamps, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost,
+                               s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        HIP_TRY(hipFree(stamps));
+        if (FILE* f = std::fopen(stamp_path, "wb")) {
+            std::fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+            std::fclose(f);
+        }
+    }
+    if (ev) HIP_TRY(hipEventRecord(ev[s->ev_per_pivot - 1], s->stream));
+    HIP_TRY(dlp::launch_price_init(s->g, s->pp, o.tol_dj, o.update_variant, s->stream));
+    s->ev_pending = ev ? 1 : 0;
+    return DLP_OK;
+}
+
 int enqueue_pivot(dlp_session* s, int64_t slot, bool last = true) {
     if (s->d.K > 1) return enqueue_pivot_defer(s, slot, last);
     hipEvent_t* ev = s->ev_per_pivot ? &s->ev[(size_t)slot * s->ev_per_pivot] : nullptr;
@@ -648,6 +716,14 @@ int poll(dlp_session* s) {
     if (s->host_st->status != DLP_RUNNING && s->host_st->status != dlp::kStatusSkip &&
         s->status == DLP_RUNNING)
         s->status = s->host_st->status;
+    if (s->cluster && s->ev_per_pivot && s->ev_pending > 0) {   // one launch per window
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, s->ev[0], s->ev[s->ev_per_pivot - 1]));
+        s->timings[DLP_PHASE_UPDATE] += ms;
+        s->nsamples += s->npivots - before;
+        s->upd_launches += 1;
+        s->ev_pending = 0;
+    }
     if (s->ev_per_pivot && s->ev_pending > 0) {
         const int64_t real = std::min<int64_t>(s->ev_pending, s->npivots - before);
         for (int64_t k = 0; k < real; ++k) {
@@ -1272,8 +1348,12 @@ int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
             }
             continue;
         }
-        const int64_t chunk = std::min<int64_t>(budget, s->opt.check_interval);
-        if (graph && chunk == s->opt.check_interval) {
+        // a small-LP window is one launch that stops by itself at the optimum: poll less
+        const int64_t chunk = std::min<int64_t>(
+            budget, s->cluster ? std::max<int64_t>(s->opt.check_interval, 1024) : s->opt.check_interval);
+        if (s->cluster) {
+            CALL_TRY(enqueue_cluster(s, chunk));
+        } else if (graph && chunk == s->opt.check_interval) {
             CALL_TRY(run_window_graph(s, chunk));
         } else {
             for (int64_t k = 0; k < chunk; ++k) CALL_TRY(enqueue_pivot(s, k, k == chunk - 1));

@@ -133,7 +133,10 @@ typedef struct dlp_options {
     int32_t ld_align;        /* tableau row stride alignment in doubles, multiple of 16, 0 = auto
                                 (default: 512 when a row has >= 4096 columns, else 16); the
                                 kernels only touch the first roundup(N+1,16) columns */
-    int32_t pad_;
+    int32_t small_lp;        /* one-launch LDS solve for small LPs (dlp_cluster.hip): 0 = auto
+                                (default: single-rank dense / random / ad-allocation problems
+                                whose tableau is under 32 MiB and fits the LDS of the device's
+                                CUs), 1 = whenever it fits, -1 = never */
     double  tol_feas;        /* general LPs: infeasible when the Phase I optimum is below
                                 -tol_feas * (1 + max_i b'_i) (default 1e-9) */
     int32_t defer;           /* pivots per tableau pass (deferred rank-k update, results

@@ -1,0 +1,95 @@
+"""Small LPs in one launch per window (dlp_cluster.hip): the tableau in the LDS
+of G workgroups, two in-kernel hand-offs per pivot.  Bit-identical to the
+oracle and to the multi-kernel path: pivot logs, x, y, basis, objective, for
+dense, degenerate (Bland) and ad-allocation LPs, every window length, resumed
+runs and the step API continuing a cluster session."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+import distributedlpsolver_amd as dlp
+from distributedlpsolver_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_log(got, ref):
+    assert len(got) == len(ref), (len(got), len(ref))
+    g, r = np.ascontiguousarray(got), np.ascontiguousarray(ref)
+    if g.tobytes() != r.tobytes():
+        for k in range(len(r)):
+            if g[k].tobytes() != r[k].tobytes():
+                raise AssertionError(f"pivot {k}: gpu {g[k]} oracle {r[k]}")
+
+
+def _check(res, ref):
+    assert res.status == ref.status
+    _same_log(res.pivot_log, ref.pivot_log)
+    assert np.float64(res.objective).tobytes() == np.float64(ref.objective).tobytes()
+    assert res.x.tobytes() == ref.x.tobytes() and res.y.tobytes() == ref.y.tobytes()
+    assert res.basis.tobytes() == ref.basis.tobytes()
+
+
+@pytest.mark.parametrize("m,n,seed,deg", [(200, 400, 1, False), (64, 64, 2, False),
+                                          (3, 700, 2, False), (500, 3, 1, False),
+                                          (256, 512, 3, True), (128, 128, 3, True),
+                                          (1024, 1024, 5, False)])
+@pytest.mark.parametrize("pricing", [0, 1])
+def test_cluster_solve_matches_oracle(m, n, seed, deg, pricing):
+    if pricing == 1 and m * n > 300 * 600:
+        pytest.skip("pure Bland on the large dense LP takes tens of thousands of pivots")
+    A, b, c = O.gen_dense(m, n, seed, degenerate=deg)
+    ref = O.solve_dense(A, b, c, pricing=pricing)
+    res = dlp.solve(dlp.Problem.dense(A, b, c), small_lp=1, pricing=pricing, max_pivots=200_000)
+    _check(res, ref)
+
+
+@pytest.mark.parametrize("ci", [1, 7, 64, 1000])
+def test_cluster_windows_and_resume(ci):
+    A, b, c = O.gen_dense(200, 400, 6)
+    ref = O.solve_dense(A, b, c)
+    with dlp.Session(dlp.Problem.dense(A, b, c), small_lp=1, check_interval=ci, timing=1) as s:
+        st = L.RUNNING
+        while st == L.RUNNING:
+            st, _ = s.run(37)
+        res = s.result()
+        n, ms, _ = s.update_stats()
+    _check(res, ref)
+    assert n >= 1 and ms > 0
+
+
+def test_cluster_auto_policy_and_off_switch():
+    A, b, c = O.gen_dense(200, 400, 7)
+    ref = O.solve_dense(A, b, c)
+    for small in (0, -1):   # auto picks the cluster launch for this size; -1 = multi-kernel
+        _check(dlp.solve(dlp.Problem.dense(A, b, c), small_lp=small), ref)
+
+
+def test_cluster_step_api_continues():
+    """A cluster session's windows leave the HBM state (tableau, basis, pricing
+    partials) current: the step API's eager kernels continue from it."""
+    A, b, c = O.gen_dense(150, 170, 4)
+    ref = O.solve_dense(A, b, c)
+    with dlp.Session(dlp.Problem.dense(A, b, c), small_lp=1, check_interval=10) as s:
+        s.run(30)
+        for _ in range(10_000):
+            cand = s.step_candidate()
+            if s.status()[0] != L.RUNNING:
+                break
+            prow = s.step_select(cand)
+            s.step_update(prow)
+        res = s.result()
+    _check(res, ref)
+
+
+def test_cluster_adalloc_and_unbounded():
+    p = dlp.Problem.adalloc(100, 100, 1, 0.1, 0.25)
+    M, b, c = O.adalloc_lp(100, 100, 0.1, 0.25)
+    ref = O.solve_dense(M, b, c)
+    _check(dlp.solve(p, small_lp=1), ref)
+    A = np.array([[-1.0, 1.0], [1.0, -2.0]])
+    res = dlp.solve(dlp.Problem.dense(A, np.array([1.0, 2.0]), np.array([1.0, 1.0])), small_lp=1)
+    ref = O.solve_dense(A, np.array([1.0, 2.0]), np.array([1.0, 1.0]))
+    assert res.status == ref.status == L.UNBOUNDED
+    _same_log(res.pivot_log, ref.pivot_log)
