@@ -1,8 +1,9 @@
 // dlp_batched.hip — C5: thousands of independent small LPs, one workgroup per
-// LP, the whole (m+1) x (N+1) fp64 tableau resident in LDS (65 x 129 x 8 B =
-// 67 KB at m = n = 64, so two workgroups per CU of 160 KB).  HBM is touched
-// once per LP (load the generated tableau, store the outputs); every pivot is
-// LDS traffic plus workgroup barriers.
+// LP, the tableau's nonbasic columns + RHS resident in LDS ((m+1) x (n+1) fp64:
+// 65 x 129 x 8 B = 67 KB at 64 x 128, two workgroups per CU of 160 KB; 34 KB at
+// 64 x 64, four).  HBM is touched once per LP (load the generated tableau,
+// store the outputs); every pivot is LDS traffic plus workgroup barriers
+// (SURVEY.md §8a row a6).
 //
 // Pivot rule and arithmetic are exactly the big-tableau path's (dlp.h header):
 // Dantzig/Bland pricing with index ties, ratio test with basis-index ties,
@@ -79,80 +80,101 @@ struct BatchOut {
     int64_t log_cap;
 };
 
-// One workgroup = one LP.  LDS image: T[(m+1)][W] with W = N+1 (row stride
-// W is odd for even N, so a column read by consecutive rows walks the banks),
-// then prow[W], colq[m+1], basis[m], and a small reduction scratch.
-__global__ __launch_bounds__(256) void batched_solve_kernel(const double* __restrict__ Tg,
+// One workgroup = one LP.  The LDS holds only the NONBASIC columns of the
+// tableau (+ the RHS): a basic variable's column is a unit vector, so storing
+// it buys nothing, and dropping it takes the 64 x 128 tableau from 100 KB to
+// 67 KB (two LPs per CU instead of one) and 64 x 64 from 67 KB to 34 KB.
+// LDS image: T[(m+1)][W] with W = n + 1 (slots 0..n-1, RHS at slot n),
+// colq[m+1], prow[W], var[n] (the variable in each slot), basis[m], scratch.
+//
+// Same values as the full tableau: when q enters at slot s_q and l leaves row
+// p, slot s_q takes l's column.  In the full tableau that column is e_p (1.0
+// exactly at row p, a signed zero elsewhere), so its new entries are
+// prow_l = 1.0 / piv at row p and fma(-colq[i], prow_l, 0) elsewhere (or the
+// zero, when colq[i] == 0): the same bits as the full update, up to the sign
+// of a zero, which reaches no output (every later value that depends on it is
+// a fma / division whose result does not).  Pricing runs over the slots with
+// the full tableau's order: min z, ties -> smallest VARIABLE index; Bland ->
+// the smallest variable index with z < -tol.
+__global__ __launch_bounds__(512) void batched_solve_kernel(const double* __restrict__ Tg,
                                                             int64_t ldg, int m, int n,
                                                             int64_t max_pivots, int pricing,
                                                             double tol_dj, double tol_piv,
                                                             BatchOut out) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int N = n + m, W = N + 1;
-    double* T = smem;
-    double* prow = T + (m + 1) * W;
-    double* colq = prow + W;
-    int32_t* basis = (int32_t*)(colq + (m + 1));
-    // scratch: [0] q, [1] p, [2] status, [3] bland ; doubles: piv, ratio
-    int32_t* sI = basis + m + (m & 1);
-    double* sD = (double*)(sI + 4);
+    const int N = n + m, W = n + 1;
+    double* T = smem;                                   // (m+1) x W
+    double* colq = T + (m + 1) * W;                     // m+1
+    double* prow = colq + (m + 1);                      // W
+    int32_t* var = (int32_t*)(prow + W);                // n
+    int32_t* basis = var + n;                           // m
+    // scratch: [0] q (variable), [1] slot of q, [2] p, [3] status, [4] bland
+    int32_t* sI = basis + m;
+    double* sD = (double*)(sI + 6 + ((n + m) & 1));     // piv, ratio (8-B aligned)
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t lp = blockIdx.x;
     const double* src = Tg + lp * (m + 1) * ldg;
-    for (int e = tid; e < (m + 1) * W; e += blockDim.x) {
-        const int r = e / W, c = e - r * W;
-        T[e] = src[(int64_t)r * ldg + c];
-    }
+    for (int i = 0; i <= m; ++i)
+        for (int s = tid; s < W; s += blockDim.x) T[i * W + s] = src[(int64_t)i * ldg + (s < n ? s : N)];
+    for (int s = tid; s < n; s += blockDim.x) var[s] = s;
     for (int i = tid; i < m; i += blockDim.x) basis[i] = n + i;
     if (tid == 0) {
-        sI[2] = DLP_RUNNING;
-        sI[3] = pricing == DLP_PRICING_BLAND ? 1 : 0;
+        sI[3] = DLP_RUNNING;
+        sI[4] = pricing == DLP_PRICING_BLAND ? 1 : 0;
     }
     __syncthreads();
 
     int64_t k = 0;
     for (; k < max_pivots; ++k) {
-        // ---- a1 pricing (wave 0): lexicographic (z, j) min + first j < -tol
+        // ---- a1 pricing (wave 0): lexicographic (z, variable) min + first variable < -tol
         if (wid == 0) {
             double zmin = __builtin_inf();
-            int jmin = kNoIndex, jb = kNoIndex;
+            int vmin = kNoIndex, smin = -1, vb = kNoIndex, sb = -1;
             const double* z = T + m * W;
-            for (int j = lane; j < N; j += 64) {
-                const double v = z[j];
-                if (v < zmin) { zmin = v; jmin = j; }
-                if (v < -tol_dj && jb == kNoIndex) jb = j;
+            for (int s = lane; s < n; s += 64) {
+                const double v = z[s];
+                const int vr = var[s];
+                if (v < zmin || (v == zmin && vr < vmin)) { zmin = v; vmin = vr; smin = s; }
+                if (v < -tol_dj && vr < vb) { vb = vr; sb = s; }
             }
 #pragma unroll
-            for (int s = 32; s >= 1; s >>= 1) {
-                const double oz = __shfl_xor(zmin, s);
-                const int oj = __shfl_xor(jmin, s), ob = __shfl_xor(jb, s);
-                if (oz < zmin || (oz == zmin && oj < jmin)) { zmin = oz; jmin = oj; }
-                jb = ob < jb ? ob : jb;
+            for (int sh = 32; sh >= 1; sh >>= 1) {
+                const double oz = __shfl_xor(zmin, sh);
+                const int ov = __shfl_xor(vmin, sh), os = __shfl_xor(smin, sh);
+                const int ob = __shfl_xor(vb, sh), osb = __shfl_xor(sb, sh);
+                if (oz < zmin || (oz == zmin && ov < vmin)) { zmin = oz; vmin = ov; smin = os; }
+                if (ob < vb) { vb = ob; sb = osb; }
             }
             if (lane == 0) {
-                int q;
-                if (sI[3]) q = jb;
-                else q = (jmin != kNoIndex && zmin < -tol_dj) ? jmin : kNoIndex;
+                int q = kNoIndex, sq = -1;
+                if (sI[4]) {
+                    q = vb;
+                    sq = sb;
+                } else if (vmin != kNoIndex && zmin < -tol_dj) {
+                    q = vmin;
+                    sq = smin;
+                }
                 sI[0] = (q == kNoIndex) ? -1 : q;
+                sI[1] = sq;
             }
         }
         __syncthreads();
-        const int q = sI[0];
+        const int q = sI[0], sq = sI[1];
         if (q < 0) {
-            if (tid == 0) sI[2] = DLP_OK;
+            if (tid == 0) sI[3] = DLP_OK;
             break;
         }
         // ---- a2 ratio test (wave 0) + colq capture (all)
-        for (int i = tid; i <= m; i += blockDim.x) colq[i] = T[i * W + q];
+        for (int i = tid; i <= m; i += blockDim.x) colq[i] = T[i * W + sq];
         if (wid == 0) {
             Cand best;
             best.valid = 0; best.ratio = 0.0; best.basis_var = kNoIndex; best.row = -1;
             best.pad0 = 0; best.pivot = 0.0;
             for (int i = lane; i < m; i += 64) {
-                const double a = T[i * W + q];
+                const double a = T[i * W + sq];
                 if (a > tol_piv) {
-                    double rhs = T[i * W + N];
+                    double rhs = T[i * W + n];
                     if (!(rhs > 0.0)) rhs = 0.0;
                     Cand c;
                     c.ratio = rhs / a; c.basis_var = basis[i]; c.row = i; c.valid = 1;
@@ -161,25 +183,26 @@ __global__ __launch_bounds__(256) void batched_solve_kernel(const double* __rest
                 }
             }
 #pragma unroll
-            for (int s = 32; s >= 1; s >>= 1) {
+            for (int sh = 32; sh >= 1; sh >>= 1) {
                 Cand o;
-                o.ratio = __shfl_xor(best.ratio, s);
-                o.basis_var = __shfl_xor(best.basis_var, s);
-                o.row = __shfl_xor(best.row, s);
-                o.valid = __shfl_xor(best.valid, s);
+                o.ratio = __shfl_xor(best.ratio, sh);
+                o.basis_var = __shfl_xor(best.basis_var, sh);
+                o.row = __shfl_xor(best.row, sh);
+                o.valid = __shfl_xor(best.valid, sh);
                 o.pad0 = 0;
-                o.pivot = __shfl_xor(best.pivot, s);
+                o.pivot = __shfl_xor(best.pivot, sh);
                 if (cand_better(o, best)) best = o;
             }
             if (lane == 0) {
                 if (!best.valid) {
-                    sI[1] = -1;
+                    sI[2] = -1;
                 } else {   // a4 select + log
                     const int p = best.row;
                     const int leaving = basis[p];
                     basis[p] = q;
-                    sI[1] = p;
-                    sI[3] = (pricing == DLP_PRICING_BLAND) ? 1 : (best.ratio == 0.0 ? 1 : 0);
+                    var[sq] = leaving;   // the entering slot now holds the leaving variable
+                    sI[2] = p;
+                    sI[4] = (pricing == DLP_PRICING_BLAND) ? 1 : (best.ratio == 0.0 ? 1 : 0);
                     sD[0] = best.pivot;
                     sD[1] = best.ratio;
                     if (out.logs && k < out.log_cap) {
@@ -192,40 +215,54 @@ __global__ __launch_bounds__(256) void batched_solve_kernel(const double* __rest
             }
         }
         __syncthreads();
-        const int p = sI[1];
+        const int p = sI[2];
         if (p < 0) {
-            if (tid == 0) sI[2] = DLP_UNBOUNDED;
+            if (tid == 0) sI[3] = DLP_UNBOUNDED;
             break;
         }
-        // ---- a3 pivot row (IEEE division) then elimination
+        // ---- a3 pivot row (IEEE division), then the elimination: work items (slot,
+        // row group), R row groups so that the lanes share it evenly; rows 8 at a time,
+        // loads first
         const double piv = sD[0];
-        for (int j = tid; j < W; j += blockDim.x) prow[j] = T[p * W + j] / piv;
+        for (int s = tid; s < W; s += blockDim.x) prow[s] = (s == sq ? 1.0 : T[p * W + s]) / piv;
         __syncthreads();
         {
-            int i = tid / W, j = tid - (tid / W) * W;
-            const int step_i = blockDim.x / W, step_j = blockDim.x - step_i * W;
-            for (; i <= m;) {
-                if (i == p) {
-                    T[i * W + j] = prow[j];
-                } else {
-                    const double f = colq[i];
-                    if (f != 0.0) T[i * W + j] = __builtin_fma(-f, prow[j], T[i * W + j]);
+            // R row groups with W * R <= blockDim.x: no lane takes a second item
+            const int R = W >= (int)blockDim.x ? 1 : (int)(blockDim.x / W);
+            const int rpg = (m + 1 + R - 1) / R;
+            for (int item = tid; item < W * R; item += blockDim.x) {
+                const int rg = item / W, s = item - rg * W;
+                const bool ent = s == sq;               // slot of q -> column of the leaving var
+                const double pj = prow[s];
+                const int ib = rg * rpg, ie = min(ib + rpg, m + 1);
+                for (int i0 = ib; i0 < ie; i0 += 8) {
+                    double t[8], f[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int i = min(i0 + u, ie - 1);
+                        f[u] = colq[i];
+                        t[u] = ent ? 0.0 : T[i * W + s];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int i = i0 + u;
+                        const double v = __builtin_fma(-f[u], pj, t[u]);
+                        const double nv = (i == p) ? pj : (f[u] != 0.0 ? v : t[u]);
+                        if (i < ie) T[i * W + s] = nv;
+                    }
                 }
-                i += step_i;
-                j += step_j;
-                if (j >= W) { j -= W; ++i; }
             }
         }
         __syncthreads();
         if (tid == 0 && out.logs && k < out.log_cap)
-            out.logs[lp * out.log_cap + k].objective = T[m * W + N];
+            out.logs[lp * out.log_cap + k].objective = T[m * W + n];
     }
     if (tid == 0) {
-        int stt = sI[2];
+        int stt = sI[3];
         if (stt == DLP_RUNNING) stt = DLP_PIVOT_LIMIT;
         if (out.status) out.status[lp] = stt;
         if (out.npivots) out.npivots[lp] = k;
-        if (out.objective) out.objective[lp] = T[m * W + N];
+        if (out.objective) out.objective[lp] = T[m * W + n];
     }
     if (out.basis)
         for (int i = tid; i < m; i += blockDim.x) out.basis[lp * m + i] = basis[i];
@@ -255,9 +292,9 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
         dlp::set_error("dlp_batched_solve: bad arguments");
         return DLP_ERR_ARG;
     }
-    const int64_t N = n + m, W = N + 1, ldg = (N + 1 + 15) / 16 * 16;
-    const size_t lds = sizeof(double) * ((m + 1) * W + W + (m + 1)) + sizeof(int32_t) * (m + 1 + 4) +
-                       sizeof(double) * 4 + 16;
+    const int64_t N = n + m, ldg = (N + 1 + 15) / 16 * 16;
+    const size_t lds = sizeof(double) * ((m + 1) * (n + 1) + (m + 1) + (n + 1)) + sizeof(int32_t) * (n + m + 8) +
+                       sizeof(double) * 2 + 16;
     int rc = DLP_OK;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -300,7 +337,9 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
         HIP_BTRY(hipFuncSetAttribute((const void*)dlp::batched_solve_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         HIP_BTRY(hipEventRecord(e0, s));
-        dlp::batched_solve_kernel<<<(unsigned)nlp, 256, lds, s>>>(
+        // 512 lanes per LP when few LPs share a CU (LDS > 40 KB each), else 256
+        const unsigned threads = lds > 40 * 1024 ? 512 : 256;
+        dlp::batched_solve_kernel<<<(unsigned)nlp, threads, lds, s>>>(
             dT, ldg, (int)m, (int)n, o.max_pivots, o.pricing, o.tol_dj, o.tol_piv, bo);
         HIP_BTRY(hipGetLastError());
         HIP_BTRY(hipEventRecord(e1, s));
