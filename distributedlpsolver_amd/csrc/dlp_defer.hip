@@ -684,7 +684,7 @@ __device__ inline void strow(double* p, const double (&t)[V]) {
 // address space, wave-uniform loads of them are always scalar loads.
 typedef __attribute__((address_space(4))) const double* cdptr;
 
-template <bool NT, int K, int V, int U, bool PART>
+template <bool NT, int K, int V, int U, bool PART, bool DEEP = false>
 __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, int64_t rows,
                                             int64_t width, const DevState* __restrict__ st,
                                             const double* __restrict__ C, int64_t ldc,
@@ -800,6 +800,36 @@ __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, 
     double ta[U][V], tb[U][V];
     int r = 0;
     while (r < nr) {
+        if (DEEP && dense_at(r)) {
+            // form 20: three register buffers, so the rows of the next TWO dense groups
+            // are in flight while one group's chains run
+            double tc[U][V];
+            load(ta, r);
+            bool nb = dense_at(r + U);
+            load(tb, nb ? r + U : r);
+            while (true) {
+                const bool nc = nb && dense_at(r + 2 * U);
+                load(tc, nc ? r + 2 * U : r);
+                __builtin_amdgcn_sched_barrier(0);
+                group(ta, r);
+                r += U;
+                if (!nb) break;
+                const bool nd = nc && dense_at(r + 2 * U);
+                load(ta, nd ? r + 2 * U : r);
+                __builtin_amdgcn_sched_barrier(0);
+                group(tb, r);
+                r += U;
+                if (!nc) break;
+                const bool ne = nd && dense_at(r + 2 * U);
+                load(tb, ne ? r + 2 * U : r);
+                __builtin_amdgcn_sched_barrier(0);
+                group(tc, r);
+                r += U;
+                if (!nd) break;
+                nb = ne;
+            }
+            continue;
+        }
         if (dense_at(r)) {
             // a run of dense groups, ping-ponging two register buffers
             load(ta, r);
@@ -852,14 +882,14 @@ __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, 
     }
 }
 
-template <bool NT, int K, int V, int U, bool PART>
+template <bool NT, int K, int V, int U, bool PART, bool DEEP = false>
 __global__ __launch_bounds__(256) void pass_s_kernel(double* __restrict__ T, int64_t ld,
                                                      int64_t rows, int64_t width,
                                                      const DevState* __restrict__ st,
                                                      const double* __restrict__ C, int64_t ldc,
                                                      const double* __restrict__ P,
                                                      const int32_t* __restrict__ nzc, int rb) {
-    pass_s_body<NT, K, V, U, PART>(T, ld, rows, width, st, C, ldc, P, nzc, rb);
+    pass_s_body<NT, K, V, U, PART, DEEP>(T, ld, rows, width, st, C, ldc, P, nzc, rb);
 }
 
 // The same body held to 3 waves per SIMD (<= 168 VGPRs; form 4 alone takes 170, which
@@ -1262,7 +1292,8 @@ static void launch_pass_r(const Geometry& g, const Defer& d, DevState* st, int r
 template <bool NT, int K>
 static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
                        hipStream_t s) {
-    if (d.form >= 6 && d.form != 14 && d.form != 15 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31)) {
+    if (d.form >= 6 && d.form <= 19 && d.form != 14 && d.form != 15 &&
+        (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31)) {
         // streamed forms (K >= 16, a band within one 2 GiB buffer descriptor; else form 3)
         if constexpr (K >= 16) {
             if ((d.form == 6 || d.form == 7 || d.form == 10 || d.form == 11 || d.form == 16 ||
@@ -1293,7 +1324,7 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
         }
     }
     // streamed forms need K >= 16 (an even number of coefficient chunks): form 3 below
-    const int form = (d.form >= 6 && d.form != 14 && d.form != 15) ? 3 : d.form;
+    const int form = (d.form >= 6 && d.form != 14 && d.form != 15 && d.form != 20) ? 3 : d.form;
     const int cols = (form == 0 || form == 4 || form >= 14) ? kDeferTile : 256;
     const int ntiles = (int)((g.width + cols - 1) / cols);
     const int64_t bands = (g.rows + rb - 1) / rb;
@@ -1320,6 +1351,14 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
                                                                      d.C, d.ldc, d.P, d.nzc, rb);
             pass_s_kernel<NT, K, 1, 4, true><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
                                                                     d.C, d.ldc, d.P, d.nzc, rb);
+        } else if (form == 20) {
+            if constexpr (K <= 32) {
+                pass_s_kernel<NT, K, 2, 2, false, true><<<grid, 256, dyn, s>>>(
+                    g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
+                    g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+            } else
+                return hipErrorInvalidValue;
         } else if (form == 4 || form == 14 || form == 15) {
             if constexpr (K <= 32) {
                 if (form == 15)

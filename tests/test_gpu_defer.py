@@ -68,7 +68,8 @@ def test_defer_degenerate_bland(K, pricing):
                                               (64, 64, 0, 1, 12), (32, 37, 0, 1, 13),
                                               (32, 256, 0, 1, 14), (16, 64, 0, 0, 14), (8, 64, 0, 1, 14),
                                               (32, 256, 0, 1, 15), (24, 64, 0, 0, 15), (32, 16, 4, 1, 16),
-                                              (16, 64, 0, 0, 17), (64, 32, 0, 1, 18), (32, 8, 0, 1, 19)])
+                                              (16, 64, 0, 0, 17), (64, 32, 0, 1, 18), (32, 8, 0, 1, 19),
+                                              (32, 256, 0, 1, 20), (16, 64, 0, 0, 20), (24, 33, 0, 1, 20)])
 def test_defer_pass_geometry_and_tableau(K, rb, occ, nt, form):
     """Whole tableau after 45 pivots equals the eager session's, byte for byte."""
     m, n, seed = 300, 520, 5
@@ -140,7 +141,7 @@ def test_defer_retune_between_runs():
     with dlp.Session(dlp.Problem.dense(A, b, c), defer=16, check_interval=9) as s:
         for k in range(1000):
             s.set_tuning(22 if k % 2 else 26, [16, 64, 200][k % 3], k % 2)
-            s.set_defer_tuning([0, 4, 2][k % 3], k % 20)
+            s.set_defer_tuning([0, 4, 2][k % 3], k % 21)
             st, _ = s.run(11)
             if st != L.RUNNING:
                 break
