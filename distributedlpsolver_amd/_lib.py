@@ -79,17 +79,19 @@ class Candidate(C.Structure):
 
 class MWOptions(C.Structure):
     _fields_ = [("device", C.c_int32), ("binary", C.c_int32), ("epsilon", C.c_double),
-                ("tolerance", C.c_double)]
+                ("tolerance", C.c_double), ("scale", C.c_double), ("intervals", C.c_int32),
+                ("pad_", C.c_int32)]
 
 
 class MWIter(C.Structure):
     _fields_ = [("dual_value", C.c_double), ("max_infeasibility", C.c_double),
-                ("infeasible_advertiser", C.c_int32), ("pad", C.c_int32),
+                ("infeasible_advertiser", C.c_int32), ("search_levels", C.c_int32),
                 ("min_weight", C.c_double), ("max_weight", C.c_double),
                 ("weighted_budget", C.c_double)]
 
 
 assert C.sizeof(Pivot) == 32 and C.sizeof(Candidate) == 32 and C.sizeof(MWIter) == 48
+assert C.sizeof(MWOptions) == 40
 
 _P = C.c_void_p
 _I64 = C.c_int64

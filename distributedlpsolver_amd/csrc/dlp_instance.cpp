@@ -172,36 +172,60 @@ int Instance::RunSimplex(const dlp_options& options) {
     return status_;
 }
 
-// R/instance.cpp:117-134 -> R/allocation_mw.cpp:271-326: the MW loop, on the
-// GPU (dlp_mw_*), sort mode.  binary = true (R/main.cpp:36) selects the
-// reference's bisection budget split, whose 1e-16 stop is below fp64
-// resolution; the sort-mode split is used instead and a note
-// is printed.  Prints the reference's per-iteration report lines.
-void Instance::RunMultiplicativeWeights(long double num_iterations,
-                                        long double numerical_accuracy_tolerance, bool binary) {
-    if (!problem_) GenerateInstance();
-    BuildPrimals();
-    if (binary && verbose)
-        std::cout << "note: binary-search budget split is not reproducible in fp64; using sort mode\n";
+// R/instance.cpp:117-141 -> R/allocation_mw.cpp:271-326: the MW loop on the
+// GPU (dlp_mw_*), sort mode (binary = false) or the threshold search
+// (binary = true, R/global_problem.cpp:46-222, the mode R/main.cpp:36 runs)
+// with the fp64 spec of DESIGN.md §9.  Prints the reference's per-iteration
+// report lines.
+namespace {
+void run_mw(dlp_problem* problem, long double epsilon, int T, long double tol, bool binary,
+            double scale, int intervals, std::vector<dlp_mw_iter>& log, std::vector<double>& xa,
+            std::vector<double>& xc) {
     dlp_mw_options o;
     dlp_mw_options_default(&o);
-    o.epsilon = (double)epsilon_;
-    o.tolerance = (double)numerical_accuracy_tolerance;
+    o.epsilon = (double)epsilon;
+    o.tolerance = (double)tol;
+    o.binary = binary ? 1 : 0;
+    o.scale = scale;
+    o.intervals = intervals;
     dlp_mw* mw = nullptr;
-    int rc = dlp_mw_create(problem_, &o, &mw);
+    int rc = dlp_mw_create(problem, &o, &mw);
     if (rc != DLP_OK) throw std::runtime_error(std::string("RunMultiplicativeWeights: ") + dlp_last_error());
-    const int T = (int)num_iterations;
-    std::vector<dlp_mw_iter> log(T > 0 ? T : 1);
+    log.assign(T > 0 ? T : 1, dlp_mw_iter{});
     rc = dlp_mw_run(mw, T, log.data(), nullptr);
     if (rc != DLP_OK) {
         dlp_mw_free(mw);
         throw std::runtime_error(std::string("RunMultiplicativeWeights: ") + dlp_last_error());
     }
     int64_t m = 0, n = 0;
-    dlp_problem_dims(problem_, &m, &n);
-    std::vector<double> xa(n), xc(n);
+    dlp_problem_dims(problem, &m, &n);
+    xa.assign(n, 0.0);
+    xc.assign(n, 0.0);
     dlp_mw_solution(mw, xa.data(), xc.data(), nullptr);
     dlp_mw_free(mw);
+}
+}  // namespace
+
+void Instance::RunMultiplicativeWeights(long double num_iterations,
+                                        long double numerical_accuracy_tolerance, bool binary) {
+    // The reference's 3-argument path leaves cr_transition_scale_ and
+    // num_bin_intervals_ unset (R/global_problem.cpp:18-27); binary = true here
+    // takes R/main.cpp's values (1 - epsilon * 0.001, 3).
+    RunMultiplicativeWeights(num_iterations, numerical_accuracy_tolerance, binary,
+                             1 - epsilon_ * 0.001, 3);
+}
+
+void Instance::RunMultiplicativeWeights(long double num_iterations,
+                                        long double numerical_accuracy_tolerance, bool binary,
+                                        long double scale, int intervals) {
+    if (!problem_) GenerateInstance();
+    BuildPrimals();
+    const int T = (int)num_iterations;
+    std::vector<dlp_mw_iter> log;
+    std::vector<double> xa, xc;
+    run_mw(problem_, epsilon_, T, numerical_accuracy_tolerance, binary, (double)scale, intervals, log,
+           xa, xc);
+    const int64_t n = (int64_t)xa.size();
     std::vector<int32_t> adv(n), imp(n);
     int64_t nnz = n;
     dlp_problem_adalloc_bids(problem_, &nnz, adv.data(), imp.data(), nullptr);
@@ -218,14 +242,6 @@ void Instance::RunMultiplicativeWeights(long double num_iterations,
     dual_value_ = T > 0 ? log[T - 1].dual_value : 0.0L;
     status_ = DLP_OK;
     num_pivots_ = 0;
-}
-
-void Instance::RunMultiplicativeWeights(long double num_iterations,
-                                        long double numerical_accuracy_tolerance, bool binary,
-                                        long double scale, int intervals) {
-    (void)scale;
-    (void)intervals;
-    RunMultiplicativeWeights(num_iterations, numerical_accuracy_tolerance, binary);
 }
 
 long double Instance::MaxInfeasibility() const {

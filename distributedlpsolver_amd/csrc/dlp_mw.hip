@@ -19,6 +19,18 @@
 // points in LDS, then the monotone chain on one lane); a stable hipCUB radix
 // sort of all regions by slope; a chunked budget prefix; one lane per
 // impression / advertiser for primal and weights.
+//
+// Binary (threshold-search) mode, R/global_problem.cpp:46-222, 283-292, the
+// mode R/main.cpp:36 runs (spec: oracle/oracle_mw.cpp header): no sort.  The
+// search state lives on the device; one launch per search level evaluates the
+// nr critical ratios over all regions (one lane per impression, a 256-lane
+// tree per block) and the block that finishes last reduces the block sums
+// and applies the reference's bracket / expand / stop rule, so levels queue
+// back to back with no host round trip (the host polls `done` once per batch
+// of launches).  Instances whose impressions fit one workgroup run the whole
+// search inside one launch.  The tie allocation is the one serial step of the
+// reference (remaining budget shrinks tie by tie): compacted tie list, one
+// wave walking it with the budget in a uniform register.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -194,18 +206,19 @@ __global__ void region_count_kernel(const int32_t* __restrict__ hull_h, int I, i
 // Regions in (impression asc, region asc) order: key = slope u_j, value = id.
 __global__ void emit_regions_kernel(const int64_t* __restrict__ iptr, const int32_t* __restrict__ hull_h,
                                     const int32_t* __restrict__ roff, const double* __restrict__ env_u,
-                                    int I, double* keys, int32_t* ids, int32_t* reg_imp,
-                                    int32_t* reg_j) {
+                                    const double* __restrict__ cut, int I, double* keys, int32_t* ids,
+                                    int32_t* reg_imp, int32_t* reg_j, double* rwidth) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= I) return;
     const int h = hull_h[i];
-    const int64_t bu = iptr[i] + i;
+    const int64_t bu = iptr[i] + i, bc = iptr[i] + 2 * (int64_t)i;
     for (int j = 0; j + 1 < h; ++j) {
         const int id = roff[i] + j;
         keys[id] = env_u[bu + j];
         ids[id] = id;
         reg_imp[id] = i;
         reg_j[id] = j;
+        if (rwidth) rwidth[id] = cut[bc + j + 1] - cut[bc + j];
     }
 }
 
@@ -267,7 +280,7 @@ __global__ void primal_kernel(const int64_t* __restrict__ iptr, const int32_t* _
                               const int32_t* __restrict__ hull_h, const int32_t* __restrict__ roff,
                               const double* __restrict__ env_u, const double* __restrict__ env_v,
                               const double* __restrict__ inc_by_id, const int32_t* __restrict__ pos_by_id,
-                              int I, double tight_tol, double* __restrict__ x,
+                              int I, double tight_tol, int binary, double* __restrict__ x,
                               double* __restrict__ dcontrib) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= I) return;
@@ -276,11 +289,21 @@ __global__ void primal_kernel(const int64_t* __restrict__ iptr, const int32_t* _
     dcontrib[i] = 0.0;
     const int h = hull_h[i];
     if (h < 2) return;
-    // visit this impression's regions in global sorted order
     double beta = 0.0;
     int jstar = -1;
+    if (binary) {
+        // binary mode: pos_by_id holds the region state (1 full, 2 tie); full
+        // regions first, then ties, each in region order (R/global_problem.cpp:166-221)
+        for (int pass = 1; pass <= 2; ++pass)
+            for (int j = 0; j < h - 1; ++j)
+                if (pos_by_id[roff[i] + j] == pass) {
+                    beta = beta + inc_by_id[roff[i] + j];
+                    jstar = j;
+                }
+    }
+    // sort mode: visit this impression's regions in global sorted order
     int last = -1;
-    for (int step = 0; step < h - 1; ++step) {
+    for (int step = 0; !binary && step < h - 1; ++step) {
         int best = -1, bpos = 0x7fffffff;
         for (int j = 0; j < h - 1; ++j) {
             const int pos = pos_by_id[roff[i] + j];
@@ -370,6 +393,9 @@ __global__ void advertiser_kernel(const int64_t* __restrict__ aptr, const int64_
     w[a] = w[a] * f;
 }
 
+struct BinState;
+__device__ inline int bin_levels(const BinState* st);
+
 // Per-iteration report (one wave): worst average infeasibility (first index
 // on ties), min / max weight; writes log[t].
 __global__ __launch_bounds__(64) void report_kernel(const double* __restrict__ avg_slack,
@@ -377,6 +403,7 @@ __global__ __launch_bounds__(64) void report_kernel(const double* __restrict__ a
                                                     const double* __restrict__ w, int A,
                                                     const double* __restrict__ dual,
                                                     const double* __restrict__ Bptr,
+                                                    const BinState* __restrict__ bst,
                                                     dlp_mw_iter* __restrict__ log) {
     double worst = 0.0, mn = 100000.0, mx = 0.0;
     int wi = -1;
@@ -402,12 +429,379 @@ __global__ __launch_bounds__(64) void report_kernel(const double* __restrict__ a
         e.dual_value = *dual;
         e.max_infeasibility = worst;
         e.infeasible_advertiser = wi;
-        e.pad = 0;
+        e.search_levels = bst ? bin_levels(bst) : 0;
         e.min_weight = mn;
         e.max_weight = mx;
         e.weighted_budget = *Bptr;
         *log = e;
     }
+}
+
+// ---------------------------------------------------------------- binary mode
+constexpr int kBinMaxRatios = 8;      // num_bin_intervals accepted (the reference uses 3)
+constexpr int kBinMaxLevels = 2048;   // spec: level cap
+constexpr int kBinBlock = 256;        // spec: block of the blocked sum
+constexpr int kBinSingleBlocks = 64;  // whole search in one workgroup up to 64 x 256 impressions
+
+// Search state, device resident across levels (R/global_problem.cpp:46-53).
+struct BinState {
+    double lower, upper;
+    double cr[kBinMaxRatios];
+    double S[kBinMaxRatios];          // usage at the last level's ratios (diagnostic)
+    double fin_lo, fin_up;            // final interval, (cr, cr) on an exact hit
+    double slope_lo, slope_hi;        // FindMinMaxSlope, iteration 1 only
+    double rem;                       // budget left for the tie regions
+    int32_t nr, levels, done, mode;   // mode 1 = exact ratio, 2 = range
+    uint32_t ticket, pad;
+};
+
+__device__ inline int bin_levels(const BinState* st) { return st->levels; }
+
+// Critical ratios of a level: ratio = lower - d, cr_k = (ratio += d)  R/global_problem.cpp:55-62
+__device__ inline void bin_set_ratios(BinState* st) {
+    const int nr = st->nr;
+    const double d = (st->upper - st->lower) / (double)nr;
+    double r = st->lower - d;
+    for (int k = 0; k < nr; ++k) {
+        r = r + d;
+        st->cr[k] = r;
+    }
+}
+
+// The reference's bracket / expand / exact rule after one level
+// (R/global_problem.cpp:66-111) and the spec's fp64 stop.  One thread.
+__device__ inline void bin_control(BinState* st, const double* S, double B) {
+    const int nr = st->nr;
+    double lower = st->lower, upper = st->upper;
+    st->levels += 1;
+    for (int k = 0; k < nr; ++k) st->S[k] = S[k];
+    bool expanded = false;
+    int exact = -1;
+    for (int k = 0; k < nr; ++k) {
+        const double delta = S[k] - B;
+        if (k == 0 && delta < 0.0) { lower = lower * 0.9; expanded = true; break; }
+        if (k == nr - 1 && delta > 0.0) { upper = upper / 0.9; expanded = true; break; }
+        if (delta > 0.0) lower = st->cr[k];
+        else if (delta < 0.0) { upper = st->cr[k]; break; }
+        else { exact = k; break; }
+    }
+    if (exact >= 0) {
+        st->mode = 1;
+        st->fin_lo = st->fin_up = st->cr[exact];
+        st->done = 1;
+        return;
+    }
+    st->lower = lower;
+    st->upper = upper;
+    const double a = __builtin_fabs(upper) * 0x1p-42;
+    const double tol = (1e-16 < a) ? a : 1e-16;   // std::max(1e-16, |upper| 2^-42)
+    if ((!expanded && upper - lower < tol) || st->levels >= kBinMaxLevels) {
+        st->mode = 2;
+        st->fin_lo = lower;
+        st->fin_up = upper;
+        st->done = 1;
+        return;
+    }
+    bin_set_ratios(st);
+}
+
+// usage_i(cr_k) = sum over the impression's regions (in order) of width if u >= cr_k.
+__device__ inline void bin_usage(int i, int I, const int32_t* __restrict__ roff,
+                                 const int32_t* __restrict__ rcnt, const double* __restrict__ keys,
+                                 const double* __restrict__ rwidth, const double* cr, int nr,
+                                 double* acc) {
+#pragma unroll
+    for (int k = 0; k < kBinMaxRatios; ++k) acc[k] = 0.0;
+    if (i >= I) return;
+    const int r0 = roff[i], n = rcnt[i];
+    for (int j = 0; j < n; ++j) {
+        const double u = keys[r0 + j], w = rwidth[r0 + j];
+#pragma unroll
+        for (int k = 0; k < kBinMaxRatios; ++k)
+            if (k < nr && u >= cr[k]) acc[k] = acc[k] + w;
+    }
+}
+
+// Spec block tree over 256 lanes (lds[k][256] filled, synchronised): s_l += s_{l+w},
+// w = 128 .. 1; the block sum of row k lands in lane 0 of wave 0 (returned there).
+template <int NK>
+__device__ inline void bin_block_tree(double (*lds)[kBinBlock], int nk, int tid, double* out) {
+    if (tid < 128)
+        for (int k = 0; k < nk; ++k) lds[k][tid] = lds[k][tid] + lds[k][tid + 128];
+    __syncthreads();
+    if (tid < 64) {
+        for (int k = 0; k < nk; ++k) {
+            double x = lds[k][tid] + lds[k][tid + 64];
+#pragma unroll
+            for (int w = 32; w >= 1; w >>= 1) x = x + __shfl_down(x, w);
+            if (tid == 0) out[k] = x;
+        }
+    }
+}
+
+// sum_fixed by one wave over n values at stride 1 (spec: 64 strided chains, halving tree).
+__device__ inline double wave_sum_fixed(const double* x, int n, int lane) {
+    double a = 0.0;
+    for (int q = lane; q < n; q += 64) a = a + x[q];
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) a = a + __shfl_down(a, w);
+    return a;
+}
+
+// FindMinMaxSlope (R/global_problem.cpp:116-135) over regions in id order =
+// (impression asc, region asc), in chunks of 256: a region is a running-maximum
+// record iff it exceeds the maximum before it (initial 0); the minimum runs
+// over the non-records only (the reference's else-if).
+__global__ void rec_chunk_max_kernel(const double* __restrict__ keys, int64_t R, double* __restrict__ cmax) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k0 = c * kBinBlock;
+    if (k0 >= R) return;
+    const int64_t k1 = (k0 + kBinBlock < R) ? k0 + kBinBlock : R;
+    double mx = -DBL_MAX;
+    for (int64_t k = k0; k < k1; ++k) mx = __builtin_fmax(mx, keys[k]);
+    cmax[c] = mx;
+}
+
+__global__ void rec_prefix_kernel(const double* __restrict__ cmax, int64_t nch, double* __restrict__ pmax) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double run = 0.0;   // max_weight = 0.0
+    for (int64_t c = 0; c < nch; ++c) {
+        pmax[c] = run;
+        run = __builtin_fmax(run, cmax[c]);
+    }
+}
+
+__global__ void rec_chunk_min_kernel(const double* __restrict__ keys, int64_t R,
+                                     const double* __restrict__ pmax, double* __restrict__ cmin,
+                                     double* __restrict__ cmax) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k0 = c * kBinBlock;
+    if (k0 >= R) return;
+    const int64_t k1 = (k0 + kBinBlock < R) ? k0 + kBinBlock : R;
+    double run = pmax[c], mn = DBL_MAX;
+    for (int64_t k = k0; k < k1; ++k) {
+        const double u = keys[k];
+        if (u > run) run = u;
+        else if (u < mn) mn = u;
+    }
+    cmin[c] = mn;
+    cmax[c] = run;   // running maximum at the chunk's end
+}
+
+__global__ __launch_bounds__(64) void rec_final_kernel(const double* __restrict__ cmin,
+                                                       const double* __restrict__ cmax, int64_t nch,
+                                                       BinState* st) {
+    double mn = DBL_MAX, mx = 0.0;
+    for (int64_t c = threadIdx.x; c < nch; c += 64) {
+        mn = __builtin_fmin(mn, cmin[c]);
+        mx = __builtin_fmax(mx, cmax[c]);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        mn = __builtin_fmin(mn, __shfl_xor(mn, m));
+        mx = __builtin_fmax(mx, __shfl_xor(mx, m));
+    }
+    if (threadIdx.x == 0) {
+        st->slope_lo = 1.0 / mx;   // min_slope_ = 1 / max_weight
+        st->slope_hi = 1.0 / mn;   // max_slope_ = 1 / min_weight
+    }
+}
+
+// Start of a search: [slope_lo, slope_hi] at iteration 1, [slope_lo*scale,
+// slope_hi/scale] after (R/global_problem.cpp:283-292).
+__global__ void bin_begin_kernel(BinState* st, int first, double scale, int nr) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    st->lower = first ? st->slope_lo : st->slope_lo * scale;
+    st->upper = first ? st->slope_hi : st->slope_hi / scale;
+    st->nr = nr;
+    st->levels = 0;
+    st->done = 0;
+    st->mode = 0;
+    st->ticket = 0;
+    st->rem = 0.0;
+    bin_set_ratios(st);
+}
+
+// One search level over all impressions; the last block to finish reduces
+// the block sums and applies the control rule.  A launch after the search
+// stopped returns at once.
+__global__ __launch_bounds__(kBinBlock) void bin_level_kernel(BinState* st, const int32_t* __restrict__ roff,
+                                                              const int32_t* __restrict__ rcnt,
+                                                              const double* __restrict__ keys,
+                                                              const double* __restrict__ rwidth, int I,
+                                                              double* bsum, const double* __restrict__ Bptr) {
+    if (st->done) return;
+    __shared__ double lds[kBinMaxRatios][kBinBlock];
+    __shared__ double tot[kBinMaxRatios];
+    __shared__ int last;
+    const int nr = st->nr, tid = threadIdx.x, nb = gridDim.x, b = blockIdx.x;
+    double cr[kBinMaxRatios], acc[kBinMaxRatios];
+#pragma unroll
+    for (int k = 0; k < kBinMaxRatios; ++k) cr[k] = (k < nr) ? st->cr[k] : 0.0;
+    bin_usage(b * kBinBlock + tid, I, roff, rcnt, keys, rwidth, cr, nr, acc);
+#pragma unroll
+    for (int k = 0; k < kBinMaxRatios; ++k)
+        if (k < nr) lds[k][tid] = acc[k];
+    __syncthreads();
+    bin_block_tree<kBinMaxRatios>(lds, nr, tid, tot);
+    if (tid == 0) {
+        for (int k = 0; k < nr; ++k) bsum[(int64_t)k * nb + b] = tot[k];
+        __threadfence();
+        last = (atomicAdd(&st->ticket, 1u) == (unsigned)(nb - 1));
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const int wv = tid >> 6, lane = tid & 63;
+    for (int k = wv; k < nr; k += kBinBlock / 64) {
+        const double a = wave_sum_fixed(bsum + (int64_t)k * nb, nb, lane);
+        if (lane == 0) tot[k] = a;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        bin_control(st, tot, *Bptr);
+        st->ticket = 0;
+    }
+}
+
+// The whole search in one workgroup of 1024 lanes (nb <= kBinSingleBlocks):
+// four 256-lane groups take the blocks of the spec in turn; the control state
+// lives in LDS.
+__global__ __launch_bounds__(1024) void bin_search_single_kernel(BinState* st, const int32_t* __restrict__ roff,
+                                                                 const int32_t* __restrict__ rcnt,
+                                                                 const double* __restrict__ keys,
+                                                                 const double* __restrict__ rwidth, int I,
+                                                                 const double* __restrict__ Bptr) {
+    __shared__ double lds[4][kBinMaxRatios][kBinBlock];
+    __shared__ double bs[kBinMaxRatios][kBinSingleBlocks];
+    __shared__ double tot[kBinMaxRatios];
+    __shared__ BinState ss;
+    const int tid = threadIdx.x, g = tid >> 8, gl = tid & 255;
+    const int nb = (I + kBinBlock - 1) / kBinBlock;
+    if (tid == 0) ss = *st;
+    __syncthreads();
+    const int nr = ss.nr;
+    const double B = *Bptr;
+    while (!ss.done) {
+        double cr[kBinMaxRatios], acc[kBinMaxRatios];
+#pragma unroll
+        for (int k = 0; k < kBinMaxRatios; ++k) cr[k] = (k < nr) ? ss.cr[k] : 0.0;
+        for (int b0 = 0; b0 < nb; b0 += 4) {
+            const int b = b0 + g;
+            bin_usage(b < nb ? b * kBinBlock + gl : I, I, roff, rcnt, keys, rwidth, cr, nr, acc);
+#pragma unroll
+            for (int k = 0; k < kBinMaxRatios; ++k)
+                if (k < nr) lds[g][k][gl] = acc[k];
+            __syncthreads();
+            if (gl < 128)
+                for (int k = 0; k < nr; ++k) lds[g][k][gl] = lds[g][k][gl] + lds[g][k][gl + 128];
+            __syncthreads();
+            if (gl < 64 && b < nb) {
+                for (int k = 0; k < nr; ++k) {
+                    double x = lds[g][k][gl] + lds[g][k][gl + 64];
+#pragma unroll
+                    for (int w = 32; w >= 1; w >>= 1) x = x + __shfl_down(x, w);
+                    if (gl == 0) bs[k][b] = x;
+                }
+            }
+            __syncthreads();
+        }
+        const int wv = tid >> 6, lane = tid & 63;
+        if (wv < nr) {
+            const double a = wave_sum_fixed(bs[wv], nb, lane);
+            if (lane == 0) tot[wv] = a;
+        }
+        __syncthreads();
+        if (tid == 0) bin_control(&ss, tot, B);
+        __syncthreads();
+    }
+    if (tid == 0) *st = ss;
+}
+
+// Final allocation, full part (R/global_problem.cpp:166-178 exact hit,
+// 180-195 range): state 1 + inc = width for regions u >= cr (exact) or
+// u > upper (range); tie candidates lower < u <= upper flagged; rem = B -
+// sum_blocked(full part per impression) by the last block.
+__global__ __launch_bounds__(kBinBlock) void bin_assign_kernel(BinState* st, const int32_t* __restrict__ roff,
+                                                               const int32_t* __restrict__ rcnt,
+                                                               const double* __restrict__ keys,
+                                                               const double* __restrict__ rwidth, int I,
+                                                               int32_t* __restrict__ rstate,
+                                                               double* __restrict__ inc,
+                                                               uint8_t* __restrict__ flags, double* bsum,
+                                                               const double* __restrict__ Bptr) {
+    __shared__ double lds[1][kBinBlock];
+    __shared__ double tot[1];
+    __shared__ int last;
+    const int tid = threadIdx.x, nb = gridDim.x, b = blockIdx.x;
+    const int i = b * kBinBlock + tid;
+    const int mode = st->mode;
+    const double lo = st->fin_lo, up = st->fin_up;
+    double beta = 0.0;
+    if (i < I) {
+        const int r0 = roff[i], n = rcnt[i];
+        for (int j = 0; j < n; ++j) {
+            const double u = keys[r0 + j], w = rwidth[r0 + j];
+            const bool full = (mode == 1) ? (u >= lo) : (u > up);
+            const bool tie = (mode == 2) && (u > lo) && (u <= up);
+            rstate[r0 + j] = full ? 1 : 0;
+            inc[r0 + j] = full ? w : 0.0;
+            flags[r0 + j] = tie ? 1 : 0;
+            if (full) beta = beta + w;
+        }
+    }
+    lds[0][tid] = beta;
+    __syncthreads();
+    bin_block_tree<1>(lds, 1, tid, tot);
+    if (tid == 0) {
+        bsum[b] = tot[0];
+        __threadfence();
+        last = (atomicAdd(&st->ticket, 1u) == (unsigned)(nb - 1));
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (tid < 64) {
+        const double a = wave_sum_fixed(bsum, nb, tid);
+        if (tid == 0) {
+            st->rem = *Bptr - a;
+            st->ticket = 0;
+        }
+    }
+}
+
+// Tie regions in (impression, region) order (R/global_problem.cpp:197-221):
+// inc = min(rem, width), assigned whatever its sign, rem -= inc, stop at
+// rem == 0.  One wave; 64 widths per load, walked with the budget uniform.
+__global__ __launch_bounds__(64) void bin_tie_chain_kernel(BinState* st, const int32_t* __restrict__ tie_ids,
+                                                           const int32_t* __restrict__ num_ties,
+                                                           const double* __restrict__ rwidth,
+                                                           int32_t* __restrict__ rstate,
+                                                           double* __restrict__ inc) {
+    const int lane = threadIdx.x;
+    const int n = *num_ties;
+    double rem = st->rem;
+    bool stop = false;
+    for (int base = 0; base < n && !stop; base += 64) {
+        const int q = base + lane;
+        const int id = (q < n) ? tie_ids[q] : 0;
+        const double w = (q < n) ? rwidth[id] : 0.0;
+        const int cnt = (n - base < 64) ? n - base : 64;
+        for (int k = 0; k < cnt; ++k) {
+            const double wk = __shfl(w, k);
+            const double a = (wk < rem) ? wk : rem;   // std::min(rem, width)
+            if (lane == k) {
+                inc[id] = a;
+                rstate[id] = 2;
+            }
+            rem = rem - a;
+            if (rem == 0.0) {
+                stop = true;
+                break;
+            }
+        }
+    }
+    if (lane == 0) st->rem = rem;
 }
 
 }  // namespace mw
@@ -434,6 +828,13 @@ struct dlp_mw {
     int32_t *rtotal = nullptr;
     dlp_mw_iter* dlog = nullptr;
     int log_cap = 0;
+    // binary mode
+    int binary = 0, nr = 3;
+    double scale = 0.0;
+    double *rwidth = nullptr, *bsum = nullptr, *cmax = nullptr, *pmax = nullptr, *cmin = nullptr;
+    uint8_t* flags = nullptr;
+    int32_t *tie_ids = nullptr, *num_ties = nullptr;
+    dlp::mw::BinState* bst = nullptr;
     void* cub_tmp = nullptr;
     size_t cub_bytes = 0;
     std::vector<int64_t> var_to_imp;   // problem variable k -> impression-major index
@@ -468,7 +869,9 @@ void mw_free(dlp_mw* m) {
                     m->slack, m->avg_slack, m->x, m->xa, m->env_u, m->env_v, m->cut, m->hull_h,
                     m->rcnt, m->roff, m->keys, m->keys_sorted, m->width_sorted, m->ids,
                     m->ids_sorted, m->reg_imp, m->reg_j, m->pos_by_id, m->inc_by_id, m->chunk,
-                    m->offs, m->dcontrib, m->B, m->dual, m->rtotal, m->dlog, m->cub_tmp};
+                    m->offs, m->dcontrib, m->B, m->dual, m->rtotal, m->dlog, m->cub_tmp,
+                    m->rwidth, m->bsum, m->cmax, m->pmax, m->cmin, m->flags, m->tie_ids,
+                    m->num_ties, m->bst};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -539,6 +942,21 @@ int mw_init(const dlp_problem* prob, const dlp_mw_options* o, dlp_mw* m) {
     MW_ALLOC(m->reg_j, nnz); MW_ALLOC(m->pos_by_id, nnz); MW_ALLOC(m->inc_by_id, nnz);
     MW_ALLOC(m->chunk, nnz / dlp::mw::kChunk + 2); MW_ALLOC(m->offs, nnz / dlp::mw::kChunk + 2);
     MW_ALLOC(m->dcontrib, I); MW_ALLOC(m->B, 1); MW_ALLOC(m->dual, 1); MW_ALLOC(m->rtotal, 1);
+    m->binary = o->binary ? 1 : 0;
+    if (m->binary) {
+        using dlp::mw::kBinBlock;
+        using dlp::mw::kBinMaxRatios;
+        m->nr = o->intervals;
+        // R/main.cpp:38: cr_transition_scale = 1 - epsilon * 0.001 (x87 long double), unless given
+        m->scale = (o->scale > 0.0) ? o->scale
+                                    : (double)(1.0L - (long double)o->epsilon * (long double)0.001);
+        const int64_t nb = (I + kBinBlock - 1) / kBinBlock, nch = nnz / kBinBlock + 2;
+        MW_ALLOC(m->rwidth, nnz); MW_ALLOC(m->bsum, kBinMaxRatios * nb); MW_ALLOC(m->flags, nnz);
+        MW_ALLOC(m->tie_ids, nnz); MW_ALLOC(m->num_ties, 1);
+        MW_ALLOC(m->cmax, nch); MW_ALLOC(m->pmax, nch); MW_ALLOC(m->cmin, nch);
+        MW_ALLOC(m->bst, 1);
+        MW_TRY(hipMemset(m->bst, 0, sizeof(dlp::mw::BinState)));
+    }
 #undef MW_ALLOC
     std::vector<double> ones(A, 1.0), zeros_a(A, 0.0), zeros_n(nnz, 0.0);
     MW_TRY(hipMemcpy(m->iptr, iptr.data(), sizeof(int64_t) * (I + 1), hipMemcpyHostToDevice));
@@ -559,8 +977,63 @@ int mw_init(const dlp_problem* prob, const dlp_mw_options* o, dlp_mw* m) {
                                                        m->ids_sorted, (int)std::max<int64_t>(nnz, 1),
                                                        0, 64, m->stream));
     MW_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, m->rcnt, m->roff, std::max(I, 1), m->stream));
-    m->cub_bytes = std::max(b1, b2);
+    size_t b3 = 0;
+    if (m->binary)
+        MW_TRY(hipcub::DeviceSelect::Flagged(nullptr, b3, hipcub::CountingInputIterator<int32_t>(0), m->flags,
+                                             m->tie_ids, m->num_ties, (int)std::max<int64_t>(nnz, 1),
+                                             m->stream));
+    m->cub_bytes = std::max(std::max(b1, b2), b3);
     MW_TRY(hipMalloc(&m->cub_tmp, std::max<size_t>(m->cub_bytes, 16)));
+    return DLP_OK;
+}
+
+// Binary-mode budget split (R/global_problem.cpp:46-222, 283-292): the search,
+// then the full / tie allocation into inc_by_id + region states (pos_by_id).
+int bin_allocate(dlp_mw* m, int64_t R, int t) {
+    using namespace dlp::mw;
+    hipStream_t s = m->stream;
+    const int I = m->I;
+    const int nb = (I + kBinBlock - 1) / kBinBlock;
+    if (t == 1) {   // FindMinMaxSlope
+        const int64_t nch = (R + kBinBlock - 1) / kBinBlock;
+        const unsigned g = (unsigned)((nch + 255) / 256);
+        if (nch > 0) {
+            rec_chunk_max_kernel<<<g, 256, 0, s>>>(m->keys, R, m->cmax);
+            rec_prefix_kernel<<<1, 64, 0, s>>>(m->cmax, nch, m->pmax);
+            rec_chunk_min_kernel<<<g, 256, 0, s>>>(m->keys, R, m->pmax, m->cmin, m->cmax);
+        }
+        rec_final_kernel<<<1, 64, 0, s>>>(m->cmin, m->cmax, nch, m->bst);
+    }
+    bin_begin_kernel<<<1, 64, 0, s>>>(m->bst, t == 1 ? 1 : 0, m->scale, m->nr);
+    if (nb <= kBinSingleBlocks) {
+        bin_search_single_kernel<<<1, 1024, 0, s>>>(m->bst, m->roff, m->rcnt, m->keys, m->rwidth, I, m->B);
+    } else {
+        int32_t done = 0;
+        for (int issued = 0; !done;) {
+            const int batch = issued == 0 ? 48 : 32;
+            for (int k = 0; k < batch; ++k)
+                bin_level_kernel<<<nb, kBinBlock, 0, s>>>(m->bst, m->roff, m->rcnt, m->keys, m->rwidth, I,
+                                                          m->bsum, m->B);
+            issued += batch;
+            MW_TRY(hipGetLastError());
+            MW_TRY(hipMemcpyAsync(&done, &m->bst->done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            MW_TRY(hipStreamSynchronize(s));
+            if (!done && issued > kBinMaxLevels + 64) {
+                set_error("dlp_mw: binary search did not stop within the level cap");
+                return DLP_ERR_STATE;
+            }
+        }
+    }
+    bin_assign_kernel<<<nb, kBinBlock, 0, s>>>(m->bst, m->roff, m->rcnt, m->keys, m->rwidth, I, m->pos_by_id,
+                                               m->inc_by_id, m->flags, m->bsum, m->B);
+    if (R > 0) {
+        size_t bytes = m->cub_bytes;
+        MW_TRY(hipcub::DeviceSelect::Flagged(m->cub_tmp, bytes, hipcub::CountingInputIterator<int32_t>(0),
+                                             m->flags, m->tie_ids, m->num_ties, (int)R, s));
+        bin_tie_chain_kernel<<<1, 64, 0, s>>>(m->bst, m->tie_ids, m->num_ties, m->rwidth, m->pos_by_id,
+                                              m->inc_by_id);
+    }
+    MW_TRY(hipGetLastError());
     return DLP_OK;
 }
 
@@ -579,15 +1052,19 @@ int mw_iteration(dlp_mw* m, dlp_mw_iter* dlog_entry) {
     region_count_kernel<<<(I + tb - 1) / tb, tb, 0, s>>>(m->hull_h, I, m->rcnt);
     size_t bytes = m->cub_bytes;
     MW_TRY(hipcub::DeviceScan::ExclusiveSum(m->cub_tmp, bytes, m->rcnt, m->roff, I, s));
-    emit_regions_kernel<<<(I + tb - 1) / tb, tb, 0, s>>>(m->iptr, m->hull_h, m->roff, m->env_u, I,
-                                                         m->keys, m->ids, m->reg_imp, m->reg_j);
+    emit_regions_kernel<<<(I + tb - 1) / tb, tb, 0, s>>>(m->iptr, m->hull_h, m->roff, m->env_u, m->cut,
+                                                         I, m->keys, m->ids, m->reg_imp, m->reg_j,
+                                                         m->rwidth);
     // region count R = roff[I-1] + rcnt[I-1]: read back (the sort needs it on the host)
     int32_t last[2] = {0, 0};
     MW_TRY(hipMemcpyAsync(&last[0], m->roff + (I - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s));
     MW_TRY(hipMemcpyAsync(&last[1], m->rcnt + (I - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s));
     MW_TRY(hipStreamSynchronize(s));
     const int64_t R = (int64_t)last[0] + last[1];
-    if (R > 0) {
+    if (m->binary) {
+        int rc = bin_allocate(m, R, t);
+        if (rc != DLP_OK) return rc;
+    } else if (R > 0) {
         bytes = m->cub_bytes;
         MW_TRY(hipcub::DeviceRadixSort::SortPairsDescending(m->cub_tmp, bytes, m->keys, m->keys_sorted,
                                                            m->ids, m->ids_sorted, (int)R, 0, 64, s));
@@ -600,13 +1077,13 @@ int mw_iteration(dlp_mw* m, dlp_mw_iter* dlog_entry) {
     }
     primal_kernel<<<(I + tb - 1) / tb, tb, 0, s>>>(m->iptr, m->iadv, m->ibid, m->w, m->hull_h, m->roff,
                                                    m->env_u, m->env_v, m->inc_by_id, m->pos_by_id, I,
-                                                   m->tight_tol, m->x, m->dcontrib);
+                                                   m->tight_tol, m->binary, m->x, m->dcontrib);
     sum_fixed_kernel<<<1, 64, 0, s>>>(m->dcontrib, I, m->dual);
     average_kernel<<<(unsigned)((nnz + tb - 1) / tb), tb, 0, s>>>(m->x, m->xa, nnz, fa, fb);
     advertiser_kernel<<<(A + tb - 1) / tb, tb, 0, s>>>(m->aptr, m->apos, m->abid, m->budgets, m->x, A,
                                                        fa, fb, m->width, m->lp, m->lm, m->slack,
                                                        m->avg_slack, m->w);
-    report_kernel<<<1, 64, 0, s>>>(m->avg_slack, m->budgets, m->w, A, m->dual, m->B, dlog_entry);
+    report_kernel<<<1, 64, 0, s>>>(m->avg_slack, m->budgets, m->w, A, m->dual, m->B, m->bst, dlog_entry);
     MW_TRY(hipGetLastError());
     m->t = t;
     return DLP_OK;
@@ -623,6 +1100,8 @@ void dlp_mw_options_default(dlp_mw_options* o) {
     o->binary = 0;
     o->epsilon = 0.01;
     o->tolerance = 1e-18;
+    o->scale = 0.0;       // derived: 1 - epsilon * 0.001 (R/main.cpp:38)
+    o->intervals = 3;     // R/main.cpp:37
 }
 
 int dlp_mw_create(const dlp_problem* prob, const dlp_mw_options* opt, dlp_mw** out) {
@@ -632,9 +1111,9 @@ int dlp_mw_create(const dlp_problem* prob, const dlp_mw_options* opt, dlp_mw** o
         set_error("dlp_mw_create: needs an ad-allocation problem (dlp_problem_create_adalloc)");
         return DLP_ERR_ARG;
     }
-    if (o.binary) {
-        set_error("dlp_mw: binary-search mode stops at 1e-16, below fp64 resolution; use sort mode");
-        return DLP_ERR_UNSUPPORTED;
+    if (o.binary && (o.intervals < 1 || o.intervals > dlp::mw::kBinMaxRatios)) {
+        set_error("dlp_mw: binary mode needs 1 <= intervals <= 8");
+        return DLP_ERR_ARG;
     }
     if (!(o.epsilon > 0.0 && o.epsilon < 1.0)) {
         set_error("dlp_mw: epsilon must be in (0, 1)");

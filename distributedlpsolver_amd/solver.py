@@ -390,20 +390,27 @@ def batched_solve(nlp: int, m: int, n: int, seed: int, degenerate: bool = False,
 
 
 MW_ITER_DTYPE = np.dtype([("dual_value", "<f8"), ("max_infeasibility", "<f8"),
-                          ("infeasible_advertiser", "<i4"), ("pad", "<i4"), ("min_weight", "<f8"),
+                          ("infeasible_advertiser", "<i4"), ("search_levels", "<i4"), ("min_weight", "<f8"),
                           ("max_weight", "<f8"), ("weighted_budget", "<f8")])
 
 
 class MW:
-    """The reference's multiplicative-weights loop (sort mode) on the GPU
-    (dlp_mw_*): replaces Instance::RunMultiplicativeWeights(T, tol, false),
-    R/instance.cpp:117-124.  Needs a Problem.adalloc problem."""
+    """The reference's multiplicative-weights loop on the GPU (dlp_mw_*):
+    replaces Instance::RunMultiplicativeWeights(T, tol, binary[, scale,
+    intervals]), R/instance.cpp:117-141.  binary=False is sort mode
+    (R/global_problem.cpp:224-255), binary=True the threshold search
+    (R/global_problem.cpp:46-222) that R/main.cpp:36 runs; scale=None derives
+    cr_transition_scale = 1 - epsilon * 0.001 (R/main.cpp:38).  Needs a
+    Problem.adalloc problem."""
 
     def __init__(self, problem: Problem, epsilon: float = 0.01, tolerance: float = 1e-18,
-                 device: int = 0):
+                 device: int = 0, binary: bool = False, scale: float | None = None,
+                 intervals: int = 3):
         o = L.MWOptions()
         L.lib().dlp_mw_options_default(C.byref(o))
         o.epsilon, o.tolerance, o.device = epsilon, tolerance, device
+        o.binary, o.intervals = (1 if binary else 0), intervals
+        o.scale = 0.0 if scale is None else scale
         self.problem = problem
         h = C.c_void_p()
         L.check(L.lib().dlp_mw_create(problem._h, C.byref(o), C.byref(h)), "dlp_mw_create")

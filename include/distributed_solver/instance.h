@@ -53,10 +53,12 @@ class Instance {
     void WriteInstanceToCSV(std::string file_name_handle);
     void GenerateAndWriteInstance(std::string file_name_handle);
 
-    // R/instance.h:52-53.  The reference's MW loop on the GPU (dlp_mw_*, sort
-    // mode, fp64 spec of DESIGN.md §9); prints the reference's per-iteration
-    // "Dual Value" / infeasibility / weight lines.  binary = true falls back to
-    // the sort-mode split (the bisection's 1e-16 stop is below fp64 resolution).
+    // R/instance.h:52-53.  The reference's MW loop on the GPU (dlp_mw_*, fp64
+    // spec of DESIGN.md §9): binary = false sort mode, binary = true the
+    // threshold search with cr_transition_scale `scale` and `intervals`
+    // critical ratios per level (3-argument form: 1 - epsilon * 0.001 and 3,
+    // R/main.cpp:37-38); prints the reference's per-iteration "Dual Value" /
+    // infeasibility / weight lines.
     void RunMultiplicativeWeights(long double num_iterations,
                                   long double numerical_accuracy_tolerance, bool binary);
     void RunMultiplicativeWeights(long double num_iterations,

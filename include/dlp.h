@@ -340,27 +340,32 @@ int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, uint64_t seed
 
 /* ---- multiplicative-weights path ------------------
  * The reference's own epsilon-approximate MW loop (R/allocation_mw.cpp:271-326,
- * sort mode) on the GPU for an ad-allocation problem (dlp_problem_create_adalloc),
+ * sort or binary-search mode) on the GPU for an ad-allocation problem (dlp_problem_create_adalloc),
  * with the fp64 spec of DESIGN.md §9 (fixed tie orders, fixed-order sums,
  * deterministic exp): per impression an upper envelope (wave-level bitonic
  * sort + monotone chain), a global slope sort (hipCUB radix sort), a blocked
  * budget prefix, primal construction, per-advertiser slacks and weights.
  * Scales to the reference's 100k x 1M x 1e-4 scenario, where a dense tableau
- * cannot exist.  Replaces Instance::RunMultiplicativeWeights(T, tol, false)
- * (R/instance.h:52, R/instance.cpp:117-124). */
+ * cannot exist.  Replaces Instance::RunMultiplicativeWeights(T, tol, binary[, scale,
+ * intervals]) (R/instance.h:52-55, R/instance.cpp:117-141). */
 typedef struct dlp_mw dlp_mw;
 typedef struct dlp_mw_options {
     int32_t device;
-    int32_t binary;        /* must be 0: binary mode's 1e-16 stop is below fp64 */
+    int32_t binary;        /* 0 sort mode (R/global_problem.cpp:224-255); 1 threshold search
+                              (R/global_problem.cpp:46-222, the mode R/main.cpp:36 runs) with the
+                              fp64 stop of DESIGN.md §9 (1e-16 is below fp64 resolution) */
     double  epsilon;       /* default 0.01 (R/main.cpp:33) */
     double  tolerance;     /* numerical_accuracy_tolerance, default 1e-18; tight-set test uses max(tol, 1e-12) */
+    double  scale;         /* binary: cr_transition_scale; <= 0 -> 1 - epsilon * 0.001 (R/main.cpp:38) */
+    int32_t intervals;     /* binary: critical ratios per level, 1..8, default 3 (R/main.cpp:37) */
+    int32_t pad_;
 } dlp_mw_options;
 typedef struct dlp_mw_iter {   /* per-iteration report (the reference's stdout, R/global_problem.cpp:320,
                                   R/allocation_mw.cpp:214-220,264-268) */
     double  dual_value;
     double  max_infeasibility;
     int32_t infeasible_advertiser;
-    int32_t pad;
+    int32_t search_levels;     /* binary mode: threshold-search levels this iteration; 0 in sort mode */
     double  min_weight, max_weight, weighted_budget;
 } dlp_mw_iter;
 void dlp_mw_options_default(dlp_mw_options* opt);

@@ -109,6 +109,18 @@ int oracle_run_generated(int kind, int64_t m, int64_t n, uint64_t seed, int64_t 
 int oracle_mw_run(int A, int I, double sparsity, double scaling, double epsilon, int T, double tol,
                   double* dual, double* infeas, int32_t* infeas_idx, double* wmin, double* wmax,
                   double* budget_w, double* x_avg_out, double* weights_out, int64_t* nnz_out);
+/* The same, either mode: binary = 1 selects the threshold search of
+ * R/global_problem.cpp:46-222 (spec in oracle_mw.cpp's header) with
+ * cr_transition_scale `scale` and `intervals` critical ratios per level (1..8).
+ * levels_out (T entries) gets the number of search levels per iteration,
+ * interval_out (2T) the final (lower, upper) (cr, cr for an exact hit); both
+ * may be NULL and are untouched in sort mode. */
+int oracle_mw_run_mode(int A, int I, double sparsity, double scaling, double epsilon, int T,
+                       double tol, int binary, double scale, int intervals, double* dual,
+                       double* infeas, int32_t* infeas_idx, double* wmin, double* wmax,
+                       double* budget_w, double* x_avg_out, double* weights_out, int64_t* nnz_out,
+                       int32_t* levels_out, double* interval_out);
+double oracle_sum_blocked(const double* x, int64_t n);
 double oracle_dexp(double x);
 double oracle_sum_fixed(const double* x, int64_t n);
 

@@ -1,6 +1,7 @@
 // oracle_mw.cpp — TEST INFRASTRUCTURE ONLY.  fp64 restatement of the
-// reference's multiplicative-weights (MW) iteration in SORT mode
-// (SURVEY.md §8f row f3), the CPU checker of the GPU MW path.
+// reference's multiplicative-weights (MW) iteration in SORT and BINARY
+// (threshold-search) mode, the CPU checker of the GPU
+// MW path.
 //
 // The reference computes in x87 long double and leaves several choices to
 // std::sort / hash_map order; this restatement fixes every such choice (the
@@ -26,10 +27,42 @@
 //     dexp = round-to-nearest range reduction by ln2 (hi/lo), degree-13 Taylor
 //     Horner with fma, ldexp                                 R/allocation_mw.cpp:173-190
 //   * averages x_avg = ((t-1)/t) x_avg + (1/t) x             R/instance.cpp:143-152
+//
+// BINARY mode (R/global_problem.cpp:46-222, 283-292; the mode R/main.cpp:36 runs):
+//   * iteration 1: FindMinMaxSlope over regions (impression asc, region asc)
+//     with the reference's else-if (a new running maximum is never a minimum
+//     candidate), slope_lo = 1/max, slope_hi = 1/min; the interval is
+//     [slope_lo, slope_hi] at iteration 1 and [slope_lo*scale, slope_hi/scale]
+//     after (slope_lo/hi are never recomputed)      R/global_problem.cpp:116-135, 283-292
+//   * one level: d = (upper-lower)/nr, ratio = lower-d, cr_k = (ratio += d);
+//     usage_i(r) = sum over regions j (in order) of width_j if u_j >= r;
+//     S(r) = sum_blocked(usage) (blocks of 256 impressions, zero padded,
+//     halving tree s_l += s_{l+w}, w = 128..1, then sum_fixed of the block
+//     sums); delta_k = S(cr_k) - B                       R/global_problem.cpp:137-162
+//   * per k: k == 0 and delta < 0 -> lower *= 0.9, next level; k == nr-1 and
+//     delta > 0 -> upper /= 0.9, next level; else delta > 0 -> lower = cr_k,
+//     delta < 0 -> upper = cr_k and stop the scan, delta == 0 -> allocate at
+//     cr_k (all regions u >= cr_k)                        R/global_problem.cpp:66-98
+//   * after a level without expansion: stop when upper - lower <
+//     max(1e-16, |upper| 2^-42).  The reference's 1e-16 is an x87 long double
+//     window of ~925 representable values near 1 (and below fp64 resolution);
+//     2^-42 |upper| keeps the same granularity in fp64 (1024..2048 ulp).  A
+//     finer fp64 window makes a critical ratio land exactly on a region slope
+//     U often (then lower = U and no region is in (lower, upper]: dual 0,
+//     which the reference shows only at iteration 1).  At most 2048 levels
+//     (the reference recurses without bound when the regions never hold B).
+//   * range allocation (lower, upper): regions with u > upper in full
+//     (impression asc, region asc), rem = B - sum_blocked(full per
+//     impression); then the regions with lower < u <= upper in (impression,
+//     region) order: inc = min(rem, width), assigned (beta += inc, j* = j)
+//     whatever its sign, rem -= inc, stop when rem == 0   R/global_problem.cpp:180-222
+//   * a region assigned with width 0 still sets j* (the reference's make_pair)
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -68,6 +101,23 @@ double dexp(double x) {
     return std::ldexp(p, (int)k);
 }
 
+// Fixed-order blocked sum of the binary-mode spec: blocks of 256 (zero
+// padded), halving tree inside a block, sum_fixed over the block sums.
+double sum_blocked(const double* x, int64_t n) {
+    const int64_t nb = (n + 255) / 256;
+    std::vector<double> bs(nb);
+    for (int64_t b = 0; b < nb; ++b) {
+        double s[256];
+        for (int l = 0; l < 256; ++l) s[l] = (b * 256 + l < n) ? x[b * 256 + l] : 0.0;
+        for (int w = 128; w >= 1; w >>= 1)
+            for (int l = 0; l < w; ++l) s[l] = s[l] + s[l + w];
+        bs[b] = s[0];
+    }
+    return sum_fixed(bs.data(), nb);
+}
+
+constexpr int kMaxLevels = 2048;
+
 struct Pt {
     double p, c;
     int adv;   // -1 for the origin
@@ -80,10 +130,13 @@ struct Impression {
 
 }  // namespace
 
-extern "C" int oracle_mw_run(int A, int I, double sparsity, double scaling, double epsilon,
-                             int T, double tol, double* dual, double* infeas, int32_t* infeas_idx,
-                             double* wmin, double* wmax, double* budget_w, double* x_avg_out,
-                             double* weights_out, int64_t* nnz_out) {
+extern "C" int oracle_mw_run_mode(int A, int I, double sparsity, double scaling, double epsilon,
+                                  int T, double tol, int binary, double scale, int intervals,
+                                  double* dual, double* infeas, int32_t* infeas_idx, double* wmin,
+                                  double* wmax, double* budget_w, double* x_avg_out,
+                                  double* weights_out, int64_t* nnz_out, int32_t* levels_out,
+                                  double* interval_out) {
+    if (binary && (intervals < 1 || intervals > 8 || !(scale > 0.0))) return -2;
     int64_t nnz = 0;
     if (oracle_gen_adalloc(A, I, sparsity, scaling, &nnz, nullptr, nullptr, nullptr, nullptr,
                            nullptr, nullptr) != 0)
@@ -120,6 +173,7 @@ extern "C" int oracle_mw_run(int A, int I, double sparsity, double scaling, doub
     std::vector<double> x(nnz, 0.0), xa(nnz, 0.0), wb(A);
     std::vector<Impression> sub(I);
     std::vector<double> dcontrib(I);
+    double slope_lo = 0.0, slope_hi = DBL_MAX;   // R/global_problem.cpp:38-39
 
     for (int t = 1; t <= T; ++t) {
         for (int a = 0; a < A; ++a) wb[a] = w[a] * budgets[a];
@@ -171,6 +225,91 @@ extern "C" int oracle_mw_run(int A, int I, double sparsity, double scaling, doub
             }
             s.cut.push_back(DBL_MAX);
         }
+        std::vector<double> beta(I, 0.0);
+        std::vector<int> jstar(I, -1);
+        if (binary) {
+            // ---- global budget split, binary mode (header)
+            const int nr = intervals;
+            static const bool trace = std::getenv("ORACLE_MW_TRACE") != nullptr;
+            std::vector<double> usage(I);
+            auto S = [&](double r, bool strict) {
+                for (int i = 0; i < I; ++i) {
+                    double acc = 0.0;
+                    for (int j = 0; j < sub[i].h - 1; ++j) {
+                        const double u = sub[i].u[j];
+                        if (strict ? (u > r) : (u >= r)) acc = acc + (sub[i].cut[j + 1] - sub[i].cut[j]);
+                    }
+                    usage[i] = acc;
+                }
+                return sum_blocked(usage.data(), I);
+            };
+            if (t == 1) {
+                double maxw = 0.0, minw = DBL_MAX;
+                for (int i = 0; i < I; ++i)
+                    for (int j = 0; j < sub[i].h - 1; ++j) {
+                        const double u = sub[i].u[j];
+                        if (u > maxw) maxw = u;
+                        else if (u < minw) minw = u;
+                    }
+                slope_lo = 1.0 / maxw;
+                slope_hi = 1.0 / minw;
+            }
+            double lower = (t == 1) ? slope_lo : slope_lo * scale;
+            double upper = (t == 1) ? slope_hi : slope_hi / scale;
+            int levels = 0, mode = 0;   // 1 exact (at cr_exact), 2 range (lower, upper)
+            double cr_exact = 0.0;
+            double cr[8], delta[8];
+            for (;;) {
+                ++levels;
+                const double d = (upper - lower) / (double)nr;
+                double r = lower - d;
+                for (int k = 0; k < nr; ++k) { r = r + d; cr[k] = r; }
+                for (int k = 0; k < nr; ++k) delta[k] = S(cr[k], false) - B;
+                if (trace)
+                    std::fprintf(stderr, "t=%d level=%d lower=%.17g upper=%.17g d0=%.6g d%d=%.6g\n", t,
+                                 levels, lower, upper, delta[0], nr - 1, delta[nr - 1]);
+                bool expanded = false;
+                for (int k = 0; k < nr; ++k) {
+                    if (k == 0 && delta[k] < 0.0) { lower = lower * 0.9; expanded = true; break; }
+                    if (k == nr - 1 && delta[k] > 0.0) { upper = upper / 0.9; expanded = true; break; }
+                    if (delta[k] > 0.0) lower = cr[k];
+                    else if (delta[k] < 0.0) { upper = cr[k]; break; }
+                    else { mode = 1; cr_exact = cr[k]; break; }
+                }
+                if (mode == 1) break;
+                if (!expanded && upper - lower < std::max(1e-16, std::fabs(upper) * 0x1p-42)) { mode = 2; break; }
+                if (levels >= kMaxLevels) { mode = 2; break; }
+            }
+            if (levels_out) levels_out[t - 1] = levels;
+            if (interval_out) {
+                interval_out[2 * (t - 1)] = mode == 1 ? cr_exact : lower;
+                interval_out[2 * (t - 1) + 1] = mode == 1 ? cr_exact : upper;
+            }
+            for (int i = 0; i < I; ++i)
+                for (int j = 0; j < sub[i].h - 1; ++j) {
+                    const double u = sub[i].u[j];
+                    if (mode == 1 ? (u >= cr_exact) : (u > upper)) {
+                        beta[i] = beta[i] + (sub[i].cut[j + 1] - sub[i].cut[j]);
+                        jstar[i] = j;
+                    }
+                }
+            if (mode == 2) {
+                double rem = B - sum_blocked(beta.data(), I);
+                bool stop = false;
+                for (int i = 0; i < I && !stop; ++i)
+                    for (int j = 0; j < sub[i].h - 1; ++j) {
+                        const double u = sub[i].u[j];
+                        if (u > lower && u <= upper) {
+                            const double wd = sub[i].cut[j + 1] - sub[i].cut[j];
+                            const double inc = (wd < rem) ? wd : rem;   // std::min(rem, width)
+                            beta[i] = beta[i] + inc;
+                            jstar[i] = j;
+                            rem = rem - inc;
+                            if (rem == 0.0) { stop = true; break; }
+                        }
+                    }
+            }
+        } else {
         // ---- global budget split, sort mode
         struct Reg { double slope, width; int i, j; };
         std::vector<Reg> regs;
@@ -197,8 +336,6 @@ extern "C" int oracle_mw_run(int A, int I, double sparsity, double scaling, doub
             }
             off = off + chunk[c];
         }
-        std::vector<double> beta(I, 0.0);
-        std::vector<int> jstar(I, -1);
         for (int64_t k = 0; k < R; ++k) {
             double rem = B - pre[k];
             if (!(rem > 0.0)) rem = 0.0;
@@ -207,6 +344,7 @@ extern "C" int oracle_mw_run(int A, int I, double sparsity, double scaling, doub
                 beta[regs[k].i] = beta[regs[k].i] + inc;
                 jstar[regs[k].i] = regs[k].j;
             }
+        }
         }
         // ---- primal + dual value
         std::fill(x.begin(), x.end(), 0.0);
@@ -288,5 +426,15 @@ extern "C" int oracle_mw_run(int A, int I, double sparsity, double scaling, doub
     return 0;
 }
 
+extern "C" int oracle_mw_run(int A, int I, double sparsity, double scaling, double epsilon,
+                             int T, double tol, double* dual, double* infeas, int32_t* infeas_idx,
+                             double* wmin, double* wmax, double* budget_w, double* x_avg_out,
+                             double* weights_out, int64_t* nnz_out) {
+    return oracle_mw_run_mode(A, I, sparsity, scaling, epsilon, T, tol, 0, 0.0, 0, dual, infeas,
+                              infeas_idx, wmin, wmax, budget_w, x_avg_out, weights_out, nnz_out,
+                              nullptr, nullptr);
+}
+
 extern "C" double oracle_dexp(double x) { return dexp(x); }
+extern "C" double oracle_sum_blocked(const double* x, int64_t n) { return sum_blocked(x, n); }
 extern "C" double oracle_sum_fixed(const double* x, int64_t n) { return sum_fixed(x, n); }

@@ -1,9 +1,11 @@
 // The reference's driver call sequence (R/main.cpp:44-64), compiled against the
 // drop-in facade (include/distributed_solver/instance.h) instead of the
-// reference sources.  argv: A I sparsity [solve|simplex] [iterations]
+// reference sources.  argv: A I sparsity [solve|simplex] [iterations] [sort]
 //   no mode: GenerateInstance only (host-only, prints the topology);
-//   "solve": RunMultiplicativeWeights exactly as the reference calls it (the
-//            MW loop on the GPU) -> per-iteration "Dual Value = ..." lines;
+//   "solve": R/main.cpp:58-64 literally (use_binary_search = true: the
+//            threshold-search MW loop on the GPU; a trailing "sort" flips the
+//            flag as R/main.cpp:36's comment describes) -> per-iteration
+//            "Dual Value = ..." lines;
 //   "simplex": the added exact entry RunSimplex (dense-tableau simplex).
 // Both solve modes end with one "status ... pivots ... objective ..." line.
 #include <cstdlib>
@@ -21,15 +23,20 @@ int main(int argc, const char* argv[]) {
     int num_iterations = argc > 5 ? std::atoi(argv[5]) : 300;
     long double epsilon = 0.01;
     long double numerical_accuracy_tolerance = 0.000000000000000001;
-    bool use_binary_search = false;
+    bool use_binary_search = true;	// Setting this to false runs the sort method
+    if (argc > 6 && std::string(argv[6]) == "sort") use_binary_search = false;
     int num_bin_intervals = 3;
     long double cr_transition_scale = 1 - epsilon * 0.001;
 
     Instance inst = Instance(A, I, 1, sparsity, epsilon, 0.25, numerical_accuracy_tolerance);
     inst.GenerateInstance();
     if (mode == "solve") {
-        inst.RunMultiplicativeWeights(num_iterations, numerical_accuracy_tolerance,
-                                      use_binary_search, cr_transition_scale, num_bin_intervals);
+        if (!use_binary_search) {
+            inst.RunMultiplicativeWeights(num_iterations, numerical_accuracy_tolerance, use_binary_search);
+        } else {
+            inst.RunMultiplicativeWeights(num_iterations, numerical_accuracy_tolerance, use_binary_search,
+                                          cr_transition_scale, num_bin_intervals);
+        }
     } else if (mode == "simplex") {
         dlp_options o;
         dlp_options_default(&o);

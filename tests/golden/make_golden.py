@@ -165,6 +165,32 @@ def reference_mw_sort():
         runs=out))
 
 
+def reference_mw_binary():
+    """The reference's MW loop in binary (threshold-search) mode, the mode R/main.cpp:36 runs
+    (RunMultiplicativeWeights(T, 1e-18, true, 1 - epsilon * 0.001, 3)), through the same driver."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "dlp_ref_mw")
+    if not os.path.exists(ref):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "ref"])
+    out = {}
+    for (A, I, sp, T) in [(1000, 1000, 0.1, 300), (100, 100, 0.1, 100)]:
+        txt = subprocess.run([ref, str(A), str(I), str(sp), str(T), "binary"], capture_output=True,
+                             text=True, cwd="/tmp", check=True).stdout
+        w = re.findall(r"min weight = (\S+), max weight = (\S+)", txt)
+        cr = re.findall(r"CR: \((\S+), (\S+)\)", txt)
+        out[f"{A}x{I}"] = dict(
+            A=A, I=I, sparsity=sp, iterations=T,
+            dual_values=[float(v) for v in re.findall(r"Dual Value = (\S+)", txt)],
+            max_infeasibility=[float(v) for v in re.findall(r"max infeasiblity was (\S+)", txt)],
+            min_weight=[float(a) for a, _ in w], max_weight=[float(b) for _, b in w],
+            critical_interval=[[float(a), float(b)] for a, b in cr],
+            ratios_in_range=[int(v) for v in re.findall(r"total ratios in range (\d+)", txt)])
+    dump("ref_mw_binary.json", dict(
+        source="oracle/_ref/dlp_ref_mw = reference solver sources + oracle/ref_mw_main.cpp driver, "
+               "binary mode (RunMultiplicativeWeights(T, 1e-18, true, 1 - 0.01 * 0.001, 3)), "
+               "long double, stdout at 6 digits",
+        runs=out))
+
+
 # ---------------------------------------------------------------- general LPs (f4)
 INF = float("inf")
 
@@ -330,9 +356,14 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "general":
     general()
     sys.exit(0)
 
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "mw_binary":
+    reference_mw_binary()
+    sys.exit(0)
+
 if __name__ == "__main__":
     kats()
     generated()
     adalloc()
     reference_run()
     reference_mw_sort()
+    reference_mw_binary()

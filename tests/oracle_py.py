@@ -235,12 +235,22 @@ def bench_windows(m, n, seed, runs, gen_threads, degenerate=False):
     return [(float(s), int(k)) for s, k in zip(secs, done)], gen.value
 
 
-def mw_run(A, I, sparsity=0.1, scaling=0.25, epsilon=0.01, T=300, tol=1e-18):
-    """fp64 MW spec (oracle/oracle_mw.cpp), sort mode.  Returns a dict of per-iteration arrays."""
+def mw_scale(epsilon=0.01):
+    """R/main.cpp:38 cr_transition_scale = 1 - epsilon * 0.001 in x87 long double, to fp64."""
+    return float(np.longdouble(1) - np.longdouble(epsilon) * np.longdouble(0.001))
+
+
+def mw_run(A, I, sparsity=0.1, scaling=0.25, epsilon=0.01, T=300, tol=1e-18, binary=False,
+           scale=None, intervals=3):
+    """fp64 MW spec (oracle/oracle_mw.cpp), sort or binary mode.  Returns a dict of
+    per-iteration arrays (binary mode adds search `levels` and the final `interval`)."""
     L = lib()
     if not getattr(L, "_mw_bound", False):
-        L.oracle_mw_run.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
-                                    C.c_double, _D, _D, _I32, _D, _D, _D, _D, _D, _I64]
+        L.oracle_mw_run_mode.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                         C.c_int, C.c_double, C.c_int, C.c_double, C.c_int, _D, _D,
+                                         _I32, _D, _D, _D, _D, _D, _I64, _I32, _D]
+        L.oracle_sum_blocked.restype = C.c_double
+        L.oracle_sum_blocked.argtypes = [_D, C.c_int64]
         L.oracle_dexp.restype = C.c_double
         L.oracle_dexp.argtypes = [C.c_double]
         L.oracle_sum_fixed.restype = C.c_double
@@ -252,11 +262,19 @@ def mw_run(A, I, sparsity=0.1, scaling=0.25, epsilon=0.01, T=300, tol=1e-18):
     xa = np.zeros(nnz)
     w = np.zeros(A)
     n = C.c_int64()
-    rc = L.oracle_mw_run(A, I, sparsity, scaling, epsilon, T, tol, _d(out["dual"]), _d(out["infeas"]),
-                         idx.ctypes.data_as(_I32), _d(out["wmin"]), _d(out["wmax"]), _d(out["budget"]),
-                         _d(xa), _d(w), C.byref(n))
+    levels = np.zeros(T, np.int32)
+    interval = np.zeros((T, 2))
+    if scale is None:
+        scale = mw_scale(epsilon)
+    rc = L.oracle_mw_run_mode(A, I, sparsity, scaling, epsilon, T, tol, 1 if binary else 0,
+                              scale, intervals, _d(out["dual"]), _d(out["infeas"]),
+                              idx.ctypes.data_as(_I32), _d(out["wmin"]), _d(out["wmax"]),
+                              _d(out["budget"]), _d(xa), _d(w), C.byref(n),
+                              levels.ctypes.data_as(_I32), _d(interval))
     assert rc == 0
     out.update(infeas_idx=idx, x_avg=xa, weights=w, nnz=n.value)
+    if binary:
+        out.update(levels=levels, interval=interval)
     return out
 
 

@@ -79,16 +79,19 @@ def test_reference_driver_simplex_is_exact(driver):
 
 
 @pytest.mark.gpu
-def test_reference_driver_mw_matches_spec(driver):
-    """RunMultiplicativeWeights as R/main.cpp:64 calls it: the GPU MW loop, whose
-    per-iteration duals equal the fp64 spec (oracle/oracle_mw.cpp) bit for bit."""
+@pytest.mark.parametrize("mode", ["binary", "sort"])
+def test_reference_driver_mw_matches_spec(driver, mode):
+    """RunMultiplicativeWeights as R/main.cpp:58-64 calls it (binary search, the
+    reference's default; and the sort method its flag selects): the GPU MW loop,
+    whose per-iteration duals equal the fp64 spec (oracle/oracle_mw.cpp) bit
+    for bit."""
     import oracle_py as O
     T = 40
-    out = subprocess.run([driver, "200", "300", "0.1", "solve", str(T)], capture_output=True,
-                         text=True, check=True, timeout=300).stdout
+    args = [driver, "200", "300", "0.1", "solve", str(T)] + (["sort"] if mode == "sort" else [])
+    out = subprocess.run(args, capture_output=True, text=True, check=True, timeout=300).stdout
     duals = [float(v) for v in re.findall(r"^Dual Value = (\S+)$", out, re.M)]
     assert len(duals) == T
-    r = O.mw_run(200, 300, 0.1, 0.25, 0.01, T)
+    r = O.mw_run(200, 300, 0.1, 0.25, 0.01, T, binary=(mode == "binary"))
     # printed at the reference's default 6-digit precision
     for d, e in zip(duals, r["dual"]):
         assert abs(d - e) <= 5e-6 * abs(e)
