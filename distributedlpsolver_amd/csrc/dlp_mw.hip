@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -80,13 +81,36 @@ __device__ inline double dexp(double x) {
     return __builtin_ldexp(p, (int)k);
 }
 
+// One lane's chain of the fixed-order sum: x[lane], x[lane+64], ... added in
+// order; loads issued 16 ahead of the dependent adds (same order, no stall per
+// element).
+__device__ inline double lane_chain(const double* __restrict__ x, int64_t n, int lane) {
+    constexpr int U = 16;
+    double acc = 0.0;
+    int64_t k = lane;
+    for (; k + 64 * (U - 1) < n; k += 64 * U) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = x[k + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = acc + v[u];
+    }
+    for (; k < n; k += 64) acc = acc + x[k];
+    return acc;
+}
+
+// sum_fixed by one wave (spec: 64 strided sequential chains, halving tree).
+__device__ inline double wave_sum_fixed(const double* x, int64_t n, int lane) {
+    double a = lane_chain(x, n, lane);
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) a = a + __shfl_down(a, w);
+    return a;
+}
+
 // Fixed-order sum (spec): 64 strided sequential chains, then the halving tree.
 __global__ __launch_bounds__(64) void sum_fixed_kernel(const double* __restrict__ x, int64_t n,
                                                        double* __restrict__ out) {
-    double acc = 0.0;
-    for (int64_t k = threadIdx.x; k < n; k += 64) acc = acc + x[k];
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) acc = acc + __shfl_down(acc, w);
+    const double acc = wave_sum_fixed(x, n, threadIdx.x);
     if (threadIdx.x == 0) *out = acc;
 }
 
@@ -105,6 +129,48 @@ __device__ inline bool hull_before(const HullPt& a, const HullPt& b) {   // (c d
     if (a.c != b.c) return a.c > b.c;
     if (a.p != b.p) return a.p > b.p;
     return a.adv < b.adv;
+}
+
+// Monotone chain over the n sorted points (lane 0), envelope points and
+// cutoffs to the impression's slots (R/upper_envelope.cpp:15-38,
+// R/subproblem.cpp:186-233).
+__device__ inline void envelope_chain(const double* sc, const double* sp, const int* sa, int* stk, int n,
+                                      int64_t b0, int i, double* env_u, double* env_v, double* cut,
+                                      int32_t* hull_h) {
+    (void)sa;
+    int h = 0;
+    for (int q = 0; q < n; ++q) {
+        while (h >= 2) {
+            const int O = stk[h - 2], Aq = stk[h - 1];
+            const double d1 = (sc[Aq] - sc[O]) * (sp[q] - sp[O]);
+            const double d2 = (sp[Aq] - sp[O]) * (sc[q] - sc[O]);
+            if (d1 - d2 <= kHullTol) --h; else break;
+        }
+        stk[h++] = q;
+    }
+    const int64_t bu = b0 + i, bc = b0 + 2 * (int64_t)i;
+    {
+        const int q = stk[h - 2];
+        env_u[bu] = sp[q] / sc[q];
+        env_v[bu] = 0.0;
+    }
+    int e = 1;
+    for (int k = h - 2; k > 0; --k, ++e) {
+        const int q1 = stk[k - 1], q0 = stk[k];
+        const double uu = (sp[q1] - sp[q0]) / (sc[q1] - sc[q0]);
+        env_u[bu + e] = uu;
+        const double t = sc[q1] * uu;
+        env_v[bu + e] = sp[q1] - t;
+    }
+    env_u[bu + e] = 0.0;
+    env_v[bu + e] = sp[stk[0]];
+    cut[bc] = 0.0;
+    for (int k = 0; k < h - 1; ++k) {
+        const double du = env_u[bu + k] - env_u[bu + k + 1];
+        cut[bc + k + 1] = (du > kHullTol) ? (env_v[bu + k + 1] - env_v[bu + k]) / du : cut[bc + k];
+    }
+    cut[bc + h] = DBL_MAX;
+    hull_h[i] = h;
 }
 
 // One 64-lane workgroup per impression: points to LDS, bitonic sort, monotone
@@ -163,39 +229,67 @@ __global__ __launch_bounds__(64) void envelope_kernel(const int64_t* __restrict_
         }
     }
     if (lane != 0) return;
-    int h = 0;
-    for (int q = 0; q < n; ++q) {
-        while (h >= 2) {
-            const int O = stk[h - 2], Aq = stk[h - 1];
-            const double d1 = (sc[Aq] - sc[O]) * (sp[q] - sp[O]);
-            const double d2 = (sp[Aq] - sp[O]) * (sc[q] - sc[O]);
-            if (d1 - d2 <= kHullTol) --h; else break;
+    envelope_chain(sc, sp, sa, stk, n, b0, i, env_u, env_v, cut, hull_h);
+}
+
+// Several impressions per 64-lane workgroup (SEG lanes each, every impression
+// with deg + 1 <= SEG points): the same total-order sort (SEG-element bitonic
+// network, padding last) and the same chain, run by lane 0 of each segment.
+template <int SEG>
+__global__ __launch_bounds__(64) void envelope_seg_kernel(const int64_t* __restrict__ iptr,
+                                                          const int32_t* __restrict__ iadv,
+                                                          const double* __restrict__ ibid,
+                                                          const double* __restrict__ w, int I, double* env_u,
+                                                          double* env_v, double* cut, int32_t* hull_h) {
+    __shared__ double sc_all[64], sp_all[64];
+    __shared__ int sa_all[64], stk_all[64];
+    const int lane = threadIdx.x, sg = lane / SEG, t = lane % SEG;
+    const int i = blockIdx.x * (64 / SEG) + sg;
+    double* sc = sc_all + sg * SEG;
+    double* sp = sp_all + sg * SEG;
+    int* sa = sa_all + sg * SEG;
+    int64_t b0 = 0;
+    int deg = 0;
+    if (i < I) {
+        b0 = iptr[i];
+        deg = (int)(iptr[i + 1] - b0);
+    }
+    if (t < deg) {
+        const double p = ibid[b0 + t];
+        const int a = iadv[b0 + t];
+        sp[t] = p;
+        sc[t] = p * w[a];
+        sa[t] = a;
+    } else if (t == deg) {
+        sp[t] = 0.0;
+        sc[t] = 0.0;
+        sa[t] = -1;
+    } else {
+        sp[t] = -__builtin_inf();
+        sc[t] = -__builtin_inf();
+        sa[t] = 0x7fffffff;
+    }
+    __syncthreads();
+    for (int k = 2; k <= SEG; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int o = t ^ j;
+            if (o > t) {
+                const HullPt A{sc[t], sp[t], sa[t]}, B{sc[o], sp[o], sa[o]};
+                const bool asc = (t & k) == 0;
+                if (asc ? hull_before(B, A) : hull_before(A, B)) {
+                    sc[t] = B.c; sp[t] = B.p; sa[t] = B.adv;
+                    sc[o] = A.c; sp[o] = A.p; sa[o] = A.adv;
+                }
+            }
+            __syncthreads();
         }
-        stk[h++] = q;
     }
-    const int64_t bu = b0 + i, bc = b0 + 2 * (int64_t)i;
-    {
-        const int q = stk[h - 2];
-        env_u[bu] = sp[q] / sc[q];
-        env_v[bu] = 0.0;
+    if (t != 0 || i >= I) return;
+    if (deg == 0) {
+        hull_h[i] = 0;
+        return;
     }
-    int e = 1;
-    for (int k = h - 2; k > 0; --k, ++e) {
-        const int q1 = stk[k - 1], q0 = stk[k];
-        const double uu = (sp[q1] - sp[q0]) / (sc[q1] - sc[q0]);
-        env_u[bu + e] = uu;
-        const double t = sc[q1] * uu;
-        env_v[bu + e] = sp[q1] - t;
-    }
-    env_u[bu + e] = 0.0;
-    env_v[bu + e] = sp[stk[0]];
-    cut[bc] = 0.0;
-    for (int k = 0; k < h - 1; ++k) {
-        const double du = env_u[bu + k] - env_u[bu + k + 1];
-        cut[bc + k + 1] = (du > kHullTol) ? (env_v[bu + k + 1] - env_v[bu + k]) / du : cut[bc + k];
-    }
-    cut[bc + h] = DBL_MAX;
-    hull_h[i] = h;
+    envelope_chain(sc, sp, sa, stk_all + sg * SEG, deg + 1, b0, i, env_u, env_v, cut, hull_h);
 }
 
 __global__ void region_count_kernel(const int32_t* __restrict__ hull_h, int I, int32_t* cnt) {
@@ -396,18 +490,45 @@ __global__ void advertiser_kernel(const int64_t* __restrict__ aptr, const int64_
 struct BinState;
 __device__ inline int bin_levels(const BinState* st);
 
-// Per-iteration report (one wave): worst average infeasibility (first index
-// on ties), min / max weight; writes log[t].
-__global__ __launch_bounds__(64) void report_kernel(const double* __restrict__ avg_slack,
-                                                    const double* __restrict__ budgets,
-                                                    const double* __restrict__ w, int A,
-                                                    const double* __restrict__ dual,
-                                                    const double* __restrict__ Bptr,
-                                                    const BinState* __restrict__ bst,
-                                                    dlp_mw_iter* __restrict__ log) {
-    double worst = 0.0, mn = 100000.0, mx = 0.0;
+// Per-iteration report: worst average infeasibility (first index on ties),
+// min / max weight; writes log[t].  Every combine is exact (max with a first-
+// index tie rule, fmin, fmax), so blocks of 256 lanes reduce in any order;
+// the block that finishes last combines the block partials.
+struct ReportPart {
+    double worst, mn, mx;
+    int32_t wi, pad;
+};
+
+__device__ inline void report_combine(double& worst, int& wi, double& mn, double& mx, double ow, int oi,
+                                      double omn, double omx) {
+    if (ow > worst || (ow == worst && oi >= 0 && (wi < 0 || oi < wi))) {
+        worst = ow;
+        wi = oi;
+    }
+    mn = __builtin_fmin(mn, omn);
+    mx = __builtin_fmax(mx, omx);
+}
+
+__device__ inline void report_wave(double& worst, int& wi, double& mn, double& mx) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+        report_combine(worst, wi, mn, mx, __shfl_xor(worst, m), __shfl_xor(wi, m), __shfl_xor(mn, m),
+                       __shfl_xor(mx, m));
+}
+
+__global__ __launch_bounds__(256) void report_kernel(const double* __restrict__ avg_slack,
+                                                     const double* __restrict__ budgets,
+                                                     const double* __restrict__ w, int A,
+                                                     const double* __restrict__ dual,
+                                                     const double* __restrict__ Bptr,
+                                                     const BinState* __restrict__ bst, ReportPart* part,
+                                                     uint32_t* ticket, dlp_mw_iter* __restrict__ log) {
+    __shared__ ReportPart sp[4];
+    __shared__ int last;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double worst = 0.0, mn = 100000.0, mx = 0.0;   // R/allocation_mw.cpp:254-255
     int wi = -1;
-    for (int a = threadIdx.x; a < A; a += 64) {
+    for (int a = blockIdx.x * 256 + tid; a < A; a += gridDim.x * 256) {
         const double s = avg_slack[a];
         if (s > 0.0) {
             const double r = s / budgets[a];
@@ -416,15 +537,25 @@ __global__ __launch_bounds__(64) void report_kernel(const double* __restrict__ a
         mn = __builtin_fmin(mn, w[a]);
         mx = __builtin_fmax(mx, w[a]);
     }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const double ow = __shfl_xor(worst, m);
-        const int oi = __shfl_xor(wi, m);
-        if (ow > worst || (ow == worst && oi >= 0 && (wi < 0 || oi < wi))) { worst = ow; wi = oi; }
-        mn = __builtin_fmin(mn, __shfl_xor(mn, m));
-        mx = __builtin_fmax(mx, __shfl_xor(mx, m));
+    report_wave(worst, wi, mn, mx);
+    if (lane == 0) sp[wv] = ReportPart{worst, mn, mx, wi, 0};
+    __syncthreads();
+    if (tid == 0) {
+        for (int k = 1; k < 4; ++k) report_combine(worst, wi, mn, mx, sp[k].worst, sp[k].wi, sp[k].mn, sp[k].mx);
+        part[blockIdx.x] = ReportPart{worst, mn, mx, wi, 0};
+        __threadfence();
+        last = (atomicAdd(ticket, 1u) == gridDim.x - 1);
     }
-    if (threadIdx.x == 0) {
+    __syncthreads();
+    if (!last || wv != 0) return;
+    __threadfence();
+    worst = 0.0; mn = 100000.0; mx = 0.0; wi = -1;
+    for (int b = lane; b < (int)gridDim.x; b += 64) {
+        const ReportPart q = part[b];
+        report_combine(worst, wi, mn, mx, q.worst, q.wi, q.mn, q.mx);
+    }
+    report_wave(worst, wi, mn, mx);
+    if (lane == 0) {
         dlp_mw_iter e;
         e.dual_value = *dual;
         e.max_infeasibility = worst;
@@ -434,6 +565,7 @@ __global__ __launch_bounds__(64) void report_kernel(const double* __restrict__ a
         e.max_weight = mx;
         e.weighted_budget = *Bptr;
         *log = e;
+        *ticket = 0;
     }
 }
 
@@ -452,7 +584,7 @@ struct BinState {
     double slope_lo, slope_hi;        // FindMinMaxSlope, iteration 1 only
     double rem;                       // budget left for the tie regions
     int32_t nr, levels, done, mode;   // mode 1 = exact ratio, 2 = range
-    uint32_t ticket, pad;
+    int32_t pad;
 };
 
 __device__ inline int bin_levels(const BinState* st) { return st->levels; }
@@ -505,21 +637,38 @@ __device__ inline void bin_control(BinState* st, const double* S, double B) {
     bin_set_ratios(st);
 }
 
-// usage_i(cr_k) = sum over the impression's regions (in order) of width if u >= cr_k.
+// usage_i(cr_k) = sum over the impression's regions (in order) of width if
+// u >= cr_k, for the n regions at r0 of ku (slopes) / kw (widths).
+__device__ inline void bin_usage_rn(int r0, int n, const double* ku, const double* kw, const double* cr, int nr,
+                                    double* acc) {
+#pragma unroll
+    for (int k = 0; k < kBinMaxRatios; ++k) acc[k] = 0.0;
+    // loads issued 4 regions ahead of the (ordered) conditional adds
+    constexpr int U = 4;
+    for (int j0 = 0; j0 < n; j0 += U) {
+        double u[U], w[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int j = (j0 + q < n) ? j0 + q : n - 1;
+            u[q] = ku[r0 + j];
+            w[q] = kw[r0 + j];
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            if (j0 + q >= n) break;
+#pragma unroll
+            for (int k = 0; k < kBinMaxRatios; ++k)
+                if (k < nr && u[q] >= cr[k]) acc[k] = acc[k] + w[q];
+        }
+    }
+}
+
 __device__ inline void bin_usage(int i, int I, const int32_t* __restrict__ roff,
                                  const int32_t* __restrict__ rcnt, const double* __restrict__ keys,
                                  const double* __restrict__ rwidth, const double* cr, int nr,
                                  double* acc) {
-#pragma unroll
-    for (int k = 0; k < kBinMaxRatios; ++k) acc[k] = 0.0;
-    if (i >= I) return;
-    const int r0 = roff[i], n = rcnt[i];
-    for (int j = 0; j < n; ++j) {
-        const double u = keys[r0 + j], w = rwidth[r0 + j];
-#pragma unroll
-        for (int k = 0; k < kBinMaxRatios; ++k)
-            if (k < nr && u >= cr[k]) acc[k] = acc[k] + w;
-    }
+    const bool in = i < I;
+    bin_usage_rn(in ? roff[i] : 0, in ? rcnt[i] : 0, keys, rwidth, cr, nr, acc);
 }
 
 // Spec block tree over 256 lanes (lds[k][256] filled, synchronised): s_l += s_{l+w},
@@ -537,15 +686,6 @@ __device__ inline void bin_block_tree(double (*lds)[kBinBlock], int nk, int tid,
             if (tid == 0) out[k] = x;
         }
     }
-}
-
-// sum_fixed by one wave over n values at stride 1 (spec: 64 strided chains, halving tree).
-__device__ inline double wave_sum_fixed(const double* x, int n, int lane) {
-    double a = 0.0;
-    for (int q = lane; q < n; q += 64) a = a + x[q];
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) a = a + __shfl_down(a, w);
-    return a;
 }
 
 // FindMinMaxSlope (R/global_problem.cpp:116-135) over regions in id order =
@@ -617,23 +757,23 @@ __global__ void bin_begin_kernel(BinState* st, int first, double scale, int nr) 
     st->levels = 0;
     st->done = 0;
     st->mode = 0;
-    st->ticket = 0;
     st->rem = 0.0;
     bin_set_ratios(st);
 }
 
-// One search level over all impressions; the last block to finish reduces
-// the block sums and applies the control rule.  A launch after the search
-// stopped returns at once.
-__global__ __launch_bounds__(kBinBlock) void bin_level_kernel(BinState* st, const int32_t* __restrict__ roff,
+// One search level over all impressions: block sums of the nr usages (spec
+// tree per 256 impressions).  A launch after the search stopped returns at
+// once.  No cross-block hand-off inside the kernel: a device-scope fence per
+// block is an L2 write-back per block on gfx950; the kernel boundary orders
+// the block sums for bin_control_kernel instead.
+__global__ __launch_bounds__(kBinBlock) void bin_level_kernel(const BinState* st, const int32_t* __restrict__ roff,
                                                               const int32_t* __restrict__ rcnt,
                                                               const double* __restrict__ keys,
                                                               const double* __restrict__ rwidth, int I,
-                                                              double* bsum, const double* __restrict__ Bptr) {
+                                                              double* __restrict__ bsum) {
     if (st->done) return;
     __shared__ double lds[kBinMaxRatios][kBinBlock];
     __shared__ double tot[kBinMaxRatios];
-    __shared__ int last;
     const int nr = st->nr, tid = threadIdx.x, nb = gridDim.x, b = blockIdx.x;
     double cr[kBinMaxRatios], acc[kBinMaxRatios];
 #pragma unroll
@@ -644,41 +784,56 @@ __global__ __launch_bounds__(kBinBlock) void bin_level_kernel(BinState* st, cons
         if (k < nr) lds[k][tid] = acc[k];
     __syncthreads();
     bin_block_tree<kBinMaxRatios>(lds, nr, tid, tot);
-    if (tid == 0) {
+    if (tid == 0)
         for (int k = 0; k < nr; ++k) bsum[(int64_t)k * nb + b] = tot[k];
-        __threadfence();
-        last = (atomicAdd(&st->ticket, 1u) == (unsigned)(nb - 1));
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const int wv = tid >> 6, lane = tid & 63;
+}
+
+// sum_fixed of each ratio's block sums (one wave per ratio) and the control rule.
+__global__ __launch_bounds__(kBinBlock) void bin_control_kernel(BinState* st, const double* __restrict__ bsum,
+                                                                int nb, const double* __restrict__ Bptr) {
+    if (st->done) return;
+    __shared__ double tot[kBinMaxRatios];
+    const int nr = st->nr, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     for (int k = wv; k < nr; k += kBinBlock / 64) {
         const double a = wave_sum_fixed(bsum + (int64_t)k * nb, nb, lane);
         if (lane == 0) tot[k] = a;
     }
     __syncthreads();
-    if (tid == 0) {
-        bin_control(st, tot, *Bptr);
-        st->ticket = 0;
-    }
+    if (tid == 0) bin_control(st, tot, *Bptr);
 }
 
 // The whole search in one workgroup of 1024 lanes (nb <= kBinSingleBlocks):
 // four 256-lane groups take the blocks of the spec in turn; the control state
-// lives in LDS.
+// lives in LDS.  With at most 4 blocks every lane keeps its impression's
+// region range in registers, and the regions (slope, width) are staged in LDS
+// once when they fit (`cached`), so a level touches no global memory.
 __global__ __launch_bounds__(1024) void bin_search_single_kernel(BinState* st, const int32_t* __restrict__ roff,
                                                                  const int32_t* __restrict__ rcnt,
                                                                  const double* __restrict__ keys,
                                                                  const double* __restrict__ rwidth, int I,
+                                                                 int R, int cached,
                                                                  const double* __restrict__ Bptr) {
-    __shared__ double lds[4][kBinMaxRatios][kBinBlock];
+    extern __shared__ double rcache[];   // 2R doubles when cached
+    __shared__ double lds[4][kBinBlock];
     __shared__ double bs[kBinMaxRatios][kBinSingleBlocks];
     __shared__ double tot[kBinMaxRatios];
     __shared__ BinState ss;
     const int tid = threadIdx.x, g = tid >> 8, gl = tid & 255;
     const int nb = (I + kBinBlock - 1) / kBinBlock;
     if (tid == 0) ss = *st;
+    if (cached)
+        for (int k = tid; k < R; k += 1024) {
+            rcache[k] = keys[k];
+            rcache[R + k] = rwidth[k];
+        }
+    const double* ku = cached ? rcache : keys;
+    const double* kw = cached ? rcache + R : rwidth;
+    const bool one_round = nb <= 4;
+    int r0 = 0, n = 0;
+    if (one_round && g * kBinBlock + gl < I) {
+        r0 = roff[g * kBinBlock + gl];
+        n = rcnt[g * kBinBlock + gl];
+    }
     __syncthreads();
     const int nr = ss.nr;
     const double B = *Bptr;
@@ -688,23 +843,27 @@ __global__ __launch_bounds__(1024) void bin_search_single_kernel(BinState* st, c
         for (int k = 0; k < kBinMaxRatios; ++k) cr[k] = (k < nr) ? ss.cr[k] : 0.0;
         for (int b0 = 0; b0 < nb; b0 += 4) {
             const int b = b0 + g;
-            bin_usage(b < nb ? b * kBinBlock + gl : I, I, roff, rcnt, keys, rwidth, cr, nr, acc);
+            if (!one_round) {
+                const int i = b * kBinBlock + gl;
+                r0 = (b < nb && i < I) ? roff[i] : 0;
+                n = (b < nb && i < I) ? rcnt[i] : 0;
+            }
+            bin_usage_rn(r0, b < nb ? n : 0, ku, kw, cr, nr, acc);
 #pragma unroll
-            for (int k = 0; k < kBinMaxRatios; ++k)
-                if (k < nr) lds[g][k][gl] = acc[k];
-            __syncthreads();
-            if (gl < 128)
-                for (int k = 0; k < nr; ++k) lds[g][k][gl] = lds[g][k][gl] + lds[g][k][gl + 128];
-            __syncthreads();
-            if (gl < 64 && b < nb) {
-                for (int k = 0; k < nr; ++k) {
-                    double x = lds[g][k][gl] + lds[g][k][gl + 64];
+            for (int k = 0; k < kBinMaxRatios; ++k) {
+                if (k >= nr) break;
+                lds[g][gl] = acc[k];
+                __syncthreads();
+                if (gl < 128) lds[g][gl] = lds[g][gl] + lds[g][gl + 128];
+                __syncthreads();
+                if (gl < 64 && b < nb) {
+                    double x = lds[g][gl] + lds[g][gl + 64];
 #pragma unroll
                     for (int w = 32; w >= 1; w >>= 1) x = x + __shfl_down(x, w);
                     if (gl == 0) bs[k][b] = x;
                 }
+                __syncthreads();
             }
-            __syncthreads();
         }
         const int wv = tid >> 6, lane = tid & 63;
         if (wv < nr) {
@@ -720,20 +879,19 @@ __global__ __launch_bounds__(1024) void bin_search_single_kernel(BinState* st, c
 
 // Final allocation, full part (R/global_problem.cpp:166-178 exact hit,
 // 180-195 range): state 1 + inc = width for regions u >= cr (exact) or
-// u > upper (range); tie candidates lower < u <= upper flagged; rem = B -
-// sum_blocked(full part per impression) by the last block.
-__global__ __launch_bounds__(kBinBlock) void bin_assign_kernel(BinState* st, const int32_t* __restrict__ roff,
+// u > upper (range); tie candidates lower < u <= upper flagged; block sums
+// of the full part per impression (spec tree) for bin_rem_kernel.
+__global__ __launch_bounds__(kBinBlock) void bin_assign_kernel(const BinState* st, const int32_t* __restrict__ roff,
                                                                const int32_t* __restrict__ rcnt,
                                                                const double* __restrict__ keys,
                                                                const double* __restrict__ rwidth, int I,
                                                                int32_t* __restrict__ rstate,
                                                                double* __restrict__ inc,
-                                                               uint8_t* __restrict__ flags, double* bsum,
-                                                               const double* __restrict__ Bptr) {
+                                                               uint8_t* __restrict__ flags,
+                                                               double* __restrict__ bsum) {
     __shared__ double lds[1][kBinBlock];
     __shared__ double tot[1];
-    __shared__ int last;
-    const int tid = threadIdx.x, nb = gridDim.x, b = blockIdx.x;
+    const int tid = threadIdx.x, b = blockIdx.x;
     const int i = b * kBinBlock + tid;
     const int mode = st->mode;
     const double lo = st->fin_lo, up = st->fin_up;
@@ -753,26 +911,22 @@ __global__ __launch_bounds__(kBinBlock) void bin_assign_kernel(BinState* st, con
     lds[0][tid] = beta;
     __syncthreads();
     bin_block_tree<1>(lds, 1, tid, tot);
-    if (tid == 0) {
-        bsum[b] = tot[0];
-        __threadfence();
-        last = (atomicAdd(&st->ticket, 1u) == (unsigned)(nb - 1));
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    if (tid < 64) {
-        const double a = wave_sum_fixed(bsum, nb, tid);
-        if (tid == 0) {
-            st->rem = *Bptr - a;
-            st->ticket = 0;
-        }
-    }
+    if (tid == 0) bsum[b] = tot[0];
+}
+
+// rem = B - sum_fixed(block sums of the full part).
+__global__ __launch_bounds__(64) void bin_rem_kernel(BinState* st, const double* __restrict__ bsum, int nb,
+                                                     const double* __restrict__ Bptr) {
+    const double a = wave_sum_fixed(bsum, nb, threadIdx.x);
+    if (threadIdx.x == 0) st->rem = *Bptr - a;
 }
 
 // Tie regions in (impression, region) order (R/global_problem.cpp:197-221):
 // inc = min(rem, width), assigned whatever its sign, rem -= inc, stop at
-// rem == 0.  One wave; 64 widths per load, walked with the budget uniform.
+// rem == 0.  rem reaches 0 exactly at the first tie whose width is not below
+// the budget left (fl(a - b) == 0 iff a == b), so a batch of 64 runs the
+// serial chain r_{k+1} = r_k - w_k alone (one dependent add per tie; r_k
+// parked in lane k), then one ballot finds the stopping tie.  One wave.
 __global__ __launch_bounds__(64) void bin_tie_chain_kernel(BinState* st, const int32_t* __restrict__ tie_ids,
                                                            const int32_t* __restrict__ num_ties,
                                                            const double* __restrict__ rwidth,
@@ -781,25 +935,46 @@ __global__ __launch_bounds__(64) void bin_tie_chain_kernel(BinState* st, const i
     const int lane = threadIdx.x;
     const int n = *num_ties;
     double rem = st->rem;
-    bool stop = false;
-    for (int base = 0; base < n && !stop; base += 64) {
+    int serial_from = -1;
+    for (int base = 0; base < n; base += 64) {
         const int q = base + lane;
         const int id = (q < n) ? tie_ids[q] : 0;
         const double w = (q < n) ? rwidth[id] : 0.0;
         const int cnt = (n - base < 64) ? n - base : 64;
+        const uint64_t wb = __builtin_bit_cast(uint64_t, w);
+        const int wlo = (int)(uint32_t)wb, whi = (int)(uint32_t)(wb >> 32);
+        double r = 0.0;   // r_lane
         for (int k = 0; k < cnt; ++k) {
-            const double wk = __shfl(w, k);
-            const double a = (wk < rem) ? wk : rem;   // std::min(rem, width)
-            if (lane == k) {
-                inc[id] = a;
-                rstate[id] = 2;
-            }
-            rem = rem - a;
-            if (rem == 0.0) {
-                stop = true;
-                break;
-            }
+            r = (lane == k) ? rem : r;
+            const uint64_t kb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(whi, k) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane(wlo, k);
+            rem = rem - __builtin_bit_cast(double, kb);
         }
+        const bool stop_here = (lane < cnt) && !(w < r);   // std::min(rem, width) takes rem
+        const uint64_t ball = __ballot(stop_here);
+        const int f = ball ? __builtin_ctzll(ball) : cnt;
+        if (lane < cnt && lane <= f) {
+            inc[id] = (lane == f) ? r : w;
+            rstate[id] = 2;
+        }
+        if (ball) {
+            const double rf = __shfl(r, f);
+            rem = rf - rf;   // 0 unless the budget is not finite
+            if (rem != 0.0) serial_from = base + f + 1;
+            break;
+        }
+    }
+    // non-finite budget (inf - inf): the literal walk for the rest
+    for (int q = serial_from; q >= 0 && q < n; ++q) {
+        const int id = tie_ids[q];
+        const double w = rwidth[id];
+        const double a = (w < rem) ? w : rem;
+        if (lane == 0) {
+            inc[id] = a;
+            rstate[id] = 2;
+        }
+        rem = rem - a;
+        if (rem == 0.0) break;
     }
     if (lane == 0) st->rem = rem;
 }
@@ -829,12 +1004,16 @@ struct dlp_mw {
     dlp_mw_iter* dlog = nullptr;
     int log_cap = 0;
     // binary mode
+    int maxdeg = 0;
     int binary = 0, nr = 3;
     double scale = 0.0;
     double *rwidth = nullptr, *bsum = nullptr, *cmax = nullptr, *pmax = nullptr, *cmin = nullptr;
     uint8_t* flags = nullptr;
     int32_t *tie_ids = nullptr, *num_ties = nullptr;
     dlp::mw::BinState* bst = nullptr;
+    dlp::mw::ReportPart* rpart = nullptr;
+    uint32_t* rticket = nullptr;
+    int report_blocks = 1;
     void* cub_tmp = nullptr;
     size_t cub_bytes = 0;
     std::vector<int64_t> var_to_imp;   // problem variable k -> impression-major index
@@ -871,7 +1050,7 @@ void mw_free(dlp_mw* m) {
                     m->ids_sorted, m->reg_imp, m->reg_j, m->pos_by_id, m->inc_by_id, m->chunk,
                     m->offs, m->dcontrib, m->B, m->dual, m->rtotal, m->dlog, m->cub_tmp,
                     m->rwidth, m->bsum, m->cmax, m->pmax, m->cmin, m->flags, m->tie_ids,
-                    m->num_ties, m->bst};
+                    m->num_ties, m->bst, m->rpart, m->rticket};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -903,6 +1082,7 @@ int mw_init(const dlp_problem* prob, const dlp_mw_options* o, dlp_mw* m) {
     for (int a = 0; a < A; ++a) aptr[a + 1] += aptr[a];
     int maxdeg = 0;
     for (int i = 0; i < I; ++i) maxdeg = std::max<int>(maxdeg, (int)(iptr[i + 1] - iptr[i]));
+    m->maxdeg = maxdeg;
     if (maxdeg + 1 > dlp::mw::kDegMax) {
         set_error("dlp_mw: an impression has more bids than the envelope kernel holds");
         return DLP_ERR_UNSUPPORTED;
@@ -942,6 +1122,9 @@ int mw_init(const dlp_problem* prob, const dlp_mw_options* o, dlp_mw* m) {
     MW_ALLOC(m->reg_j, nnz); MW_ALLOC(m->pos_by_id, nnz); MW_ALLOC(m->inc_by_id, nnz);
     MW_ALLOC(m->chunk, nnz / dlp::mw::kChunk + 2); MW_ALLOC(m->offs, nnz / dlp::mw::kChunk + 2);
     MW_ALLOC(m->dcontrib, I); MW_ALLOC(m->B, 1); MW_ALLOC(m->dual, 1); MW_ALLOC(m->rtotal, 1);
+    m->report_blocks = std::max(1, std::min(1024, (A + 255) / 256));
+    MW_ALLOC(m->rpart, m->report_blocks); MW_ALLOC(m->rticket, 1);
+    MW_TRY(hipMemset(m->rticket, 0, sizeof(uint32_t)));
     m->binary = o->binary ? 1 : 0;
     if (m->binary) {
         using dlp::mw::kBinBlock;
@@ -1006,14 +1189,28 @@ int bin_allocate(dlp_mw* m, int64_t R, int t) {
     }
     bin_begin_kernel<<<1, 64, 0, s>>>(m->bst, t == 1 ? 1 : 0, m->scale, m->nr);
     if (nb <= kBinSingleBlocks) {
-        bin_search_single_kernel<<<1, 1024, 0, s>>>(m->bst, m->roff, m->rcnt, m->keys, m->rwidth, I, m->B);
+        constexpr size_t kCacheMax = 144 * 1024;   // LDS for the region cache (static part ~12.5 KB)
+        static bool attr_set[64] = {};
+        if (!attr_set[m->device & 63]) {
+            MW_TRY(hipFuncSetAttribute((const void*)bin_search_single_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCacheMax));
+            attr_set[m->device & 63] = true;
+        }
+        // DLP_MW_NO_LDS_CACHE=1: regions read from HBM every level (test knob)
+        const char* nc = std::getenv("DLP_MW_NO_LDS_CACHE");
+        const bool allow = !(nc && nc[0] == '1');
+        const int cached = (allow && R > 0 && (size_t)R * 16 <= kCacheMax) ? 1 : 0;
+        bin_search_single_kernel<<<1, 1024, cached ? (size_t)R * 16 : 0, s>>>(
+            m->bst, m->roff, m->rcnt, m->keys, m->rwidth, I, (int)R, cached, m->B);
     } else {
         int32_t done = 0;
         for (int issued = 0; !done;) {
             const int batch = issued == 0 ? 48 : 32;
-            for (int k = 0; k < batch; ++k)
+            for (int k = 0; k < batch; ++k) {
                 bin_level_kernel<<<nb, kBinBlock, 0, s>>>(m->bst, m->roff, m->rcnt, m->keys, m->rwidth, I,
-                                                          m->bsum, m->B);
+                                                          m->bsum);
+                bin_control_kernel<<<1, kBinBlock, 0, s>>>(m->bst, m->bsum, nb, m->B);
+            }
             issued += batch;
             MW_TRY(hipGetLastError());
             MW_TRY(hipMemcpyAsync(&done, &m->bst->done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1025,7 +1222,8 @@ int bin_allocate(dlp_mw* m, int64_t R, int t) {
         }
     }
     bin_assign_kernel<<<nb, kBinBlock, 0, s>>>(m->bst, m->roff, m->rcnt, m->keys, m->rwidth, I, m->pos_by_id,
-                                               m->inc_by_id, m->flags, m->bsum, m->B);
+                                               m->inc_by_id, m->flags, m->bsum);
+    bin_rem_kernel<<<1, 64, 0, s>>>(m->bst, m->bsum, nb, m->B);
     if (R > 0) {
         size_t bytes = m->cub_bytes;
         MW_TRY(hipcub::DeviceSelect::Flagged(m->cub_tmp, bytes, hipcub::CountingInputIterator<int32_t>(0),
@@ -1047,8 +1245,15 @@ int mw_iteration(dlp_mw* m, dlp_mw_iter* dlog_entry) {
     const double fa = (double)(t - 1) / (double)t, fb = 1.0 / (double)t;
     weighted_budget_kernel<<<(A + tb - 1) / tb, tb, 0, s>>>(m->w, m->budgets, A, m->wb);
     sum_fixed_kernel<<<1, 64, 0, s>>>(m->wb, A, m->B);
-    envelope_kernel<<<I, 64, 0, s>>>(m->iptr, m->iadv, m->ibid, m->w, m->env_u, m->env_v, m->cut,
-                                     m->hull_h);
+    if (m->maxdeg + 1 <= 16)
+        envelope_seg_kernel<16><<<(I + 3) / 4, 64, 0, s>>>(m->iptr, m->iadv, m->ibid, m->w, I, m->env_u,
+                                                         m->env_v, m->cut, m->hull_h);
+    else if (m->maxdeg + 1 <= 32)
+        envelope_seg_kernel<32><<<(I + 1) / 2, 64, 0, s>>>(m->iptr, m->iadv, m->ibid, m->w, I, m->env_u,
+                                                         m->env_v, m->cut, m->hull_h);
+    else
+        envelope_kernel<<<I, 64, 0, s>>>(m->iptr, m->iadv, m->ibid, m->w, m->env_u, m->env_v, m->cut,
+                                         m->hull_h);
     region_count_kernel<<<(I + tb - 1) / tb, tb, 0, s>>>(m->hull_h, I, m->rcnt);
     size_t bytes = m->cub_bytes;
     MW_TRY(hipcub::DeviceScan::ExclusiveSum(m->cub_tmp, bytes, m->rcnt, m->roff, I, s));
@@ -1083,7 +1288,8 @@ int mw_iteration(dlp_mw* m, dlp_mw_iter* dlog_entry) {
     advertiser_kernel<<<(A + tb - 1) / tb, tb, 0, s>>>(m->aptr, m->apos, m->abid, m->budgets, m->x, A,
                                                        fa, fb, m->width, m->lp, m->lm, m->slack,
                                                        m->avg_slack, m->w);
-    report_kernel<<<1, 64, 0, s>>>(m->avg_slack, m->budgets, m->w, A, m->dual, m->B, m->bst, dlog_entry);
+    report_kernel<<<m->report_blocks, 256, 0, s>>>(m->avg_slack, m->budgets, m->w, A, m->dual, m->B, m->bst,
+                                                   m->rpart, m->rticket, dlog_entry);
     MW_TRY(hipGetLastError());
     m->t = t;
     return DLP_OK;

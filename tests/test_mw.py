@@ -214,6 +214,16 @@ def test_mw_gpu_binary_bit_identical_to_spec(A, I, sp, T):
 
 
 @pytest.mark.gpu
+def test_mw_gpu_binary_uncached_and_multi_round_bit_identical_to_spec(monkeypatch):
+    """One workgroup, regions read from HBM each level (LDS cache off); and
+    1024 < I <= 16384, where each 256-lane group walks several spec blocks."""
+    monkeypatch.setenv("DLP_MW_NO_LDS_CACHE", "1")
+    _gpu_vs_spec_binary(1000, 1000, 0.1, 20)
+    monkeypatch.delenv("DLP_MW_NO_LDS_CACHE")
+    _gpu_vs_spec_binary(100, 5000, 0.02, 15)
+
+
+@pytest.mark.gpu
 def test_mw_gpu_binary_multi_launch_bit_identical_to_spec():
     """I > 16384: one launch per search level, last-block reduction + control."""
     _gpu_vs_spec_binary(300, 40000, 0.004, 12)

@@ -110,27 +110,6 @@ out["f1_adalloc_1000x1000"] = dict(m=p.m, n=p.n, pivots=res.num_pivots, gpu_s=t_
                                    objective=res.objective, status=res.status,
                                    reference_mw_300_iterations_s="8.27 (BASELINE.md, 1 core, build container)",
                                    reference_mw_final_dual_value=125.37)
-# f3: the reference's MW loop (R/main.cpp:19-64 default scenario, 300 iterations) in the mode
-# main() runs (binary search) and in sort mode; then the reference's commented-out large
-# scenario shape (100k x 1M x 1e-4) for a few iterations
-for binary in (True, False):
-    mw = dlp.MW(p, binary=binary)
-    (log, ms), t = timed(lambda: mw.run(300))
-    mw.close()
-    out["f3_mw_1000x1000x300_" + ("binary" if binary else "sort")] = dict(
-        wall_s=t, kernel_ms=ms, final_dual=float(log["dual_value"][-1]),
-        mean_search_levels=float(log["search_levels"].mean()),
-        reference_s="8.27 (binary, BASELINE.md, 1 core, build container)")
-pl = dlp.Problem.adalloc(100000, 1000000, 1, 1e-4, 0.25)
-for binary in (True, False):
-    mw = dlp.MW(pl, binary=binary)
-    mw.run(1)
-    (log, ms), t = timed(lambda: mw.run(5))
-    mw.close()
-    out["f3_mw_100kx1Mx1e-4_5it_" + ("binary" if binary else "sort")] = dict(
-        wall_s=t, kernel_ms=ms, ms_per_iteration=t * 1e3 / 5,
-        mean_search_levels=float(log["search_levels"].mean()),
-        final_dual=float(log["dual_value"][-1]))
 print(json.dumps(out, indent=1))
 if a.out:
     json.dump(out, open(a.out, "w"), indent=1)
