@@ -49,8 +49,8 @@ __global__ __launch_bounds__(kUpdThreads) void price_init_kernel(const double* _
 // tile partials (<= a few KB, L2-resident) so no extra launch is needed; then
 // one lane per local row (objective row included for colq) reads T[i][q] and
 // T[i][N] (two strided 8-B loads), captures colq[i], and forms the ratio
-// candidate.  The last workgroup to arrive (agent-scope release/acquire
-// ticket, cdna_hip_programming.md Guideline 16) reduces the per-WG partials.
+// candidate.  The last workgroup to arrive (ticket; sc1 hand-off, no fences)
+// reduces the per-WG partials.
 // Nearest reference analog: the tolerance-gated tight-set test
 // R/global_problem.cpp:372-380 and first-wins scans :335-361.
 __global__ __launch_bounds__(kRatioThreads) void ratio_kernel(
@@ -99,10 +99,18 @@ __global__ __launch_bounds__(kRatioThreads) void ratio_kernel(
     }
     c = block_cand(c, lds_c);
 
-    // ---- last-arriving workgroup reduces the partials
+    // ---- last-arriving workgroup reduces the partials.  No fences (an agent
+    // release is an L2 write-back per workgroup on gfx950): write-through (sc1)
+    // stores drained by vmcnt(0) before the ticket add, sc1 loads after it.
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    constexpr int kAuxSc1 = 16;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)partials, (short)0, (int)(gridDim.x * sizeof(Cand)), 0x00020000);
     if (threadIdx.x == 0) {
-        partials[blockIdx.x] = c;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const u4v* cv = (const u4v*)&c;
+        __builtin_amdgcn_raw_buffer_store_b128(cv[0], prs, (int)(blockIdx.x * sizeof(Cand)), 0, kAuxSc1);
+        __builtin_amdgcn_raw_buffer_store_b128(cv[1], prs, (int)(blockIdx.x * sizeof(Cand)) + 16, 0,
+                                               kAuxSc1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev =
             __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -110,14 +118,12 @@ __global__ __launch_bounds__(kRatioThreads) void ratio_kernel(
     }
     __syncthreads();
     if (!s_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
     Cand best = cand_empty();
     for (int k = threadIdx.x; k < (int)gridDim.x; k += blockDim.x) {
-        const Cand o = partials[k];
+        Cand o;
+        u4v* ov = (u4v*)&o;
+        ov[0] = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(k * sizeof(Cand)), 0, kAuxSc1);
+        ov[1] = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(k * sizeof(Cand)) + 16, 0, kAuxSc1);
         if (cand_better(o, best)) best = o;
     }
     best = block_cand(best, lds_c);

@@ -21,3 +21,15 @@ def test_cpu_baseline_small():
 def test_committed_traffic_unknown_geometry():
     val, src = bench.committed_traffic({"workload": "none", "kernel": "pass", "K": -1})
     assert val is None and src is None
+
+
+def test_committed_traffic_for_the_default_bench_geometry():
+    """The default bench (C3, K = 32, form 4) finds its committed PMC summary, and
+    profiles/ travels to the GPU box (bench.py reads it there)."""
+    geo = {"workload": "c3", "kernel": "pass", "K": 32, "form": 4, "rows_per_block": 256,
+           "nontemporal": 1, "ld": 66048, "rows_local": 32768}
+    val, src = bench.committed_traffic(geo)
+    assert val and 3.0e10 < val < 4.5e10 and src.startswith("profiles/")
+    with open(os.path.join(ROOT, ".gpurunignore")) as f:
+        pats = [line.strip() for line in f if line.strip()]
+    assert not any(p.strip("./").startswith("profiles") for p in pats)
