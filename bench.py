@@ -74,6 +74,8 @@ def parse():
                     help="pivots per tableau pass (1 = eager rank-1 per pivot, 0 = auto)")
     ap.add_argument("--occupancy", type=int, default=-1, help="pass workgroups/CU cap (-1 = default)")
     ap.add_argument("--form", type=int, default=-1, help="pass kernel form (-1 = default)")
+    ap.add_argument("--lookahead", type=int, default=-1,
+                    help="select block b+1 during the pass of block b: 1 on, 0 off, -1 auto")
     ap.add_argument("--pmc-dir", default=None,
                     help="rocprofv3 --pmc output dir (FETCH_SIZE / WRITE_SIZE) to fill roofline.traffic")
     return ap.parse_args()
@@ -205,11 +207,12 @@ def main():
                        nontemporal=args.nontemporal, update_variant=args.variant,
                        ld_align=args.ld_align, rows_per_block=args.rows_per_block,
                        max_pivots=64 * (args.warmup + args.steps) + args.steps + 2, log_pivots=1,
-                       defer=args.defer)
+                       defer=args.defer, lookahead=args.lookahead)
     if args.occupancy >= 0 or args.form >= 0:
         if sess.update_stats()[2] > 1:
             sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 0, args.form)
     K = sess.update_stats()[2]
+    lookahead_on = sess.lookahead()
     per_step = K if args.step_unit == "block" else 1
     warm, timed = args.warmup * per_step, args.steps * per_step
 
@@ -298,7 +301,8 @@ def main():
                        "rows_per_rank": rows_local, "parallelism": f"rowblock{world}",
                        "pricing": "dantzig->bland on degeneracy", "pivots_per_tableau_pass": K,
                        "step": (f"{per_step} pivots + their rank-{K} tableau pass" if per_step > 1
-                                else "one pivot")},
+                                else "one pivot"),
+                       "lookahead": lookahead_on},
             "pivots_timed": timed,
             "pivots_per_step": per_step,
             "K": K,

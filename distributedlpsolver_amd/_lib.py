@@ -52,6 +52,8 @@ class Options(C.Structure):
         ("tol_feas", C.c_double),
         ("defer", C.c_int32),
         ("n_gpus", C.c_int32),
+        ("lookahead", C.c_int32),
+        ("pad_", C.c_int32),
     ]
 
 
@@ -143,6 +145,7 @@ SIGNATURES = [
     ("dlp_session_update_stats", C.c_int, [_P, C.POINTER(_I64), _DP, C.POINTER(C.c_int)]),
     ("dlp_session_set_defer_tuning", C.c_int, [_P, C.c_int, C.c_int]),
     ("dlp_session_set_fused_pivot", C.c_int, [_P, C.c_int]),
+    ("dlp_session_get_lookahead", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("dlp_session_get_defer_tuning", C.c_int,
      [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dlp_session_set_tuning", C.c_int, [_P, C.c_int, C.c_int, C.c_int]),

@@ -95,7 +95,8 @@ __device__ __forceinline__ void ratio_defer_body(
     DevState* st, double* __restrict__ C, int64_t ldc, double* __restrict__ Cc, int64_t ldcc,
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
-    dlp_pivot* log, int64_t log_cap, int nblocks) {
+    dlp_pivot* log, int64_t log_cap, int nblocks, const double* __restrict__ Ccp = nullptr,
+    const double* __restrict__ Pp = nullptr, int prev_seal = -1) {
     __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
     __shared__ Cand lds_c[kRatioDeferThreads / 64];
     __shared__ int s_last;
@@ -103,21 +104,26 @@ __device__ __forceinline__ void ratio_defer_body(
     __shared__ int32_t s_pl[KMAX];
     if (st->status != DLP_RUNNING) return;
 
+    // replayed steps: the sealed previous block (lookahead: not yet applied to T, its kp
+    // steps first), then this block's j steps; C / Cc / nzc are written at index j
     const int j = st->blk;
+    const int kp = prev_seal >= 0 ? st->seal[prev_seal].blk : 0;
+    const int J = kp + j;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (int l = threadIdx.x; l < j; l += blockDim.x) {
-        s_pn[l] = P[(int64_t)l * ld + ncols];
-        s_pl[l] = st->pl[l];
+    for (int l = threadIdx.x; l < J; l += blockDim.x) {
+        s_pn[l] = l < kp ? Pp[(int64_t)l * ld + ncols] : P[(int64_t)(l - kp) * ld + ncols];
+        s_pl[l] = l < kp ? st->seal[prev_seal].pl[l] : st->pl[l - kp];
     }
     const int64_t ic = i < rows ? i : rows;   // clamped: loads need no guard
     double f[KMAX];
 #pragma unroll
-    for (int l = 0; l < KMAX; ++l) f[l] = (l < j) ? Cc[(int64_t)l * ldcc + ic] : 0.0;
+    for (int l = 0; l < KMAX; ++l)
+        f[l] = (l < J) ? (l < kp ? Ccp[(int64_t)l * ldcc + ic] : Cc[(int64_t)(l - kp) * ldcc + ic]) : 0.0;
     double r_in = 0.0;
     int32_t nz_in = 0, bvar = 0;
     if (i < rows && j > 0) nz_in = nzc[i];
     if (i < rows_elig) {
-        r_in = j == 0 ? T[i * ld + ncols] : rhs[i];
+        r_in = J == 0 ? T[i * ld + ncols] : rhs[i];
         bvar = basis[row_first + i];
     }
 
@@ -138,7 +144,8 @@ __device__ __forceinline__ void ratio_defer_body(
         return;
     }
 
-    for (int l = threadIdx.x; l < j; l += blockDim.x) s_pq[l] = P[(int64_t)l * ld + q];
+    for (int l = threadIdx.x; l < J; l += blockDim.x)
+        s_pq[l] = l < kp ? Pp[(int64_t)l * ld + q] : P[(int64_t)(l - kp) * ld + q];
     __syncthreads();
 
     Cand c = cand_empty();
@@ -147,7 +154,7 @@ __device__ __forceinline__ void ratio_defer_body(
         if (i < rows) {
 #pragma unroll
             for (int l = 0; l < KMAX; ++l) {
-                if (l < j) {
+                if (l < J) {
                     if (i == s_pl[l])
                         a = s_pq[l];
                     else if (f[l] != 0.0)
@@ -160,8 +167,8 @@ __device__ __forceinline__ void ratio_defer_body(
         if (i < rows) nzc[i] = (j == 0 ? 0 : nz_in) + (a != 0.0 ? 1 : 0);   // the pass's row class
         if (i < rows_elig) {
             double r = r_in;
-            if (j > 0) {
-                const int l = j - 1;
+            if (J > 0) {
+                const int l = J - 1;
                 double fp = 0.0;   // f[j-1], selected without dynamic register indexing
 #pragma unroll
                 for (int u = 0; u < KMAX; ++u) fp = (u == l) ? f[u] : fp;
@@ -228,10 +235,11 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     DevState* st, double* __restrict__ C, int64_t ldc, double* __restrict__ Cc, int64_t ldcc,
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
-    dlp_pivot* log, int64_t log_cap) {
+    dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
+    int prev_seal) {
     ratio_defer_body<KMAX, false>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                   ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
-                                  tol_piv, pricing, log, log_cap, (int)gridDim.x);
+                                  tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal);
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
@@ -272,17 +280,20 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
     int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
-    int fused) {
+    int fused, const double* __restrict__ Cp, const double* __restrict__ Pp, int prev_seal) {
     __shared__ PricePart lds_pp[4];
     __shared__ double s_cp[kMaxDefer];
     __shared__ int32_t s_pl[kMaxDefer];
     if (st->status != DLP_RUNNING) return;
     const int s = st->blk - 1;
+    // replayed steps: the sealed previous block first (lookahead), then this block's s
+    const int kp = prev_seal >= 0 ? st->seal[prev_seal].blk : 0;
+    const int S = kp + s;
     const int32_t pl = st->p_local;
     if (pl >= 0)
-        for (int l = threadIdx.x; l < s; l += blockDim.x) {
-            s_cp[l] = C[(int64_t)pl * ldc + l];
-            s_pl[l] = st->pl[l];
+        for (int l = threadIdx.x; l < S; l += blockDim.x) {
+            s_cp[l] = l < kp ? Cp[(int64_t)pl * ldc + l] : C[(int64_t)pl * ldc + (l - kp)];
+            s_pl[l] = l < kp ? st->seal[prev_seal].pl[l] : st->pl[l - kp];
         }
     __syncthreads();
     const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
@@ -292,14 +303,17 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     if (pl >= 0 && j < ld) {
         d2 t = *(const d2*)(T + (int64_t)pl * ld + j);
         // chunks of 8 pivot rows: loads issued back to back (row index clamped), then applied in order
-        for (int l0 = 0; l0 < s; l0 += 8) {
+        for (int l0 = 0; l0 < S; l0 += 8) {
             d2 pv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) pv[u] = *(const d2*)(P + (int64_t)min(l0 + u, s - 1) * ld + j);
+            for (int u = 0; u < 8; ++u) {
+                const int l = min(l0 + u, S - 1);
+                pv[u] = *(const d2*)((l < kp ? Pp + (int64_t)l * ld : P + (int64_t)(l - kp) * ld) + j);
+            }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int l = l0 + u;
-                if (l < s) {
+                if (l < S) {
                     if (pl == s_pl[l]) {
                         t = pv[u];
                     } else if (s_cp[l] != 0.0) {
@@ -684,18 +698,24 @@ __device__ inline void strow(double* p, const double (&t)[V]) {
 // address space, wave-uniform loads of them are always scalar loads.
 typedef __attribute__((address_space(4))) const double* cdptr;
 
+// T: the tableau read; Tout: where the rows go (== T in place; lookahead: the other
+// buffer, so untouched rows are copied and an empty block copies everything); bd: the
+// block (DevState::blk / pl, or a sealed copy).
 template <bool NT, int K, int V, int U, bool PART, bool DEEP = false>
-__device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, int64_t rows,
-                                            int64_t width, const DevState* __restrict__ st,
+__device__ __forceinline__ void pass_s_body(const double* __restrict__ T, double* __restrict__ Tout,
+                                            int64_t ld, int64_t rows, int64_t width,
+                                            const BlockDesc* __restrict__ bd,
                                             const double* __restrict__ C, int64_t ldc,
                                             const double* __restrict__ P,
                                             const int32_t* __restrict__ nzc, int rb) {
     __shared__ int32_t cls[1024];
-    const int kb = st->blk;
+    const int kb = bd->blk;
+    const bool outplace = Tout != T;
     // two launches per pass: the full-block instance (kb == K) and the partial one
-    // (0 < kb < K: a window's last block, or one cut short by termination), so that
-    // neither carries the other's register pressure; exactly one of them runs
-    if (kb == 0 || (PART ? kb == K : kb != K)) return;
+    // (0 < kb < K: a window's last block, or one cut short by termination; kb == 0 out of
+    // place: a copy), so that neither carries the other's register pressure; exactly one
+    // of them runs
+    if ((kb == 0 && !outplace) || (PART ? kb == K : kb != K)) return;
     const int64_t j = (int64_t)blockIdx.x * (256 * V) + threadIdx.x * V;
     const bool colok = j < width;
     const int64_t jc = colok ? j : width - V;
@@ -715,7 +735,7 @@ __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, 
         const int nz = nzc[i0 + r];
         int last = -1;
         for (int l = 0; l < kb; ++l)
-            if (st->pl[l] == (int32_t)(i0 + r)) last = l;
+            if (bd->pl[l] == (int32_t)(i0 + r)) last = l;
         cls[r] = last >= 0 ? last : (nz == kb ? kDense : (nz == 0 ? kUntouched : kSparse));
     }
     __syncthreads();
@@ -791,7 +811,7 @@ __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, 
         }
         if (colok)
 #pragma unroll
-            for (int u = 0; u < U; ++u) strow<NT, V>(T + (i0 + r0 + u) * ld + j, t[u]);
+            for (int u = 0; u < U; ++u) strow<NT, V>(Tout + (i0 + r0 + u) * ld + j, t[u]);
     };
     auto load = [&](double (&t)[U][V], int r0) {
 #pragma unroll
@@ -856,8 +876,12 @@ __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, 
         // runtime loop over the steps with P[l] re-read from L2, so that the unrolled
         // register copy serves only the dense path
         const int c = cls[r];
-        if (c != kUntouched) {
-            double* row = T + (i0 + r) * ld;
+        if (c == kUntouched && outplace) {
+            double t[V];
+            ldrow<NT, V>(t, T + (i0 + r) * ld + jc);
+            if (colok) strow<NT, V>(Tout + (i0 + r) * ld + j, t);
+        } else if (c != kUntouched) {
+            const double* row = T + (i0 + r) * ld;
             const double* cr = C + (i0 + r) * ldc;
             double t[V];
             int l = 0;
@@ -876,30 +900,30 @@ __device__ __forceinline__ void pass_s_body(double* __restrict__ T, int64_t ld, 
                     for (int e = 0; e < V; ++e) t[e] = __builtin_fma(-f, pv[e], t[e]);
                 }
             }
-            if (colok) strow<NT, V>(row + j, t);
+            if (colok) strow<NT, V>(Tout + (i0 + r) * ld + j, t);
         }
         r += 1;
     }
 }
 
 template <bool NT, int K, int V, int U, bool PART, bool DEEP = false>
-__global__ __launch_bounds__(256) void pass_s_kernel(double* __restrict__ T, int64_t ld,
-                                                     int64_t rows, int64_t width,
-                                                     const DevState* __restrict__ st,
+__global__ __launch_bounds__(256) void pass_s_kernel(const double* __restrict__ T, double* __restrict__ Tout,
+                                                     int64_t ld, int64_t rows, int64_t width,
+                                                     const BlockDesc* __restrict__ bd,
                                                      const double* __restrict__ C, int64_t ldc,
                                                      const double* __restrict__ P,
                                                      const int32_t* __restrict__ nzc, int rb) {
-    pass_s_body<NT, K, V, U, PART, DEEP>(T, ld, rows, width, st, C, ldc, P, nzc, rb);
+    pass_s_body<NT, K, V, U, PART, DEEP>(T, Tout, ld, rows, width, bd, C, ldc, P, nzc, rb);
 }
 
 // The same body held to 3 waves per SIMD (<= 168 VGPRs; form 4 alone takes 170, which
 // allocates 176 and leaves 2 waves per SIMD).
 template <bool NT, int K, int V, int U, bool PART>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void pass_s3_kernel(
-    double* __restrict__ T, int64_t ld, int64_t rows, int64_t width, const DevState* __restrict__ st,
-    const double* __restrict__ C, int64_t ldc, const double* __restrict__ P,
-    const int32_t* __restrict__ nzc, int rb) {
-    pass_s_body<NT, K, V, U, PART>(T, ld, rows, width, st, C, ldc, P, nzc, rb);
+    const double* __restrict__ T, double* __restrict__ Tout, int64_t ld, int64_t rows, int64_t width,
+    const BlockDesc* __restrict__ bd, const double* __restrict__ C, int64_t ldc,
+    const double* __restrict__ P, const int32_t* __restrict__ nzc, int rb) {
+    pass_s_body<NT, K, V, U, PART>(T, Tout, ld, rows, width, bd, C, ldc, P, nzc, rb);
 }
 
 // Streamed form of the pass (forms 6-9): pass_s_body's per-element operations,
@@ -1196,6 +1220,18 @@ __global__ void blk_reset_kernel(DevState* st) {
     if (threadIdx.x == 0) st->blk = 0;
 }
 
+// Lookahead: the block just selected becomes st->seal[slot] (read by its pass and
+// replayed by the next block's selections); the next block starts empty.
+__global__ __launch_bounds__(64) void seal_kernel(DevState* st, int slot) {
+    const int kb = st->blk;
+    for (int l = threadIdx.x; l < kMaxDefer; l += 64) st->seal[slot].pl[l] = l < kb ? st->pl[l] : -1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st->seal[slot].blk = kb;
+        st->blk = 0;
+    }
+}
+
 }  // namespace
 
 int ratio_defer_blocks(const Geometry& g) {
@@ -1205,20 +1241,25 @@ int ratio_defer_blocks(const Geometry& g) {
 hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               const PricePart* pp, DevState* st, Cand* partials, int nblocks,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
-                              int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+                              int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
+                              const Defer* prev, int prev_seal) {
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
     nblocks = ratio_defer_blocks(g);
+    if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxDefer)) return hipErrorInvalidValue;
+    const double* Ccp = prev_seal >= 0 ? prev->Cc : nullptr;
+    const double* Pp = prev_seal >= 0 ? prev->P : nullptr;
+    const int steps = prev_seal >= 0 ? 2 * d.K : d.K;   // at most kp + j replayed steps
 #define DLP_RATIO_DEFER(KM)                                                                      \
     ratio_defer_kernel<KM><<<nblocks, kRatioDeferThreads, 0, s>>>(                               \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, \
         d.Cc, d.ldcc, d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing,   \
-        log, log_cap)
-    if (d.K <= 8)
+        log, log_cap, Ccp, Pp, prev_seal)
+    if (steps <= 8)
         DLP_RATIO_DEFER(8);
-    else if (d.K <= 16)
+    else if (steps <= 16)
         DLP_RATIO_DEFER(16);
-    else if (d.K <= 32)
+    else if (steps <= 32)
         DLP_RATIO_DEFER(32);
     else
         DLP_RATIO_DEFER(64);
@@ -1258,11 +1299,14 @@ int fused_pivot_blocks(const Geometry& g) {
 
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
-                             int64_t log_cap, int nranks, hipStream_t s) {
+                             int64_t log_cap, int nranks, hipStream_t s, const Defer* prev,
+                             int prev_seal) {
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
+    if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxDefer)) return hipErrorInvalidValue;
     prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
                                              d.P, prow_bits, pp, tol_dj, log, log_cap,
-                                             nranks == 1 ? 1 : 0);
+                                             nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
+                                             prev_seal >= 0 ? prev->P : nullptr, prev_seal);
     return hipGetLastError();
 }
 
@@ -1291,7 +1335,11 @@ static void launch_pass_r(const Geometry& g, const Defer& d, DevState* st, int r
 
 template <bool NT, int K>
 static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
-                       hipStream_t s) {
+                       hipStream_t s, double* Tout, int seal) {
+    // lookahead: out of place, the sealed block; pass_s forms only (lookahead_form)
+    if (seal >= 0 && !lookahead_form(d.form)) return hipErrorInvalidValue;
+    const BlockDesc* bd = seal >= 0 ? &st->seal[seal] : (const BlockDesc*)&st->blk;
+    double* To = Tout ? Tout : g.T;
     if (d.form >= 6 && d.form <= 19 && d.form != 14 && d.form != 15 &&
         (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31)) {
         // streamed forms (K >= 16, a band within one 2 GiB buffer descriptor; else form 3)
@@ -1347,26 +1395,26 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             else
                 return hipErrorInvalidValue;
         } else if (form == 3) {
-            pass_s_kernel<NT, K, 1, 4, false><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
+            pass_s_kernel<NT, K, 1, 4, false><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
                                                                      d.C, d.ldc, d.P, d.nzc, rb);
-            pass_s_kernel<NT, K, 1, 4, true><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
+            pass_s_kernel<NT, K, 1, 4, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
                                                                     d.C, d.ldc, d.P, d.nzc, rb);
         } else if (form == 20) {
             if constexpr (K <= 32) {
                 pass_s_kernel<NT, K, 2, 2, false, true><<<grid, 256, dyn, s>>>(
-                    g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                    g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
                 pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
-                    g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                    g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
             } else
                 return hipErrorInvalidValue;
         } else if (form == 4 || form == 14 || form == 15) {
             if constexpr (K <= 32) {
                 if (form == 15)
                     pass_s3_kernel<NT, K, 2, 2, false><<<grid, 256, dyn, s>>>(
-                        g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
                 else
                     pass_s_kernel<NT, K, 2, 2, false><<<grid, 256, dyn, s>>>(
-                        g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
                 if (form >= 14 && K >= 16 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31)) {
                     // partial block through the streamed kernel's partial instance
                     const int nb = (int)bands;
@@ -1375,14 +1423,14 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
                             g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb, ntiles, nb, 0);
                 } else {
                     pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
-                        g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb);
+                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
                 }
             } else
                 return hipErrorInvalidValue;
         } else if (form == 5) {
-            pass_s_kernel<NT, K, 1, 8, false><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
+            pass_s_kernel<NT, K, 1, 8, false><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
                                                                      d.C, d.ldc, d.P, d.nzc, rb);
-            pass_s_kernel<NT, K, 1, 8, true><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st,
+            pass_s_kernel<NT, K, 1, 8, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
                                                                     d.C, d.ldc, d.P, d.nzc, rb);
         }
         else if (form == 1)
@@ -1392,26 +1440,35 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             pass1_kernel<NT, K, 4><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st, d.C,
                                                           d.ldc, d.P, rb);
     }
-    blk_reset_kernel<<<1, 64, 0, s>>>(st);
+    if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
     return hipGetLastError();
 }
 
 template <bool NT>
 static hipError_t pass_k(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
-                         hipStream_t s) {
-    if (d.K <= 4) return pass<NT, 4>(g, d, st, rb, occ, s);
-    if (d.K <= 8) return pass<NT, 8>(g, d, st, rb, occ, s);
-    if (d.K <= 16) return pass<NT, 16>(g, d, st, rb, occ, s);
-    if (d.K <= 32) return pass<NT, 32>(g, d, st, rb, occ, s);
-    return pass<NT, 64>(g, d, st, rb, occ, s);
+                         hipStream_t s, double* Tout, int seal) {
+    if (d.K <= 4) return pass<NT, 4>(g, d, st, rb, occ, s, Tout, seal);
+    if (d.K <= 8) return pass<NT, 8>(g, d, st, rb, occ, s, Tout, seal);
+    if (d.K <= 16) return pass<NT, 16>(g, d, st, rb, occ, s, Tout, seal);
+    if (d.K <= 32) return pass<NT, 32>(g, d, st, rb, occ, s, Tout, seal);
+    return pass<NT, 64>(g, d, st, rb, occ, s, Tout, seal);
 }
 
+bool lookahead_form(int form) { return form == 3 || form == 4 || form == 5 || form == 20; }
+
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
-                              int rows_per_block, int occupancy, hipStream_t s) {
-    if (d.K < 1 || d.K > kMaxDefer || rows_per_block < 1 || rows_per_block > 1024)
+                              int rows_per_block, int occupancy, hipStream_t s, double* Tout,
+                              int seal) {
+    if (d.K < 1 || d.K > kMaxDefer || rows_per_block < 1 || rows_per_block > 1024 || seal > 1)
         return hipErrorInvalidValue;
-    return nontemporal ? pass_k<true>(g, d, st, rows_per_block, occupancy, s)
-                       : pass_k<false>(g, d, st, rows_per_block, occupancy, s);
+    return nontemporal ? pass_k<true>(g, d, st, rows_per_block, occupancy, s, Tout, seal)
+                       : pass_k<false>(g, d, st, rows_per_block, occupancy, s, Tout, seal);
+}
+
+hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s) {
+    if (slot < 0 || slot > 1) return hipErrorInvalidValue;
+    seal_kernel<<<1, 64, 0, s>>>(st, slot);
+    return hipGetLastError();
 }
 
 }  // namespace dlp

@@ -1,6 +1,7 @@
 // dlp_internal.h — types shared by the HIP kernels (dlp_kernels.hip) and the
 // host runtime (dlp_session.cpp).  Not part of the public C ABI.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include <hip/hip_runtime.h>
@@ -63,7 +64,17 @@ struct alignas(16) DevState {
     uint32_t go;       // selection published to the pivot-row blocks
     uint32_t ticket2;  // last pivot-row block re-arms `go`
     uint32_t pad3[30];
+    // lookahead (double-buffered tableau): the two most recent sealed blocks, in the
+    // layout of (blk, pad, pl) above, so a pass reads either through a BlockDesc*
+    struct Seal {
+        int32_t blk;
+        uint32_t pad[2];
+        int32_t pl[kMaxDefer];
+        int32_t pad4;
+    } seal[2];
 };
+// A pass's block: DevState::blk/pl (in-place passes) or a sealed copy (lookahead).
+typedef DevState::Seal BlockDesc;
 
 // Candidate order: valid first, then smaller ratio, then smaller basis index.
 // Total and order-independent, so any reduction tree picks the same winner.
@@ -95,6 +106,9 @@ struct Defer {
                            // scalar-coefficient forms: 3 = 1 double x 4 rows (default; 4 at K = 32 streaming),
                            // 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows
 };
+
+static_assert(offsetof(DevState, pl) - offsetof(DevState, blk) == offsetof(BlockDesc, pl),
+              "BlockDesc must alias DevState::blk / pl");
 
 // Launchers (dlp_kernels.hip).  All asynchronous on `stream`.
 struct Geometry {
@@ -141,10 +155,13 @@ hipError_t launch_carry_in(const Geometry& g, const int64_t* in, DevState* st, i
 hipError_t launch_set_status(DevState* st, int status, hipStream_t s);
 
 // Deferred launchers (dlp_defer.hip).  Pricing tiles are kDeferTile columns.
+// prev / prev_seal (lookahead): the sealed block st->seal[prev_seal] whose arrays are
+// `prev` is not yet applied to g.T; its steps are replayed before the current block's.
 hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               const PricePart* pp, DevState* st, Cand* partials, int nblocks,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
-                              int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s);
+                              int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
+                              const Defer* prev = nullptr, int prev_seal = -1);
 // nranks == 1: ratio test + selection + pivot row + objective row + pricing in ONE launch
 // (K <= 32; grid of fused_pivot_blocks(g), all of which must be resident at once).
 int fused_pivot_blocks(const Geometry& g);
@@ -156,14 +173,22 @@ hipError_t launch_pivot_defer(const Geometry& g, const Defer& d, int32_t* basis,
 // nranks > 1: the owner's replayed pivot-row bits (others INT64_MIN) to prow_bits.
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
-                             int64_t log_cap, int nranks, hipStream_t s);
+                             int64_t log_cap, int nranks, hipStream_t s,
+                             const Defer* prev = nullptr, int prev_seal = -1);
 // nranks > 1, after the MAX all-reduce: P[s] from the exchanged bits + objective row + pricing.
 hipError_t launch_commit_defer(const Geometry& g, const Defer& d, const DevState* st,
                                const int64_t* prow_bits, PricePart* pp, double tol_dj,
                                dlp_pivot* log, int64_t log_cap, hipStream_t s);
 // The tableau pass: applies the block's st->blk steps to rows [0, rows), then blk = 0.
+// Lookahead (seal >= 0): the block st->seal[seal], read from g.T and written to Tout
+// (every row, untouched ones copied; blk is left alone).  Forms 3, 4, 5 and 20 only
+// (lookahead_form).
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
-                              int rows_per_block, int occupancy, hipStream_t s);
+                              int rows_per_block, int occupancy, hipStream_t s,
+                              double* Tout = nullptr, int seal = -1);
+bool lookahead_form(int form);
+// End of a lookahead block: st->seal[slot] := (blk, pl), blk := 0.
+hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s);
 hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits, int nranks,
                        hipStream_t s);
 hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,

@@ -121,6 +121,18 @@ struct dlp_session {
     int defer_rb = 64, defer_occ = 0;   // pass band rows (128 when streaming), WG/CU cap
     std::vector<uint8_t> ev_flush;   // per timed slot: a pass ran in it
     int64_t upd_launches = 0;
+    // lookahead: two tableau buffers; the pass of block b reads Tb[tcur]
+    // and writes the other buffer on pstream while block b+1 is selected on Tb[tread]
+    // (the pass's source) replaying block b's sealed steps first.  dslot: the block
+    // arrays of the two blocks in flight (rhs shared); zbuf: the buffer whose objective
+    // row is current.
+    bool la = false;
+    double* Tb[2] = {nullptr, nullptr};
+    int tread = 0, tcur = 0, zbuf = 0, cur = 0;
+    bool la_pending = false;   // a pass is in flight: Tb[tread] lacks block (1 - cur)
+    dlp::Defer dslot[2];
+    hipStream_t pstream = nullptr;
+    hipEvent_t ev_seal = nullptr, ev_pass = nullptr;
 };
 
 extern "C" int flush_pending(dlp_session* s);   // defined with the C entry points
@@ -209,11 +221,20 @@ void free_session(dlp_session* s) {
     if (s->graph) (void)hipGraphDestroy(s->graph);
     for (auto e : s->ev) (void)hipEventDestroy(e);
     if (s->comm) (void)ncclCommDestroy(s->comm);
-    void* dev[] = {s->T, s->colq, s->prow_send, s->partials, s->cand_send, s->cand_recv,
-                   s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc, s->d.P, s->d.rhs, s->d.nzc,
-                   s->cl_gran};
+    if (s->pstream) (void)hipStreamSynchronize(s->pstream);
+    void* dev[] = {s->Tb[0] ? s->Tb[0] : s->T, s->Tb[1], s->colq, s->prow_send, s->partials,
+                   s->cand_send, s->cand_recv, s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc,
+                   s->d.P, s->d.rhs, s->d.nzc, s->cl_gran};
     for (void* p : dev)
         if (p) (void)hipFree(p);
+    if (s->la || s->dslot[1].C) {   // slot 0 aliases s->d
+        void* sl[] = {s->dslot[1].C, s->dslot[1].Cc, s->dslot[1].P, s->dslot[1].nzc};
+        for (void* p : sl)
+            if (p) (void)hipFree(p);
+    }
+    if (s->ev_seal) (void)hipEventDestroy(s->ev_seal);
+    if (s->ev_pass) (void)hipEventDestroy(s->ev_pass);
+    if (s->pstream) (void)hipStreamDestroy(s->pstream);
     if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
     if (s->host_st) (void)hipHostFree(s->host_st);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -299,7 +320,11 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     }
     if (s->device < 0 || s->device >= ndev) { set_error("device ordinal out of range"); return DLP_ERR_ARG; }
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    // the pivot chain runs at the highest stream priority: under lookahead its small
+    // launches share the device with the pass (pstream, lowest priority)
+    int prio_least = 0, prio_greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_greatest));
 
     const int64_t rows_total = s->rows + 1;
     dlp::Geometry& g = s->g;
@@ -457,6 +482,50 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     HIP_TRY(hipMemcpyAsync(s->st, s->host_st, sizeof(st0), hipMemcpyHostToDevice, s->stream));
     HIP_TRY(dlp::launch_price_init(g, s->pp, opt->tol_dj, opt->update_variant, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    s->Tb[0] = s->T;
+
+    // lookahead: deferred, a pass form with an out-of-place instance, the exchange (if
+    // any) driven by the session, no per-phase timing, and room for a second tableau
+    {
+        const bool host_driven = nranks > 1 && !rccl;
+        bool ok = s->d.K > 1 && 2 * s->d.K <= dlp::kMaxDefer && dlp::lookahead_form(s->d.form) &&
+                  !s->general && !s->cluster && !host_driven && opt->timing < 2;
+        size_t freeb = 0, totalb = 0;
+        if (ok && hipMemGetInfo(&freeb, &totalb) == hipSuccess)
+            ok = freeb > tbytes + tbytes / 8 + ((size_t)1 << 30);
+        else
+            ok = false;
+        // auto: from 4 GiB of tableau, where the pass is several times the pivot chain it
+        // hides (C3 17 GB: 4,492 -> 4,935 pivots/s).  Below that the chain, slowed by
+        // the concurrent pass and by replaying two blocks, costs more than the pass it
+        // hides (C2 268 MB: 39.0k -> 30.2k; profiles/r02h/)
+        const bool want = opt->lookahead == 1 || (opt->lookahead < 0 && tbytes >= ((size_t)4 << 30));
+        if (ok && want) {
+            if (hipMalloc(&s->Tb[1], tbytes) != hipSuccess) {
+                set_error("hipMalloc of the second tableau buffer failed");
+                return DLP_ERR_OOM;
+            }
+            // the whole buffer, padding included, so both hold the same bytes everywhere
+            HIP_TRY(hipMemcpyAsync(s->Tb[1], s->Tb[0], tbytes, hipMemcpyDeviceToDevice, s->stream));
+            s->dslot[0] = s->d;
+            s->dslot[1] = s->d;
+            dlp::Defer& d1 = s->dslot[1];
+            const int64_t kt = s->d.K <= 4 ? 4 : s->d.K <= 8 ? 8 : s->d.K <= 16 ? 16 : s->d.K <= 32 ? 32 : 64;
+            HIP_TRY(hipMalloc(&d1.C, sizeof(double) * s->d.K * (rows_total + 1)));
+            HIP_TRY(hipMalloc(&d1.Cc, sizeof(double) * s->d.K * s->d.ldcc));
+            HIP_TRY(hipMalloc(&d1.P, sizeof(double) * kt * s->ld));
+            HIP_TRY(hipMalloc(&d1.nzc, sizeof(int32_t) * (s->rows + 1)));
+            HIP_TRY(hipMemsetAsync(d1.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
+            HIP_TRY(hipMemsetAsync(d1.Cc, 0, sizeof(double) * s->d.K * s->d.ldcc, s->stream));
+            HIP_TRY(hipMemsetAsync(d1.P, 0, sizeof(double) * kt * s->ld, s->stream));
+            HIP_TRY(hipStreamCreateWithPriority(&s->pstream, hipStreamNonBlocking, prio_least));
+            HIP_TRY(hipEventCreateWithFlags(&s->ev_seal, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s->ev_pass, hipEventDisableTiming));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            s->la = true;
+        }
+        s->opt.lookahead = s->la ? 1 : 0;
+    }
 
     if (comm_in) {
         s->comm = comm_in;
@@ -514,6 +583,70 @@ int enqueue_flush(dlp_session* s) {
     return DLP_OK;
 }
 
+// ---- lookahead --------------------------------------------
+// The objective row lives in one buffer at a time (the pivot-row kernels update it
+// in place, passes never touch it): move it along when the selections change buffer.
+int la_move_z(dlp_session* s, int to) {
+    if (s->zbuf == to) return DLP_OK;
+    HIP_TRY(hipMemcpyAsync(s->Tb[to] + s->rows * s->ld, s->Tb[s->zbuf] + s->rows * s->ld,
+                           sizeof(double) * s->width, hipMemcpyDeviceToDevice, s->stream));
+    s->zbuf = to;
+    return DLP_OK;
+}
+
+// Wait for the pass in flight; the selections then read its output, current again.
+int la_drain(dlp_session* s) {
+    if (!s->la_pending) return DLP_OK;
+    HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_pass, 0));
+    s->tread = s->tcur;
+    s->la_pending = false;
+    CALL_TRY(la_move_z(s, s->tread));
+    s->T = s->g.T = s->Tb[s->tread];
+    return DLP_OK;
+}
+
+// End of a block: seal it, start its pass (Tb[tcur] -> the other buffer) on pstream
+// behind the seal, and move the selections to the pass's source, which the previous
+// pass (if one is in flight) must have finished writing.  drain: also wait for
+// this pass (a window's end).
+int la_block_end(dlp_session* s, bool drain, hipEvent_t* evp) {
+    HIP_TRY(dlp::launch_seal_defer(s->st, s->cur, s->stream));
+    HIP_TRY(hipEventRecord(s->ev_seal, s->stream));
+    HIP_TRY(hipStreamWaitEvent(s->pstream, s->ev_seal, 0));
+    if (evp) HIP_TRY(hipEventRecord(evp[0], s->pstream));
+    dlp::Geometry gp = s->g;
+    gp.T = s->Tb[s->tcur];
+    HIP_TRY(dlp::launch_flush_defer(gp, s->dslot[s->cur], s->st, s->opt.nontemporal != 0, s->defer_rb,
+                                    s->defer_occ, s->pstream, s->Tb[1 - s->tcur], s->cur));
+    if (evp) HIP_TRY(hipEventRecord(evp[1], s->pstream));
+    if (s->la_pending) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_pass, 0));   // previous pass
+    HIP_TRY(hipEventRecord(s->ev_pass, s->pstream));                            // this pass
+    s->tread = s->tcur;
+    s->tcur = 1 - s->tcur;
+    s->la_pending = true;
+    s->cur = 1 - s->cur;
+    s->since_flush = 0;
+    CALL_TRY(la_move_z(s, s->tread));
+    s->T = s->g.T = s->Tb[s->tread];
+    if (drain) CALL_TRY(la_drain(s));
+    return DLP_OK;
+}
+
+// Back to the single-buffer path (step API, a pass form without an out-of-place
+// instance): finish what is in flight; slot 0's arrays serve the in-place blocks.
+int la_disable(dlp_session* s) {
+    if (!s->la) return DLP_OK;
+    if (s->since_flush > 0) CALL_TRY(la_block_end(s, true, nullptr));
+    CALL_TRY(la_drain(s));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    const int form = s->d.form;
+    s->d = s->dslot[0];
+    s->d.form = form;
+    s->la = false;
+    s->opt.lookahead = 0;
+    return DLP_OK;
+}
+
 // One deferred pivot: replayed ratio test, exchange, replayed pivot row (+
 // objective row and pricing), and the pass when the block is full or `last`.
 int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
@@ -521,16 +654,30 @@ int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
     // timing 2: 5 events per pivot (every phase); timing 1: 2 events around the pass only
     hipEvent_t* ev = s->ev_per_pivot == 5 ? &s->ev[(size_t)slot * 5] : nullptr;
     hipEvent_t* evp = s->ev_per_pivot == 2 ? &s->ev[(size_t)slot * 2] : nullptr;
+    // lookahead: the selections read Tb[tread] and replay the sealed block in flight first
+    dlp::Geometry gsel = s->g;
+    const dlp::Defer* dcur = &s->d;
+    const dlp::Defer* dprev = nullptr;
+    int pseal = -1;
+    if (s->la) {
+        gsel.T = s->Tb[s->tread];
+        dcur = &s->dslot[s->cur];
+        if (s->la_pending) {
+            dprev = &s->dslot[1 - s->cur];
+            pseal = 1 - s->cur;
+        }
+    }
     if (ev) HIP_TRY(hipEventRecord(ev[0], s->stream));
-    if (!s->exchange && s->fuse_pivot && s->fuse_fits && !ev) {
+    if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) {
         // single rank: ratio test, selection and pivot row in one launch
         HIP_TRY(dlp::launch_pivot_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
                                         s->ratio_blocks_max, o.tol_dj, o.tol_piv, o.pricing, s->log,
                                         s->log_cap, s->stream));
     } else {
-    HIP_TRY(dlp::launch_ratio_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
+    HIP_TRY(dlp::launch_ratio_defer(gsel, *dcur, s->basis, s->pp, s->st, s->partials,
                                     s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
-                                    o.tol_piv, o.pricing, s->log, s->log_cap, s->stream));
+                                    o.tol_piv, o.pricing, s->log, s->log_cap, s->stream, dprev,
+                                    pseal));
     if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
     if (s->exchange) {
         NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
@@ -539,21 +686,25 @@ int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
                                    s->log, s->log_cap, s->stream, false, true));
     }
     if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
-    HIP_TRY(dlp::launch_prow_defer(s->g, s->d, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
-                                   s->log_cap, s->exchange ? 2 : 1, s->stream));
+    HIP_TRY(dlp::launch_prow_defer(gsel, *dcur, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
+                                   s->log_cap, s->exchange ? 2 : 1, s->stream, dprev, pseal));
     if (s->exchange) {
         NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
                                s->comm, s->stream));
-        HIP_TRY(dlp::launch_commit_defer(s->g, s->d, s->st, s->prow_recv, s->pp, o.tol_dj, s->log,
+        HIP_TRY(dlp::launch_commit_defer(gsel, *dcur, s->st, s->prow_recv, s->pp, o.tol_dj, s->log,
                                          s->log_cap, s->stream));
     }
     }
     if (ev) HIP_TRY(hipEventRecord(ev[3], s->stream));
     s->since_flush += 1;
     const bool flush = last || s->since_flush >= s->d.K;
-    if (flush && evp) HIP_TRY(hipEventRecord(evp[0], s->stream));
-    if (flush) CALL_TRY(enqueue_flush(s));
-    if (flush && evp) HIP_TRY(hipEventRecord(evp[1], s->stream));
+    if (flush && s->la) {
+        CALL_TRY(la_block_end(s, last, evp));
+    } else {
+        if (flush && evp) HIP_TRY(hipEventRecord(evp[0], s->stream));
+        if (flush) CALL_TRY(enqueue_flush(s));
+        if (flush && evp) HIP_TRY(hipEventRecord(evp[1], s->stream));
+    }
     if (ev) HIP_TRY(hipEventRecord(ev[4], s->stream));
     if (ev || evp) s->ev_flush[slot] = flush ? 1 : 0;
     return DLP_OK;
@@ -1008,6 +1159,7 @@ void dlp_options_default(dlp_options* o) {
     o->ld_align = 0;          // auto
     o->tol_feas = 1e-9;
     o->defer = 0;   // auto
+    o->lookahead = -1;   // auto
 }
 
 const char* dlp_status_string(int st) {
@@ -1332,7 +1484,7 @@ int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
     HIP_TRY(hipSetDevice(s->device));
     const int64_t start = s->npivots;
     int64_t budget = std::min<int64_t>(max_pivots, s->opt.max_pivots - s->launched);
-    const bool graph = s->opt.use_graph && !s->exchange && s->ev_per_pivot == 0;
+    const bool graph = s->opt.use_graph && !s->exchange && s->ev_per_pivot == 0 && !s->la;
     while (s->status == DLP_RUNNING && budget > 0) {
         if (s->drive_next < s->drive.size() || s->carry_pending) {   // Phase I -> II switch
             while (s->drive_next < s->drive.size() && budget > 0) {
@@ -1407,6 +1559,10 @@ int step_update_defer(dlp_session* s) {
 // Before anything reads the tableau: apply the pending steps of a deferred block
 // (the step API leaves a partial block pending when the caller stops).
 int flush_pending(dlp_session* s) {
+    if (s->la) {
+        if (s->since_flush > 0) CALL_TRY(la_block_end(s, true, nullptr));
+        return la_drain(s);
+    }
     if (s->d.K > 1 && s->since_flush > 0) CALL_TRY(enqueue_flush(s));
     return DLP_OK;
 }
@@ -1414,6 +1570,7 @@ int flush_pending(dlp_session* s) {
 int dlp_session_step_candidate(dlp_session* s) {
     if (!s) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
+    CALL_TRY(la_disable(s));   // the step API drives single-buffer blocks
     s->step_void = false;
     // the Phase I -> II switch (drive-out pivots, carried row) runs on the eager
     // kernels in every session, as in dlp_session_run: apply a pending deferred
@@ -1562,9 +1719,19 @@ int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
         return DLP_ERR_ARG;
     }
     s->defer_occ = occupancy;
-    if (form >= 0) s->d.form = form;
+    if (form >= 0 && s->la && !dlp::lookahead_form(form)) CALL_TRY(la_disable(s));
+    if (form >= 0) {
+        s->d.form = form;
+        s->dslot[0].form = s->dslot[1].form = form;
+    }
     if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
     if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
+    return DLP_OK;
+}
+
+int dlp_session_get_lookahead(dlp_session* s, int* on) {
+    if (!s || !on) return DLP_ERR_ARG;
+    *on = s->la ? 1 : 0;
     return DLP_OK;
 }
 

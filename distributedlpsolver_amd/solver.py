@@ -297,6 +297,12 @@ class Session:
         L.check(L.lib().dlp_session_set_fused_pivot(self._h, 1 if on else 0),
                 "dlp_session_set_fused_pivot")
 
+    def lookahead(self) -> bool:
+        """True while block b+1 is selected during the pass of block b (dlp_options.lookahead)."""
+        on = C.c_int()
+        L.check(L.lib().dlp_session_get_lookahead(self._h, C.byref(on)), "dlp_session_get_lookahead")
+        return bool(on.value)
+
     def set_defer_tuning(self, occupancy: int, form: int = -1):
         """Deferred pass: workgroups/CU cap (0 = none) and form (0 wide, 1/2 narrow x 2/4 rows;
         scalar-coefficient 3 = 1 double x 4 rows, 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows)."""

@@ -152,6 +152,11 @@ typedef struct dlp_options {
                                 rank per device (ncclCommInitAll); N = 1 runs that path on
                                 a 1-rank communicator.  Sessions ignore it (one process per
                                 GPU: dlp_session_create_rank). */
+    int32_t lookahead;       /* deferred sessions: select block b+1 while the pass of block b
+                                runs, on a second tableau buffer (results unchanged, bit for
+                                bit; 2x the tableau memory): 1 = on where supported, 0 = off,
+                                -1 = auto (default: tableaus of >= 4 GiB that fit twice) */
+    int32_t pad_;
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
  * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;
@@ -309,6 +314,10 @@ int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
  * Bit-identical either way; timing >= 2 (per-phase events) always uses two
  * launches. */
 int dlp_session_set_fused_pivot(dlp_session* s, int on);
+/* *on = 1 when the session runs lookahead (dlp_options.lookahead): block b+1 selected
+ * while the pass of block b runs on a second tableau buffer.  The step API and pass
+ * forms other than 3, 4, 5 and 20 turn it off for the rest of the session. */
+int dlp_session_get_lookahead(dlp_session* s, int* on);
 /* Current deferred-pass settings (K = 1: form -1). */
 int dlp_session_get_defer_tuning(dlp_session* s, int* occupancy, int* form, int* K);
 int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,

@@ -86,6 +86,7 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K):
         assert K == want_K
         if K == 32:
             assert form == 4 and s.get_tuning()[1] == 256   # the bench's pass
+            assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
         done = 0
         while done < k:
             st, d = s.run(min(ci, k - done))
@@ -132,7 +133,7 @@ def test_c3_bench_window_digest():
     m, n = g["m"], g["n"]
     with dlp.Session(dlp.Problem.random(m, n, g["seed"]), check_interval=64 * 20, timing=1,
                      max_pivots=64 * 25 + 22) as s:
-        assert s.get_defer_tuning()[2] == 32
+        assert s.get_defer_tuning()[2] == 32 and s.lookahead()
         for k in (160, 640, 20):
             st, d = s.run(k)
             assert st == L.RUNNING and d == k
@@ -150,12 +151,14 @@ def test_c3_bench_window_digest():
     assert _sha(res.basis) == g["basis_sha256"]
 
 
-def test_c2_full_solve_digest():
-    """C2 solved to optimality on the GPU (deferred K = 16 auto) equals the
-    oracle's full solve (tests/golden/digests.json): pivot count, log, x, y,
-    basis, objective bits."""
+@pytest.mark.parametrize("lookahead", [-1, 1])
+def test_c2_full_solve_digest(lookahead):
+    """C2 solved to optimality on the GPU (deferred K = 16 auto; and with lookahead
+    forced on, which auto leaves off at 268 MB) equals the oracle's full solve
+    (tests/golden/digests.json): pivot count, log, x, y, basis, objective bits."""
     g = load_golden("digests.json")["c2"]
-    res = dlp.solve(dlp.Problem.random(g["m"], g["n"], g["seed"]), max_pivots=200_000)
+    res = dlp.solve(dlp.Problem.random(g["m"], g["n"], g["seed"]), max_pivots=200_000,
+                    lookahead=lookahead)
     assert res.status == g["status"] == L.OK
     assert res.num_pivots == g["num_pivots"]
     assert _sha(res.pivot_log) == g["log_sha256"]
