@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <utility>
 
 #include "dlp_internal.h"
 
@@ -1216,6 +1217,188 @@ __global__ __launch_bounds__(256) void pass_r_kernel(double* __restrict__ T, int
     }
 }
 
+
+// Form 21: the pass at K = 64 with the coefficients broadcast by DPP.  At 64 steps per
+// element the scalar coefficient path of forms 3-5 stalls: every chunk of 2 rows x 8
+// steps is a scalar load that misses to L2 (~800 cycles under the stream) against ~128
+// cycles of fmas, and a pass took 16 ms where the same chain with no coefficient loads
+// takes 7.1 (tools/passlab.hip, profiles/r02j/).  Here the coefficients travel as
+// ordinary vector loads, well ahead of use: lane n of each 16-lane row loads steps
+// (2n, 2n+1) of a 32-step half of its row's coefficient row with one 16-B load, and
+// v_fmac_f64_dpp ... row_newbcast:n reads lane n's value for the whole row, so the fma
+// takes its coefficient straight from another lane's register (neg modifier: fma(-c, p, t),
+// the eager operation).  1 double x 2 rows per lane, P[0..64) in 128 VGPRs, buffer
+// accesses with one 32-bit column offset per lane: 166 VGPRs, 3 waves per SIMD.
+// Coefficient registers are written only by loads (no VALU write within two
+// instructions of a DPP read: tests/test_isa.py audits the built code object).
+template <int N>
+__device__ __forceinline__ void fmac_bc(double& t, double c, double p) {
+    asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(t)
+        : "v"(c), "v"(p), "n"(N));
+}
+template <int N>
+__device__ __forceinline__ double bc_mov(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + N, 0xf, 0xf, false);
+}
+// step l of both rows: half h = l / 32, (even, odd) register e = l & 1, lane (l & 31) / 2.
+// PART: the coefficients were masked by VALU selects, so the broadcast goes through the
+// compiler's own v_mov_b64_dpp (it places the hazard wait states) instead of the fused form.
+template <bool PART, int L>
+__device__ __forceinline__ void dpp_step(double (&t)[2], const double (&c)[2][2][2], const double (&pr)[64]) {
+    constexpr int h = L / 32, e = L & 1, n = (L & 31) >> 1;
+    if constexpr (PART) {
+        const double f0 = bc_mov<n>(c[0][h][e]), f1 = bc_mov<n>(c[1][h][e]);
+        t[0] = __builtin_fma(-f0, pr[L], t[0]);
+        t[1] = __builtin_fma(-f1, pr[L], t[1]);
+    } else {
+        fmac_bc<n>(t[0], c[0][h][e], pr[L]);
+        fmac_bc<n>(t[1], c[1][h][e], pr[L]);
+    }
+}
+template <bool PART, int L0, int... I>
+__device__ __forceinline__ void dpp_half(double (&t)[2], const double (&c)[2][2][2], const double (&pr)[64],
+                                         std::integer_sequence<int, I...>) {
+    (dpp_step<PART, L0 + I>(t, c, pr), ...);
+}
+
+template <bool NT, bool PART>
+__global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ T, double* __restrict__ Tout,
+                                                     int64_t ld, int64_t rows, int64_t width,
+                                                     const BlockDesc* __restrict__ bd,
+                                                     const double* __restrict__ C, int64_t ldc,
+                                                     const double* __restrict__ P,
+                                                     const int32_t* __restrict__ nzc, int rb) {
+    constexpr int K = 64, U = 2;
+    __shared__ int32_t cls[1024];
+    const int kb = bd->blk;
+    const bool outplace = Tout != T;
+    if ((kb == 0 && !outplace) || (PART ? kb == K : kb != K)) return;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool colok = j < width;
+    const int jc = (int)(colok ? j : width - 1);
+    double pr[K];
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        const double v = P[(int64_t)(l < kb ? l : 0) * ld + jc];
+        pr[l] = l < kb ? v : 0.0;
+    }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+        const int nz = nzc[i0 + r];
+        int last = -1;
+        for (int l = 0; l < kb; ++l)
+            if (bd->pl[l] == (int32_t)(i0 + r)) last = l;
+        cls[r] = last >= 0 ? last : (nz == kb ? kDense : (nz == 0 ? kUntouched : kSparse));
+    }
+    __syncthreads();
+    // band descriptors (the caller keeps rb * ld * 8 < 2^31): rows at soffset r * ld8;
+    // stores of lanes past the width go out of range and are dropped
+    const int ld8 = (int)(ld * 8);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(T + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Tout + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(C + i0 * ldc), (short)0, (int)((int64_t)nr * ldc * 8), 0x00020000);
+    const int voff = jc * 8;
+    const int soff_bad = 0x7fffff00;
+    const int voff_st = colok ? voff : soff_bad;
+    const int n16 = threadIdx.x & 15;
+    const int coff = n16 * 16;
+    auto dense_at = [&](int r0) {
+        if (r0 + U > nr) return false;
+        return cls[r0] == kDense && cls[r0 + 1] == kDense;
+    };
+    double c[U][2][2];   // [row][half][even/odd step]
+    auto loadc = [&](int r0, int h) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rc, coff + h * 256, (r0 + u) * (int)ldc * 8, 0);
+            const d2 v = __builtin_bit_cast(d2, x);
+            c[u][h][0] = v.x;
+            c[u][h][1] = v.y;
+            if constexpr (PART) {   // steps >= kb: +0, so fma(-(+0), +0, t) = t for every t
+                const int s0 = h * 32 + 2 * n16;
+                c[u][h][0] = s0 < kb ? c[u][h][0] : 0.0;
+                c[u][h][1] = s0 + 1 < kb ? c[u][h][1] : 0.0;
+            }
+        }
+    };
+    auto loadt = [&](double (&t)[U], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rt, voff, (r0 + u) * ld8, NT ? 2 : 0);
+            t[u] = __builtin_bit_cast(double, x);
+        }
+    };
+    // one dense group (rows r0, r0+1 in t; their coefficients in c), with the loads of the
+    // next group rn issued in vmcnt order: its rows first, the first half of its
+    // coefficients once this group's first half has run, the second half at the end
+    auto group = [&](double (&t)[U], double (&tn)[U], int r0, int rn) {
+        loadt(tn, rn);
+        __builtin_amdgcn_sched_barrier(0);
+        dpp_half<PART, 0>(t, c, pr, std::make_integer_sequence<int, 32>{});
+        __builtin_amdgcn_sched_barrier(0);
+        loadc(rn, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        dpp_half<PART, 32>(t, c, pr, std::make_integer_sequence<int, 32>{});
+        __builtin_amdgcn_sched_barrier(0);
+        loadc(rn, 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t[u]), ro, voff_st, (r0 + u) * ld8,
+                                                  NT ? 2 : 0);
+    };
+    double ta[U], tb[U];
+    int r = 0;
+    while (r < nr) {
+        if (dense_at(r)) {
+            // a run of dense groups (the next group's loads are clamped to the current
+            // one at the end of a run: harmless re-reads)
+            loadt(ta, r);
+            loadc(r, 0);
+            loadc(r, 1);
+            while (true) {
+                const bool nb = dense_at(r + U);
+                group(ta, tb, r, nb ? r + U : r);
+                r += U;
+                if (!nb) break;
+                const bool na = dense_at(r + U);
+                group(tb, ta, r, na ? r + U : r);
+                r += U;
+                if (!na) break;
+            }
+            continue;
+        }
+        // generic replay, one row (as pass_s_body)
+        const int cl = cls[r];
+        if (cl == kUntouched && outplace) {
+            const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rt, voff, r * ld8, NT ? 2 : 0);
+            __builtin_amdgcn_raw_buffer_store_b64(x, ro, voff_st, r * ld8, NT ? 2 : 0);
+        } else if (cl != kUntouched) {
+            const double* cr = C + (i0 + r) * ldc;
+            double t;
+            int l = 0;
+            if (cl >= 0) {
+                t = P[(int64_t)cl * ld + jc];
+                l = cl + 1;
+            } else {
+                t = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rt, voff, r * ld8, NT ? 2 : 0));
+            }
+            for (; l < kb; ++l) {
+                const double f = cr[l];
+                if (f != 0.0) t = __builtin_fma(-f, P[(int64_t)l * ld + jc], t);
+            }
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t), ro, voff_st, r * ld8, NT ? 2 : 0);
+        }
+        r += 1;
+    }
+}
+
 __global__ void blk_reset_kernel(DevState* st) {
     if (threadIdx.x == 0) st->blk = 0;
 }
@@ -1371,8 +1554,26 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             return hipGetLastError();
         }
     }
+    if (d.form == 21 && K == 64 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31) &&
+        (int64_t)rb * d.ldc * 8 < ((int64_t)1 << 31)) {
+        // DPP-coefficient pass (K = 64 blocks; 1 double per lane: 256-column tiles)
+        if constexpr (K == 64) {
+            size_t dyn = 0;
+            if (occ > 0) dyn = (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t);
+            const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
+            if (g.rows > 0) {
+                pass_d_kernel<NT, false><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
+                                                                d.P, d.nzc, rb);
+                pass_d_kernel<NT, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
+                                                               d.P, d.nzc, rb);
+            }
+            if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
+            return hipGetLastError();
+        }
+    }
     // streamed forms need K >= 16 (an even number of coefficient chunks): form 3 below
-    const int form = (d.form >= 6 && d.form != 14 && d.form != 15 && d.form != 20) ? 3 : d.form;
+    const int form = (d.form >= 6 && d.form != 14 && d.form != 15 && d.form != 20 && d.form != 21) ? 3
+                     : d.form == 21 ? 3 : d.form;
     const int cols = (form == 0 || form == 4 || form >= 14) ? kDeferTile : 256;
     const int ntiles = (int)((g.width + cols - 1) / cols);
     const int64_t bands = (g.rows + rb - 1) / rb;
@@ -1454,7 +1655,7 @@ static hipError_t pass_k(const Geometry& g, const Defer& d, DevState* st, int rb
     return pass<NT, 64>(g, d, st, rb, occ, s, Tout, seal);
 }
 
-bool lookahead_form(int form) { return form == 3 || form == 4 || form == 5 || form == 20; }
+bool lookahead_form(int form) { return form == 3 || form == 4 || form == 5 || form == 20 || form == 21; }
 
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
                               int rows_per_block, int occupancy, hipStream_t s, double* Tout,

@@ -229,3 +229,51 @@ def test_auto_block_size_policy():
         assert s.update_stats()[2] == 1
     with dlp.Session(dlp.Problem.random(2048, 2048, 2)) as s:   # 2049 x 4097 doubles = 67 MB
         assert s.update_stats()[2] == 16
+
+
+@pytest.mark.parametrize("m,n,seed,rb,nt,occ", [(300, 520, 5, 64, 1, 0), (300, 520, 5, 256, 0, 0),
+                                                (700, 1337, 7, 1000, 1, 0), (129, 4000, 2, 37, 1, 2),
+                                                (1200, 700, 9, 128, 1, 3)])
+def test_pass_form21_dpp_full_blocks(m, n, seed, rb, nt, occ):
+    """Form 21 (DPP-broadcast coefficients, K = 64): two full blocks and a partial one
+    (17 steps: the partial instance's masked coefficients), widths that are not a
+    multiple of the 256-column tile, bands from 37 to 1000 rows (the last one short),
+    pivot rows inside the bands; whole tableau byte-equal to the eager session's."""
+    k = 2 * 64 + 17
+    prob = dlp.Problem.random(m, n, seed)
+    with dlp.Session(prob, defer=1, check_interval=k) as e:
+        e.run(k)
+        Te = e.tableau()
+        le = e.result().pivot_log
+    assert len(le) == k
+    with dlp.Session(prob, defer=64, check_interval=64, rows_per_block=rb, nontemporal=nt) as s:
+        s.set_defer_tuning(occ, 21)
+        done = 0
+        while done < k:
+            done += s.run(min(64, k - done))[1]
+        Td = s.tableau()
+        ld = s.result().pivot_log
+    _same_log(ld, le)
+    assert Td.tobytes() == Te.tobytes()
+
+
+@pytest.mark.parametrize("K", [64, 40])
+def test_pass_form21_sparse_and_degenerate(K):
+    """Form 21 on a sparse tableau (ad-allocation LP: untouched / sparse rows through
+    the generic replay) and a degenerate one (Bland), full solves against the oracle;
+    K = 40 runs form 3 (form 21 needs 64-step blocks)."""
+    p = dlp.Problem.adalloc(200, 200, 1, 0.1, 0.25)
+    M, b, c = O.adalloc_lp(200, 200, 0.1, 0.25)
+    ref = O.solve_dense(M, b, c)
+    with dlp.Session(p, defer=K) as s:
+        s.set_defer_tuning(0, 21)
+        s.run(10 ** 6)
+        res = s.result()
+    _check(res, ref)
+    A, b, c = O.gen_dense(128, 128, 3, degenerate=True)
+    ref = O.solve_dense(A, b, c, pricing=0)
+    with dlp.Session(dlp.Problem.dense(A, b, c), defer=K, check_interval=100) as s:
+        s.set_defer_tuning(0, 21)
+        s.run(10 ** 6)
+        res = s.result()
+    _check(res, ref)

@@ -1,0 +1,84 @@
+"""ISA audit of the shipped code object (CPU test, no GPU needed).
+
+The form-21 tableau pass (dlp_defer.hip, pass_d_kernel) issues v_fmac_f64_dpp
+from inline asm, where the compiler's hazard recognizer cannot see it.  gfx9
+requires two wait states between a VALU write of a VGPR and a DPP read of it;
+the kernel is written so that the DPP source (a coefficient register) is only
+ever written by a vector-memory load.  This test disassembles the gfx950 code
+objects bundled in libdlp.so and checks, for every v_fmac_f64_dpp, that no VALU
+instruction writing its DPP source sits within the two preceding wait states
+(straight-line scan; the fused DPP instructions live in unrolled straight-line
+code)."""
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "distributedlpsolver_amd", "libdlp.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _regs(tok):
+    tok = tok.strip().lstrip("-")
+    m = re.match(r"v\[(\d+):(\d+)\]$", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def _disasm():
+    if not os.path.exists(SO) or not os.path.exists(os.path.join(LLVM, "llvm-objdump")):
+        pytest.skip("libdlp.so or llvm-objdump missing")
+    d = tempfile.mkdtemp()
+    try:
+        shutil.copy(SO, os.path.join(d, "libdlp.so"))
+        subprocess.run([os.path.join(LLVM, "llvm-objdump"), "--offloading", "libdlp.so"], cwd=d,
+                       check=True, capture_output=True)
+        out = []
+        for f in sorted(os.listdir(d)):
+            if "amdgcn" in f and "gfx950" in f:
+                r = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950", f], cwd=d,
+                                   check=True, capture_output=True, text=True)
+                out.append(r.stdout)
+        return "\n".join(out)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def test_fused_dpp_fma_has_no_valu_write_hazard():
+    text = _disasm()
+    instrs = []
+    for line in text.splitlines():
+        line = line.split("//")[0].strip()
+        if not line or line.endswith(":") or line.startswith(("Disassembly", ";")) or "file format" in line:
+            continue
+        instrs.append(line)
+    n_dpp = 0
+    for i, ins in enumerate(instrs):
+        op = ins.split()[0]
+        if op != "v_fmac_f64_dpp":
+            continue
+        n_dpp += 1
+        src0 = _regs(ins.split(None, 1)[1].split(",")[1])
+        assert src0, ins
+        waits = 0
+        k = i - 1
+        while k >= 0 and waits < 2:
+            p = instrs[k]
+            pop = p.split()[0]
+            if pop.startswith("s_nop"):
+                waits += int(p.split()[1], 0) + 1
+                k -= 1
+                continue
+            if pop.startswith("v_") and not pop.startswith(("v_readlane", "v_readfirstlane", "v_cmp")):
+                dst = _regs(p.split(None, 1)[1].split(",")[0]) if len(p.split()) > 1 else set()
+                assert not (dst & src0), f"DPP hazard: '{p}' then '{ins}'"
+            waits += 1
+            k -= 1
+    # the form-21 full-block instances (nt and plain): 64 steps x 2 rows x 2 unrolled groups
+    assert n_dpp >= 512, n_dpp

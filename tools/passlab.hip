@@ -1,0 +1,1144 @@
+// passlab.hip — standalone experiments on the deferred rank-K tableau pass
+// (DESIGN.md §11), outside the session machinery: one tableau in HBM, one
+// block of K dense steps (every row touched by every step), and variants of
+// the per-element chain  t = fma(-C[i][l], P[l][j], t), l = 0..K-1.
+//
+//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/bin/passlab tools/passlab.hip
+//   run:   tools/bin/passlab [rows] [cols] [reps]      (defaults: C3, 32768 x 65537)
+//
+// Every variant is checked bit for bit against a one-thread-per-element
+// reference kernel on a small tableau before the timed runs.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                   \
+        }                                                                              \
+    } while (0)
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const double* cdptr;
+
+__device__ inline double hrand(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return (double)(x >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+}
+
+__global__ void fill_kernel(double* a, int64_t n, uint64_t seed) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        a[i] = hrand(seed * 0x100000001B3ull + (uint64_t)i);
+}
+
+// reference: one thread per element
+__global__ void ref_kernel(const double* T, double* To, int64_t ld, int64_t rows, int64_t width, int K,
+                           const double* Cr, const double* P) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = blockIdx.y;
+    if (j >= width || i >= rows) return;
+    double t = T[i * ld + j];
+    for (int l = 0; l < K; ++l) t = __builtin_fma(-Cr[i * K + l], P[(int64_t)l * ld + j], t);
+    To[i * ld + j] = t;
+}
+
+template <bool NT>
+__device__ inline d2 ldv(const double* p) {
+    if constexpr (NT) return __builtin_nontemporal_load((const d2*)p);
+    else return *(const d2*)p;
+}
+template <bool NT>
+__device__ inline void stv(double* p, d2 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, (d2*)p);
+    else *(d2*)p = v;
+}
+
+__device__ inline double rl(double v, int lane) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// MODE 0: form 4 (coefficients by scalar loads, chunks of LC steps x U rows, double
+//         buffered); 1: coefficients = kernel argument (no memory; wrong values, timing
+//         only); 2: copy (no fma); 3: coefficients by ONE vector load per group (lane =
+//         (row, step)) prefetched with the rows, moved to SGPRs with v_readlane.
+// Workgroup = 256 lanes x V doubles of columns, band of rb rows; P[0..K)[V] in VGPRs.
+template <bool NT, int K, int V, int U, int MODE>
+__global__ __launch_bounds__(256) void f4_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                 int64_t ld, int64_t rows, int64_t width,
+                                                 const double* __restrict__ Cr, const double* __restrict__ P,
+                                                 int rb, double cval) {
+    const int64_t j = (int64_t)blockIdx.x * (256 * V) + threadIdx.x * V;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - V;
+    double pr[K][V];
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        if constexpr (V == 2) {
+            const d2 v = *(const d2*)(P + (int64_t)l * ld + jc);
+            pr[l][0] = v.x;
+            pr[l][1] = v.y;
+        } else {
+            pr[l][0] = P[(int64_t)l * ld + jc];
+        }
+    }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    const int lane = threadIdx.x & 63;
+    auto load = [&](double (&t)[U][V], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double* p = T + (i0 + r0 + u) * ld + jc;
+            if constexpr (V == 2) {
+                const d2 v = ldv<NT>(p);
+                t[u][0] = v.x;
+                t[u][1] = v.y;
+            } else {
+                t[u][0] = NT ? __builtin_nontemporal_load(p) : *p;
+            }
+        }
+    };
+    auto store = [&](const double (&t)[U][V], int r0) {
+        if (!colok) return;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            double* p = To + (i0 + r0 + u) * ld + j;
+            if constexpr (V == 2) {
+                d2 v;
+                v.x = t[u][0];
+                v.y = t[u][1];
+                stv<NT>(p, v);
+            } else {
+                if (NT) __builtin_nontemporal_store(t[u][0], p);
+                else *p = t[u][0];
+            }
+        }
+    };
+    constexpr int LC = (16 / U) < K ? (16 / U) : K;
+    constexpr int NCV = (U * K + 63) / 64;   // MODE 3: coefficient doubles per lane per group
+    auto chain_s = [&](double (&t)[U][V], const double (&f)[U][LC], int l0) {
+#pragma unroll
+        for (int l = 0; l < LC; ++l)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < V; ++e) t[u][e] = __builtin_fma(-f[u][l], pr[l0 + l][e], t[u][e]);
+    };
+    auto group = [&](double (&t)[U][V], int r0, const double (&cv)[NCV]) {
+        if constexpr (MODE == 0) {
+            const cdptr cb = (cdptr)(Cr + (i0 + r0) * K);
+            double fa[U][LC], fb[U][LC];
+            auto fetch = [&](double (&f)[U][LC], int l0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int l = 0; l < LC; ++l) f[u][l] = cb[u * K + l0 + l];
+            };
+            fetch(fa, 0);
+#pragma unroll
+            for (int l0 = 0; l0 < K; l0 += 2 * LC) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                if (l0 + LC < K) fetch(fb, l0 + LC);
+                __builtin_amdgcn_sched_barrier(0);
+                chain_s(t, fa, l0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (l0 + LC < K) {
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    if (l0 + 2 * LC < K) fetch(fa, l0 + 2 * LC);
+                    __builtin_amdgcn_sched_barrier(0);
+                    chain_s(t, fb, l0 + LC);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        } else if constexpr (MODE == 1) {
+#pragma unroll
+            for (int l = 0; l < K; ++l)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int e = 0; e < V; ++e)
+                        t[u][e] = __builtin_fma(-cval, pr[l][e], t[u][e]);
+        } else if constexpr (MODE == 3) {
+#pragma unroll
+            for (int l = 0; l < K; ++l)
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int idx = u * K + l;
+                    const double f = rl(cv[idx >> 6], idx & 63);
+#pragma unroll
+                    for (int e = 0; e < V; ++e) t[u][e] = __builtin_fma(-f, pr[l][e], t[u][e]);
+                }
+        }
+        store(t, r0);
+    };
+    auto loadc = [&](double (&cv)[NCV], int r0) {
+        if constexpr (MODE == 3) {
+#pragma unroll
+            for (int k = 0; k < NCV; ++k) {
+                const int idx = k * 64 + lane;   // (u, l) = (idx / K, idx % K): row-major C is contiguous
+                cv[k] = Cr[(i0 + r0) * K + (idx < U * K ? idx : 0)];
+            }
+        }
+    };
+    double ta[U][V], tb[U][V];
+    double ca[NCV], cb2[NCV];
+    int r = 0;
+    // all rows dense; groups of U rows (nr is a multiple of U in the lab)
+    load(ta, r);
+    loadc(ca, r);
+    while (true) {
+        const bool nb = r + U < nr;
+        load(tb, nb ? r + U : r);
+        loadc(cb2, nb ? r + U : r);
+        __builtin_amdgcn_sched_barrier(0);
+        group(ta, r, ca);
+        r += U;
+        if (!nb) break;
+        const bool na = r + U < nr;
+        load(ta, na ? r + U : r);
+        loadc(ca, na ? r + U : r);
+        __builtin_amdgcn_sched_barrier(0);
+        group(tb, r, cb2);
+        r += U;
+        if (!na) break;
+    }
+}
+
+
+// Streaming-structure probe: the pass's memory traffic with no arithmetic.  U rows per
+// iteration (all loads, then all stores), band of rb rows, 512-column tiles (2 doubles
+// per lane), grid (tile, band); dynamic LDS caps workgroups per CU.
+template <int U>
+__global__ __launch_bounds__(256) void copy_kernel(double* __restrict__ T, int64_t ld, int64_t rows,
+                                                   int64_t width, int rb) {
+    extern __shared__ double dyn_lds[];
+    const int64_t j = (int64_t)blockIdx.x * 512 + threadIdx.x * 2;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 2;
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    if (rb < 0) dyn_lds[threadIdx.x] = 0.0;   // keeps the dynamic allocation
+    for (int64_t i = i0; i < iend; i += U) {
+        d2 t[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) t[u] = ldv<true>(T + (i + u) * ld + jc);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            t[u].x += 0.0;
+            if (colok) stv<true>(T + (i + u) * ld + j, t[u]);
+        }
+    }
+}
+
+
+// Persistent interleaved probe: G workgroups per 512-column tile, workgroup (x, g) walks
+// bands g, g + G, g + 2G, ... of rb rows; TF: grid x = tile (tile fastest) or band group.
+template <int U>
+__global__ __launch_bounds__(256) void copyp_kernel(double* __restrict__ T, int64_t ld, int64_t rows,
+                                                    int64_t width, int rb, int G, int tf) {
+    extern __shared__ double dyn_lds[];
+    const int ntile = (int)((width + 511) / 512);
+    const int x = tf ? blockIdx.x % ntile : blockIdx.x / G;
+    const int g = tf ? blockIdx.x / ntile : blockIdx.x % G;
+    const int64_t j = (int64_t)x * 512 + threadIdx.x * 2;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 2;
+    if (rb < 0) dyn_lds[threadIdx.x] = 0.0;
+    for (int64_t i0 = (int64_t)g * rb; i0 < rows; i0 += (int64_t)G * rb) {
+        const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+        for (int64_t i = i0; i < iend; i += U) {
+            d2 t[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) t[u] = ldv<true>(T + (i + u) * ld + jc);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                t[u].x += 0.0;
+                if (colok) stv<true>(T + (i + u) * ld + j, t[u]);
+            }
+        }
+    }
+}
+
+
+// ---- coefficients in VGPRs, delivered by DPP row broadcast (row_newbcast:n: lane n of
+// each 16-lane row to the whole row).  A coefficient register pair holds 16 coefficients
+// (replicated over the 4 rows of the wave), loaded with one vector load per 16.
+template <int N>
+__device__ inline double bc_mov(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + N, 0xf, 0xf, false);
+}
+__device__ inline double bcn(double v, int n) {
+    switch (n) {
+        case 0: return bc_mov<0>(v);   case 1: return bc_mov<1>(v);   case 2: return bc_mov<2>(v);
+        case 3: return bc_mov<3>(v);   case 4: return bc_mov<4>(v);   case 5: return bc_mov<5>(v);
+        case 6: return bc_mov<6>(v);   case 7: return bc_mov<7>(v);   case 8: return bc_mov<8>(v);
+        case 9: return bc_mov<9>(v);   case 10: return bc_mov<10>(v); case 11: return bc_mov<11>(v);
+        case 12: return bc_mov<12>(v); case 13: return bc_mov<13>(v); case 14: return bc_mov<14>(v);
+        default: return bc_mov<15>(v);
+    }
+}
+// t = fma(-c[lane n of the row], p, t) in one instruction
+template <int N>
+__device__ inline void fmac_bc(double& t, double c, double p) {
+    asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(t) : "v"(c), "v"(p), "n"(N));
+}
+__device__ inline void fmac_bcn(double& t, double c, double p, int n) {
+    switch (n) {
+        case 0: fmac_bc<0>(t, c, p); break;   case 1: fmac_bc<1>(t, c, p); break;
+        case 2: fmac_bc<2>(t, c, p); break;   case 3: fmac_bc<3>(t, c, p); break;
+        case 4: fmac_bc<4>(t, c, p); break;   case 5: fmac_bc<5>(t, c, p); break;
+        case 6: fmac_bc<6>(t, c, p); break;   case 7: fmac_bc<7>(t, c, p); break;
+        case 8: fmac_bc<8>(t, c, p); break;   case 9: fmac_bc<9>(t, c, p); break;
+        case 10: fmac_bc<10>(t, c, p); break; case 11: fmac_bc<11>(t, c, p); break;
+        case 12: fmac_bc<12>(t, c, p); break; case 13: fmac_bc<13>(t, c, p); break;
+        case 14: fmac_bc<14>(t, c, p); break; default: fmac_bc<15>(t, c, p); break;
+    }
+}
+
+
+// step I of a group's chain: l = I / U, u = I % U (all U rows at step l, then step l + 1)
+template <int K, int V, int U, bool ASM, int I>
+__device__ __forceinline__ void dstep(double (&t)[U][V], const double (&c)[U * K / 16], const double (&pr)[K][V]) {
+    constexpr int l = I / U, u = I % U, idx = u * K + l;
+    if constexpr (ASM) {
+        fmac_bc<idx & 15>(t[u][0], c[idx >> 4], pr[l][0]);
+        if constexpr (V == 2) fmac_bc<idx & 15>(t[u][1], c[idx >> 4], pr[l][1]);
+    } else {
+        const double f = bc_mov<idx & 15>(c[idx >> 4]);
+        t[u][0] = __builtin_fma(-f, pr[l][0], t[u][0]);
+        if constexpr (V == 2) t[u][1] = __builtin_fma(-f, pr[l][1], t[u][1]);
+    }
+}
+template <int K, int V, int U, bool ASM, int... I>
+__device__ __forceinline__ void dchain(double (&t)[U][V], const double (&c)[U * K / 16], const double (&pr)[K][V],
+                                       std::integer_sequence<int, I...>) {
+    (dstep<K, V, U, ASM, I>(t, c, pr), ...);
+}
+
+// f4 structure (P[0..K)[V] in VGPRs, groups of U rows, 256-row band) with the coefficients
+// of the next group loaded with its rows; ASM: fused v_fmac_f64_dpp, else mov_dpp + fma.
+template <bool NT, int K, int V, int U, bool ASM, int W = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void f4d_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                  int64_t ld, int64_t rows, int64_t width,
+                                                  const double* __restrict__ Cr, const double* __restrict__ P,
+                                                  int rb) {
+    const int64_t j = (int64_t)blockIdx.x * (256 * V) + threadIdx.x * V;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - V;
+    double pr[K][V];
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        if constexpr (V == 2) {
+            const d2 v = *(const d2*)(P + (int64_t)l * ld + jc);
+            pr[l][0] = v.x;
+            pr[l][1] = v.y;
+        } else {
+            pr[l][0] = P[(int64_t)l * ld + jc];
+        }
+    }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    const int l16 = threadIdx.x & 15;
+    constexpr int NC = U * K / 16;   // coefficient doubles per lane per group
+    auto load = [&](double (&t)[U][V], double (&c)[NC], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double* p = T + (i0 + r0 + u) * ld + jc;
+            if constexpr (V == 2) {
+                const d2 v = ldv<NT>(p);
+                t[u][0] = v.x;
+                t[u][1] = v.y;
+            } else {
+                t[u][0] = NT ? __builtin_nontemporal_load(p) : *p;
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < NC; ++v) {
+            const int idx = v * 16 + l16;
+            c[v] = Cr[(i0 + r0 + idx / K) * K + idx % K];
+        }
+    };
+    auto group = [&](double (&t)[U][V], const double (&c)[NC], int r0) {
+        dchain<K, V, U, ASM>(t, c, pr, std::make_integer_sequence<int, K * U>{});
+        if (colok)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                double* p = To + (i0 + r0 + u) * ld + j;
+                if constexpr (V == 2) {
+                    d2 v;
+                    v.x = t[u][0];
+                    v.y = t[u][1];
+                    stv<NT>(p, v);
+                } else {
+                    if (NT) __builtin_nontemporal_store(t[u][0], p);
+                    else *p = t[u][0];
+                }
+            }
+    };
+    double ta[U][V], tb[U][V], ca[NC], cb[NC];
+    int r = 0;
+    load(ta, ca, r);
+    while (true) {
+        const bool nb = r + U < nr;
+        load(tb, cb, nb ? r + U : r);
+        __builtin_amdgcn_sched_barrier(0);
+        group(ta, ca, r);
+        r += U;
+        if (!nb) break;
+        const bool na = r + U < nr;
+        load(ta, ca, na ? r + U : r);
+        __builtin_amdgcn_sched_barrier(0);
+        group(tb, cb, r);
+        r += U;
+        if (!na) break;
+    }
+}
+
+// VALU rate probe: 8 independent chains per lane, ITER x 8 steps each.
+// MODE 0: v_fma_f64 with an SGPR coefficient, 1: v_fmac_f64_dpp (row_newbcast) with a VGPR
+// coefficient, 2: v_fma_f64 with a VGPR coefficient.
+template <int MODE>
+__global__ __launch_bounds__(256) void valu_kernel(double* out, double cs, int iters) {
+    double t[8], p[8];
+    const double cv = cs + threadIdx.x * 1e-3;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        t[k] = threadIdx.x + k;
+        p[k] = 1.0 + k * 1e-9;
+    }
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if constexpr (MODE == 0) t[k] = __builtin_fma(-cs, p[s], t[k]);
+                else if constexpr (MODE == 1) fmac_bc<3>(t[k], cv, p[s]);
+                else t[k] = __builtin_fma(-cv, p[s], t[k]);
+            }
+    }
+    double a = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a += t[k];
+    out[blockIdx.x * 256 + threadIdx.x] = a;
+}
+
+// Latency probe: NCH independent chains per lane; MODE 1: v_fmac_f64_dpp, 2: v_fma_f64 (VGPR c)
+template <int MODE, int NCH>
+__global__ __launch_bounds__(256) void lat_kernel(double* out, double cs, int iters) {
+    double t[NCH], p[8];
+    const double cv = cs + threadIdx.x * 1e-3;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) t[k] = threadIdx.x + k;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[k] = 1.0 + k * 1e-9;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+            for (int k = 0; k < NCH; ++k) {
+                if constexpr (MODE == 1) fmac_bc<3>(t[k], cv, p[s]);
+                else asm("v_fma_f64 %0, -%1, %2, %0" : "+v"(t[k]) : "v"(cv), "v"(p[s]));
+            }
+    }
+    double a = 0;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) a += t[k];
+    out[blockIdx.x * 256 + threadIdx.x] = a;
+}
+
+struct Lab {
+    int64_t rows, width, ld;
+    double *T, *To, *Cr, *P;
+};
+
+typedef void (*Launch)(const Lab&, int K, int rb, hipStream_t);
+
+template <int K, int V, int U, int MODE>
+void launch_f4(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 256 * V - 1) / (256 * V)), (unsigned)((L.rows + rb - 1) / rb));
+    f4_kernel<true, K, V, U, MODE><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb, 0.5);
+}
+
+
+// Pipelined stages: workgroup = S x 256 lanes; stage s (waves 4s..4s+3) applies steps
+// [s KS, (s+1) KS) to groups of U rows of a 512-column tile, holding its P slice in VGPRs
+// and reading its coefficients by scalar loads (form 4's chunks); stage 0 loads rows from
+// HBM (one group ahead), stage S-1 stores them, stages hand groups on through LDS slots
+// (two per stage boundary).  Iteration k: stage s works on group k - s; one barrier per
+// iteration (raw s_barrier: the row prefetch stays in flight across it).
+template <bool NT, int KS, int S, int U, int D>
+__global__ __launch_bounds__(256 * S) void pipe_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                       int64_t ld, int64_t rows, int64_t width,
+                                                       const double* __restrict__ Cr, const double* __restrict__ P,
+                                                       int rb) {
+    constexpr int K = KS * S;
+    __shared__ d2 slot[(S > 1 ? S - 1 : 1)][2][U][256];
+    const int st = S == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);   // stage (wave-uniform)
+    const int tid = threadIdx.x & 255;
+    const int64_t j = (int64_t)blockIdx.x * 512 + tid * 2;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 2;
+    double pr[KS][2];
+#pragma unroll
+    for (int l = 0; l < KS; ++l) {
+        const d2 v = *(const d2*)(P + (int64_t)(st * KS + l) * ld + jc);
+        pr[l][0] = v.x;
+        pr[l][1] = v.y;
+    }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int ng = (int)((iend - i0) / U);   // the lab's bands are whole groups
+    constexpr int LC = 16 / U;
+    auto chain = [&](double (&t)[U][2], int g) {
+        const cdptr cb = (cdptr)(Cr + (i0 + (int64_t)g * U) * K + st * KS);
+        double fa[U][LC], fb[U][LC];
+        auto fetch = [&](double (&f)[U][LC], int l0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int l = 0; l < LC; ++l) f[u][l] = cb[u * K + l0 + l];
+        };
+        auto run = [&](const double (&f)[U][LC], int l0) {
+#pragma unroll
+            for (int l = 0; l < LC; ++l)
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    t[u][0] = __builtin_fma(-f[u][l], pr[l0 + l][0], t[u][0]);
+                    t[u][1] = __builtin_fma(-f[u][l], pr[l0 + l][1], t[u][1]);
+                }
+        };
+        fetch(fa, 0);
+#pragma unroll
+        for (int l0 = 0; l0 < KS; l0 += 2 * LC) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            if (l0 + LC < KS) fetch(fb, l0 + LC);
+            __builtin_amdgcn_sched_barrier(0);
+            run(fa, l0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (l0 + LC < KS) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                if (l0 + 2 * LC < KS) fetch(fa, l0 + 2 * LC);
+                __builtin_amdgcn_sched_barrier(0);
+                run(fb, l0 + LC);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    };
+    auto load = [&](double (&t)[U][2], int g) {
+        const int gg = g < ng ? g : ng - 1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const d2 v = ldv<NT>(T + (i0 + (int64_t)gg * U + u) * ld + jc);
+            t[u][0] = v.x;
+            t[u][1] = v.y;
+        }
+    };
+    // stage 0 keeps D - 1 groups of rows in flight: group g lives in buf[g % D]
+    double buf[D][U][2];
+    if (st == 0)
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d) load(buf[d], d);
+    const int total = ng + S - 1;
+    for (int k = 0; k < total; k += D) {
+#pragma unroll
+        for (int h = 0; h < D; ++h) {
+            const int kk = k + h;
+            double (&cur)[U][2] = buf[h];
+            const int g = kk - st;
+            if (kk < total && g >= 0 && g < ng) {
+                if (st == 0) {
+                    load(buf[(h + D - 1) % D], g + D - 1);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const d2 v = slot[st - 1][g & 1][u][tid];
+                        cur[u][0] = v.x;
+                        cur[u][1] = v.y;
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                chain(cur, g);
+                __builtin_amdgcn_sched_barrier(0);
+                if (st == S - 1) {
+                    if (colok)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            d2 v;
+                            v.x = cur[u][0];
+                            v.y = cur[u][1];
+                            stv<NT>(To + (i0 + (int64_t)g * U + u) * ld + j, v);
+                        }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        d2 v;
+                        v.x = cur[u][0];
+                        v.y = cur[u][1];
+                        slot[st][g & 1][u][tid] = v;
+                    }
+                }
+            }
+            if (S > 1 && kk < total) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    }
+}
+
+template <int KS, int S, int U, int D>
+void launch_pipe(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 511) / 512), (unsigned)((L.rows + rb - 1) / rb));
+    pipe_kernel<true, KS, S, U, D><<<grid, 256 * S, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
+
+template <int K, int V, int U, bool ASM, int W = 1>
+void launch_f4d(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 256 * V - 1) / (256 * V)), (unsigned)((L.rows + rb - 1) / rb));
+    f4d_kernel<true, K, V, U, ASM, W><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
+// K = 64, V = 1, U = 2 with 1.5 coefficient sets: a group's coefficient pairs 0,1,4,5 are
+// steps 0..31 of its two rows, 2,3,6,7 steps 32..63.  Group g: issue the loads of its
+// second half (into the pairs group g-1's second half used), then rows g+1; steps 0..31;
+// issue the first half of g+1 (into the pairs just consumed); steps 32..63; store.
+template <int K, int V, int U, int I0, bool ASM, int... I>
+__device__ __forceinline__ void dchain_part(double (&t)[U][V], const double (&c)[U * K / 16],
+                                            const double (&pr)[K][V], std::integer_sequence<int, I...>) {
+    (dstep<K, V, U, ASM, I0 + I>(t, c, pr), ...);
+}
+template <bool NT, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void f4e_kernel(
+    const double* __restrict__ T, double* __restrict__ To, int64_t ld, int64_t rows, int64_t width,
+    const double* __restrict__ Cr, const double* __restrict__ P, int rb) {
+    constexpr int K = 64, V = 1, U = 2, NC = 8;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 1;
+    double pr[K][V];
+#pragma unroll
+    for (int l = 0; l < K; ++l) pr[l][0] = P[(int64_t)l * ld + jc];
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    const int l16 = threadIdx.x & 15;
+    double c[NC];
+    auto loadc = [&](int r0, int half) {   // half 0: pairs 0,1,4,5; 1: pairs 2,3,6,7
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int v = (w >> 1) * 4 + half * 2 + (w & 1);
+            const int idx = v * 16 + l16;
+            c[v] = Cr[(i0 + r0 + idx / K) * K + idx % K];
+        }
+    };
+    auto loadt = [&](double (&t)[U][V], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double* p = T + (i0 + r0 + u) * ld + jc;
+            t[u][0] = NT ? __builtin_nontemporal_load(p) : *p;
+        }
+    };
+    auto group = [&](double (&t)[U][V], double (&tn)[U][V], int r0, int rn, bool more) {
+        loadc(r0, 1);
+        __builtin_amdgcn_sched_barrier(0);   // in-order vmcnt: the coefficients first
+        loadt(tn, rn);
+        __builtin_amdgcn_sched_barrier(0);
+        dchain_part<K, V, U, 0, true>(t, c, pr, std::make_integer_sequence<int, K * U / 2>{});
+        __builtin_amdgcn_sched_barrier(0);
+        loadc(rn, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        dchain_part<K, V, U, K * U / 2, true>(t, c, pr, std::make_integer_sequence<int, K * U / 2>{});
+        if (colok)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                double* p = To + (i0 + r0 + u) * ld + j;
+                if (NT) __builtin_nontemporal_store(t[u][0], p);
+                else *p = t[u][0];
+            }
+    };
+    double ta[U][V], tb[U][V];
+    int r = 0;
+    loadt(ta, 0);
+    loadc(0, 0);
+    while (true) {
+        const bool nb = r + U < nr;
+        group(ta, tb, r, nb ? r + U : r, nb);
+        r += U;
+        if (!nb) break;
+        const bool na = r + U < nr;
+        group(tb, ta, r, na ? r + U : r, na);
+        r += U;
+        if (!na) break;
+    }
+}
+template <int W>
+void launch_f4e(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 255) / 256), (unsigned)((L.rows + rb - 1) / rb));
+    f4e_kernel<true, W><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
+// f4e with buffer loads/stores: band resources in SGPRs, one 32-bit column offset per lane
+// (rows: soffset = row offset in the band; coefficients: C row-major, (u, l) at r0 K + u K + l).
+template <bool NT, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void f4b_kernel(
+    const double* __restrict__ T, double* __restrict__ To, int64_t ld, int64_t rows, int64_t width,
+    const double* __restrict__ Cr, const double* __restrict__ P, int rb) {
+    constexpr int K = 64, V = 1, U = 2, NC = 8;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool colok = j < width;
+    const int jc = (int)(colok ? j : width - 1);
+    double pr[K][V];
+#pragma unroll
+    for (int l = 0; l < K; ++l) pr[l][0] = P[(int64_t)l * ld + jc];
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(T + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(To + i0 * ld), (short)0, colok ? (int)((int64_t)nr * ld * 8) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Cr + i0 * K), (short)0, (int)((int64_t)nr * K * 8), 0x00020000);
+    const int voff = jc * 8;
+    const int coff = (threadIdx.x & 15) * 8;
+    const int rowb = (int)(ld * 8);
+    double c[NC];
+    auto loadc = [&](int r0, int half) {   // half 0: pairs 0,1,4,5; 1: pairs 2,3,6,7
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int v = (w >> 1) * 4 + half * 2 + (w & 1);
+            const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rc, coff + v * 128, r0 * K * 8, 0);
+            c[v] = __builtin_bit_cast(double, x);
+        }
+    };
+    auto loadt = [&](double (&t)[U][V], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rt, voff, (r0 + u) * rowb, NT ? 2 : 0);
+            t[u][0] = __builtin_bit_cast(double, x);
+        }
+    };
+    auto group = [&](double (&t)[U][V], double (&tn)[U][V], int r0, int rn) {
+        loadc(r0, 1);
+        __builtin_amdgcn_sched_barrier(0);   // in-order vmcnt: the coefficients first
+        loadt(tn, rn);
+        __builtin_amdgcn_sched_barrier(0);
+        dchain_part<K, V, U, 0, true>(t, c, pr, std::make_integer_sequence<int, K * U / 2>{});
+        __builtin_amdgcn_sched_barrier(0);
+        loadc(rn, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        dchain_part<K, V, U, K * U / 2, true>(t, c, pr, std::make_integer_sequence<int, K * U / 2>{});
+#pragma unroll
+        for (int u = 0; u < U; ++u)   // out-of-range lanes: num_records 0 drops the store
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t[u][0]), ro, voff, (r0 + u) * rowb,
+                                                  NT ? 2 : 0);
+    };
+    double ta[U][V], tb[U][V];
+    int r = 0;
+    loadt(ta, 0);
+    loadc(0, 0);
+    while (true) {
+        const bool nb = r + U < nr;
+        group(ta, tb, r, nb ? r + U : r);
+        r += U;
+        if (!nb) break;
+        const bool na = r + U < nr;
+        group(tb, ta, r, na ? r + U : r);
+        r += U;
+        if (!na) break;
+    }
+}
+template <int W>
+void launch_f4b(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 255) / 256), (unsigned)((L.rows + rb - 1) / rb));
+    f4b_kernel<true, W><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
+// K = 64, V = 1, U rows, coefficients rolled by quarters: pair u*4 + q holds row u's steps
+// [16q, 16q + 16); once quarter q of group g has run, those U pairs are reloaded with group
+// g+1's quarter q.  Rows of g+1 are issued at the start of g, after every coefficient load
+// group g still waits for.
+template <int K, int V, int U, int Q, bool ASM, int... I>
+__device__ __forceinline__ void qchain(double (&t)[U][V], const double (&c)[U * K / 16], const double (&pr)[K][V],
+                                       std::integer_sequence<int, I...>) {
+    // I enumerates (l within the quarter) * U + u
+    (dstep<K, V, U, ASM, (Q * 16 + I / U) * U + I % U>(t, c, pr), ...);
+}
+template <bool NT, int U, int W, int CL = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void f4q_kernel(
+    const double* __restrict__ T, double* __restrict__ To, int64_t ld, int64_t rows, int64_t width,
+    const double* __restrict__ Cr, const double* __restrict__ P, int rb) {
+    constexpr int K = 64, V = 1, NC = U * 4;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool colok = j < width;
+    const int jc = (int)(colok ? j : width - 1);
+    double pr[K][V];
+#pragma unroll
+    for (int l = 0; l < K; ++l) pr[l][0] = P[(int64_t)l * ld + jc];
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(T + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(To + i0 * ld), (short)0, colok ? (int)((int64_t)nr * ld * 8) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Cr + i0 * K), (short)0, (int)((int64_t)nr * K * 8), 0x00020000);
+    const int voff = jc * 8;
+    const int coff = (threadIdx.x & 15) * 8;
+    const int rowb = (int)(ld * 8);
+    double c[NC];
+    auto loadq = [&](int r0, int q) {
+        if constexpr (CL == 1) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rc, coff + (u * 4 + q) * 128, r0 * K * 8, 0);
+                c[u * 4 + q] = __builtin_bit_cast(double, x);
+            }
+        } else if constexpr (CL == 2) {
+            // quarter q of rows u, u+1 in one b128 per lane (timing only: wrong pairing)
+#pragma unroll
+            for (int u = 0; u < U; u += 2) {
+                const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rc, coff * 2 + (u * 4 + q) * 128, r0 * K * 8, 0);
+                const d2 d = __builtin_bit_cast(d2, x);
+                c[u * 4 + q] = d.x;
+                c[(u + 1) * 4 + q] = d.y;
+            }
+        }
+    };
+    auto loadt = [&](double (&t)[U][V], int r0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rt, voff, (r0 + u) * rowb, NT ? 2 : 0);
+            t[u][0] = __builtin_bit_cast(double, x);
+        }
+    };
+    auto group = [&](double (&t)[U][V], double (&tn)[U][V], int r0, int rn) {
+        loadt(tn, rn);
+        __builtin_amdgcn_sched_barrier(0);
+        qchain<K, V, U, 0, true>(t, c, pr, std::make_integer_sequence<int, 16 * U>{});
+        __builtin_amdgcn_sched_barrier(0);
+        loadq(rn, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        qchain<K, V, U, 1, true>(t, c, pr, std::make_integer_sequence<int, 16 * U>{});
+        __builtin_amdgcn_sched_barrier(0);
+        loadq(rn, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        qchain<K, V, U, 2, true>(t, c, pr, std::make_integer_sequence<int, 16 * U>{});
+        __builtin_amdgcn_sched_barrier(0);
+        loadq(rn, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        qchain<K, V, U, 3, true>(t, c, pr, std::make_integer_sequence<int, 16 * U>{});
+        __builtin_amdgcn_sched_barrier(0);
+        loadq(rn, 3);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t[u][0]), ro, voff, (r0 + u) * rowb,
+                                                  NT ? 2 : 0);
+    };
+    double ta[U][V], tb[U][V];
+    int r = 0;
+    loadt(ta, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) loadq(0, q);
+    while (true) {
+        const bool nb = r + U < nr;
+        group(ta, tb, r, nb ? r + U : r);
+        r += U;
+        if (!nb) break;
+        const bool na = r + U < nr;
+        group(tb, ta, r, na ? r + U : r);
+        r += U;
+        if (!na) break;
+    }
+}
+template <int U, int W, int CL = 1>
+void launch_f4q(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 255) / 256), (unsigned)((L.rows + rb - 1) / rb));
+    f4q_kernel<true, U, W, CL><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
+struct Variant {
+    const char* name;
+    int K, rb;
+    Launch fn;
+    bool exact;   // checked against the reference
+};
+
+static bool check(const Variant& v) {
+    Lab L;
+    L.rows = 1024;
+    L.width = 4112;   // 8 tiles of 512 + a ragged one
+    L.ld = 4608;
+    const int K = v.K;
+    CK(hipMalloc(&L.T, L.rows * L.ld * 8));
+    CK(hipMalloc(&L.To, L.rows * L.ld * 8));
+    double* Tr;
+    CK(hipMalloc(&Tr, L.rows * L.ld * 8));
+    CK(hipMalloc(&L.Cr, L.rows * K * 8));
+    CK(hipMalloc(&L.P, (int64_t)K * L.ld * 8));
+    fill_kernel<<<1024, 256>>>(L.T, L.rows * L.ld, 1);
+    fill_kernel<<<1024, 256>>>(L.Cr, L.rows * K, 2);
+    fill_kernel<<<1024, 256>>>(L.P, (int64_t)K * L.ld, 3);
+    CK(hipMemset(L.To, 0, L.rows * L.ld * 8));
+    CK(hipMemset(Tr, 0, L.rows * L.ld * 8));
+    ref_kernel<<<dim3((unsigned)((L.width + 255) / 256), (unsigned)L.rows), 256>>>(L.T, Tr, L.ld, L.rows, L.width,
+                                                                                  K, L.Cr, L.P);
+    v.fn(L, K, v.rb < L.rows ? v.rb : 256, 0);
+    CK(hipDeviceSynchronize());
+    std::vector<double> a(L.rows * L.ld), b(L.rows * L.ld);
+    CK(hipMemcpy(a.data(), L.To, a.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), Tr, b.size() * 8, hipMemcpyDeviceToHost));
+    int64_t bad = 0;
+    for (int64_t i = 0; i < L.rows; ++i)
+        for (int64_t jj = 0; jj < L.width; ++jj)
+            if (memcmp(&a[i * L.ld + jj], &b[i * L.ld + jj], 8) != 0) ++bad;
+    CK(hipFree(L.T));
+    CK(hipFree(L.To));
+    CK(hipFree(Tr));
+    CK(hipFree(L.Cr));
+    CK(hipFree(L.P));
+    if (bad) printf("  CHECK %-28s K=%d: %ld of %ld elements differ\n", v.name, K, (long)bad,
+                    (long)(L.rows * L.width));
+    return bad == 0;
+}
+
+int main(int argc, char** argv) {
+    const int64_t rows = argc > 1 ? atoll(argv[1]) : 32768;
+    const int64_t ncols = argc > 2 ? atoll(argv[2]) : 65537;
+    const int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const char* only = argc > 4 ? argv[4] : nullptr;
+    std::vector<Variant> vs = {
+        {"f4d K32 V2U2 mov", 32, 256, launch_f4d<32, 2, 2, false>, true},
+        {"f4d K32 V2U2 asm", 32, 256, launch_f4d<32, 2, 2, true>, true},
+        {"f4d K32 V2U4 asm", 32, 256, launch_f4d<32, 2, 4, true>, true},
+        {"f4d K64 V1U2 mov", 64, 256, launch_f4d<64, 1, 2, false>, true},
+        {"f4d K64 V1U2 asm", 64, 256, launch_f4d<64, 1, 2, true>, true},
+        {"f4d K64 V1U4 asm", 64, 256, launch_f4d<64, 1, 4, true>, true},
+        {"f4d K64 V1U8 asm", 64, 256, launch_f4d<64, 1, 8, true>, true},
+        {"f4e K64 V1U2 w1", 64, 256, launch_f4e<1>, true},
+        {"f4b K64 V1U2 w1", 64, 256, launch_f4b<1>, true},
+        {"f4q K64 V1U2 w3", 64, 256, launch_f4q<2, 3>, true},
+        {"f4q K64 V1U2 w3 noload", 64, 256, launch_f4q<2, 3, 0>, false},
+        {"f4q K64 V1U2 w3 b128", 64, 256, launch_f4q<2, 3, 2>, false},
+        {"f4q K64 V1U3 w3 rb192", 64, 192, launch_f4q<3, 3>, true},
+        {"f4q K64 V1U3 w3 rb384", 64, 384, launch_f4q<3, 3>, true},
+        {"f4q K64 V1U4 w2", 64, 256, launch_f4q<4, 2>, true},
+        {"f4q K64 V1U8 w1", 64, 256, launch_f4q<8, 1>, true},
+        {"f4b K64 V1U2 w3", 64, 256, launch_f4b<3>, true},
+        {"f4b K64 V1U2 w3 rb128", 64, 128, launch_f4b<3>, true},
+        {"f4b K64 V1U2 w3 rb512", 64, 512, launch_f4b<3>, true},
+        {"f4e K64 V1U2 w3", 64, 256, launch_f4e<3>, true},
+        {"f4e K64 V1U2 w3 rb512", 64, 512, launch_f4e<3>, true},
+        {"f4d K64 V1U2 asm w3", 64, 256, launch_f4d<64, 1, 2, true, 3>, true},
+        {"f4d K64 V1U4 asm w3", 64, 256, launch_f4d<64, 1, 4, true, 3>, true},
+        {"f4d K32 V2U2 asm w3", 32, 256, launch_f4d<32, 2, 2, true, 3>, true},
+        {"f4d K16 V2U2 asm", 16, 256, launch_f4d<16, 2, 2, true>, true},
+        {"f4d K16 V2U4 asm", 16, 256, launch_f4d<16, 2, 4, true>, true},
+        {"f4 smem K32 V2U2", 32, 256, launch_f4<32, 2, 2, 0>, true},
+        {"f4 const K32 V2U2", 32, 256, launch_f4<32, 2, 2, 1>, false},
+        {"f4 copy V2U2", 32, 256, launch_f4<32, 2, 2, 2>, false},
+        {"f4 readlane K32 V2U2", 32, 256, launch_f4<32, 2, 2, 3>, true},
+        {"f4 smem K64 V1U4", 64, 256, launch_f4<64, 1, 4, 0>, true},
+        {"f4 const K64 V1U2", 64, 256, launch_f4<64, 1, 2, 1>, false},
+        {"f4 readlane K64 V1U2", 64, 256, launch_f4<64, 1, 2, 3>, true},
+        {"f4 smem K16 V2U2", 16, 256, launch_f4<16, 2, 2, 0>, true},
+        {"pipe K64 S2 U2 D2 rb256", 64, 256, launch_pipe<32, 2, 2, 2>, true},
+        {"pipe K64 S2 U2 D3 rb256", 64, 256, launch_pipe<32, 2, 2, 3>, true},
+        {"pipe K64 S2 U2 D4 rb256", 64, 256, launch_pipe<32, 2, 2, 4>, true},
+        {"pipe K64 S2 U4 D2 rb256", 64, 256, launch_pipe<32, 2, 4, 2>, true},
+        {"pipe K64 S2 U4 D3 rb256", 64, 256, launch_pipe<32, 2, 4, 3>, true},
+        {"pipe K64 S2 U1 D4 rb256", 64, 256, launch_pipe<32, 2, 1, 4>, true},
+        {"pipe K32 S2 U2 D3 rb256", 32, 256, launch_pipe<16, 2, 2, 3>, true},
+        {"pipe K32 S1 U2 D3 rb256", 32, 256, launch_pipe<32, 1, 2, 3>, true},
+        {"pipe K96 S3 U2 D3 rb256", 96, 256, launch_pipe<32, 3, 2, 3>, true},
+        {"pipe K96 S3 U2 D4 rb256", 96, 256, launch_pipe<32, 3, 2, 4>, true},
+        {"pipe K128 S4 U2 D3 rb256", 128, 256, launch_pipe<32, 4, 2, 3>, true},
+    };
+    for (auto& v : vs)
+        if (v.exact && !(only && !strcmp(only, "copy")) && (!only || strstr(v.name, only))) printf("check %-28s %s\n", v.name, check(v) ? "bit-exact" : "FAILED");
+    Lab L;
+    L.rows = rows;
+    L.width = (ncols + 15) / 16 * 16;
+    L.ld = L.width >= 4096 ? (L.width + 511) / 512 * 512 : L.width;
+    if (getenv("LAB_LD")) L.ld = atoll(getenv("LAB_LD"));
+    printf("tableau %ld x %ld (width %ld, ld %ld): %.2f GB\n", (long)rows, (long)ncols, (long)L.width, (long)L.ld,
+           rows * L.ld * 8 / 1e9);
+    CK(hipMalloc(&L.T, rows * L.ld * 8));
+    L.To = L.T;   // in place, as the product's pass
+    CK(hipMalloc(&L.Cr, rows * 128 * 8));
+    CK(hipMalloc(&L.P, (int64_t)128 * L.ld * 8));
+    fill_kernel<<<4096, 256>>>(L.T, rows * L.ld, 1);
+    fill_kernel<<<1024, 256>>>(L.Cr, rows * 128, 2);
+    fill_kernel<<<1024, 256>>>(L.P, (int64_t)128 * L.ld, 3);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const double bytes = 16.0 * rows * ncols;
+
+
+
+
+    if (only && !strcmp(only, "lat")) {
+        double* out;
+        CK(hipMalloc(&out, 256 * 8192 * 8));
+        const int iters = 2048;
+        for (int mode = 1; mode <= 2; ++mode)
+            for (int nch : {1, 2, 4, 8})
+                for (int w : {1, 2, 3, 4}) {
+                    const int wg = 256 * w;   // w waves per SIMD
+                    auto go = [&]() {
+#define LK(M, N) lat_kernel<M, N><<<wg, 256>>>(out, 0.5, iters)
+                        if (mode == 1) { if (nch == 1) LK(1, 1); else if (nch == 2) LK(1, 2); else if (nch == 4) LK(1, 4); else LK(1, 8); }
+                        else { if (nch == 1) LK(2, 1); else if (nch == 2) LK(2, 2); else if (nch == 4) LK(2, 4); else LK(2, 8); }
+#undef LK
+                    };
+                    go();
+                    CK(hipDeviceSynchronize());
+                    CK(hipEventRecord(e0, 0));
+                    go();
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    const double fl = 2.0 * 8.0 * nch * iters * wg * 256;
+                    printf("lat %s chains %d waves/SIMD %d: %.1f TF/s\n", mode == 1 ? "fmac_dpp" : "fma     ", nch, w,
+                           fl / ms / 1e9);
+                }
+        return 0;
+    }
+    if (only && !strcmp(only, "valu")) {
+        double* out;
+        CK(hipMalloc(&out, 256 * 8192 * 8));
+        const int iters = 4096;
+        for (int mode = 0; mode < 3; ++mode)
+            for (int wg : {1024, 2048, 4096}) {
+                auto go = [&]() {
+                    if (mode == 0) valu_kernel<0><<<wg, 256>>>(out, 0.5, iters);
+                    else if (mode == 1) valu_kernel<1><<<wg, 256>>>(out, 0.5, iters);
+                    else valu_kernel<2><<<wg, 256>>>(out, 0.5, iters);
+                };
+                go();
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(e0, 0));
+                go();
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double fl = 2.0 * 64.0 * iters * wg * 256;
+                printf("valu mode %d wgs %d: %.3f ms  %.1f TF/s\n", mode, wg, ms, fl / ms / 1e9);
+            }
+        return 0;
+    }
+    if (only && !strcmp(only, "copyp")) {
+        struct C { int U, rb, occ, G, tf; };
+        std::vector<C> cs;
+        for (int U : {1, 2})
+            for (int rb : {8, 16})
+                for (int G : {2, 3, 4, 8})
+                    for (int tf : {1, 0}) cs.push_back({U, rb, U == 1 ? 4 : 2, G, tf});
+        cs.push_back({2, 8, 2, 0, 1});   // G = 0: plain short bands (reference)
+        const int ntile = (int)((L.width + 511) / 512);
+        for (auto& c : cs) {
+            const size_t dyn = c.occ ? (size_t)160 * 1024 / c.occ - 512 : 0;
+            auto go = [&]() {
+                if (c.G == 0) {
+                    dim3 grid((unsigned)ntile, (unsigned)((L.rows + c.rb - 1) / c.rb));
+                    copy_kernel<2><<<grid, 256, dyn>>>(L.T, L.ld, L.rows, L.width, c.rb);
+                    return;
+                }
+                const unsigned nb = (unsigned)(ntile * c.G);
+                if (c.U == 1) copyp_kernel<1><<<nb, 256, dyn>>>(L.T, L.ld, L.rows, L.width, c.rb, c.G, c.tf);
+                else copyp_kernel<2><<<nb, 256, dyn>>>(L.T, L.ld, L.rows, L.width, c.rb, c.G, c.tf);
+            };
+            go();
+            CK(hipDeviceSynchronize());
+            std::vector<float> ms(reps);
+            for (int r = 0; r < reps; ++r) {
+                CK(hipEventRecord(e0, 0));
+                go();
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                CK(hipEventElapsedTime(&ms[r], e0, e1));
+            }
+            std::sort(ms.begin(), ms.end());
+            printf("copyp U=%d rb=%3d occ=%d G=%d tf=%d  median %.3f ms  %6.0f GB/s\n", c.U, c.rb, c.occ, c.G, c.tf,
+                   ms[reps / 2], bytes / ms[reps / 2] / 1e6);
+            fflush(stdout);
+        }
+        return 0;
+    }
+    if (only && !strcmp(only, "copy")) {
+        struct C { int U, rb, occ; };
+        std::vector<C> cs;
+        for (int U : {1, 2, 4, 8})
+            for (int rb : {8, 32, 256})
+                for (int occ : {0, 4, 2})
+                    if (rb % U == 0) cs.push_back({U, rb, occ});
+        for (auto& c : cs) {
+            const size_t dyn = c.occ ? (size_t)160 * 1024 / c.occ - 512 : 0;
+            auto go = [&]() {
+                dim3 grid((unsigned)((L.width + 511) / 512), (unsigned)((L.rows + c.rb - 1) / c.rb));
+                switch (c.U) {
+                    case 1: copy_kernel<1><<<grid, 256, dyn>>>(L.T, L.ld, L.rows, L.width, c.rb); break;
+                    case 2: copy_kernel<2><<<grid, 256, dyn>>>(L.T, L.ld, L.rows, L.width, c.rb); break;
+                    case 4: copy_kernel<4><<<grid, 256, dyn>>>(L.T, L.ld, L.rows, L.width, c.rb); break;
+                    default: copy_kernel<8><<<grid, 256, dyn>>>(L.T, L.ld, L.rows, L.width, c.rb); break;
+                }
+            };
+            go();
+            CK(hipDeviceSynchronize());
+            std::vector<float> ms(reps);
+            for (int r = 0; r < reps; ++r) {
+                CK(hipEventRecord(e0, 0));
+                go();
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                CK(hipEventElapsedTime(&ms[r], e0, e1));
+            }
+            std::sort(ms.begin(), ms.end());
+            printf("copy U=%d rb=%4d occ=%d  median %.3f ms  %6.0f GB/s\n", c.U, c.rb, c.occ, ms[reps / 2],
+                   bytes / ms[reps / 2] / 1e6);
+            fflush(stdout);
+        }
+        return 0;
+    }
+    for (auto& v : vs) {
+        if (only && !strstr(v.name, only)) continue;
+        v.fn(L, v.K, v.rb, 0);   // warm
+        CK(hipDeviceSynchronize());
+        std::vector<float> ms(reps);
+        for (int r = 0; r < reps; ++r) {
+            CK(hipEventRecord(e0, 0));
+            v.fn(L, v.K, v.rb, 0);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&ms[r], e0, e1));
+        }
+        std::vector<float> s = ms;
+        std::sort(s.begin(), s.end());
+        const float med = s[reps / 2];
+        printf("%-28s K=%2d rb=%4d  median %.3f ms  %6.0f GB/s  %.4f ms/step\n", v.name, v.K, v.rb, med,
+               bytes / med / 1e6, med / v.K);
+        fflush(stdout);
+    }
+    return 0;
+}
