@@ -283,8 +283,8 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
     int fused, const double* __restrict__ Cp, const double* __restrict__ Pp, int prev_seal) {
     __shared__ PricePart lds_pp[4];
-    __shared__ double s_cp[kMaxDefer];
-    __shared__ int32_t s_pl[kMaxDefer];
+    __shared__ double s_cp[kMaxReplay];
+    __shared__ int32_t s_pl[kMaxReplay];
     if (st->status != DLP_RUNNING) return;
     const int s = st->blk - 1;
     // replayed steps: the sealed previous block first (lookahead), then this block's s
@@ -1230,7 +1230,8 @@ __global__ __launch_bounds__(256) void pass_r_kernel(double* __restrict__ T, int
 // the eager operation).  1 double x 2 rows per lane, P[0..64) in 128 VGPRs, buffer
 // accesses with one 32-bit column offset per lane: 166 VGPRs, 3 waves per SIMD.
 // Coefficient registers are written only by loads (no VALU write within two
-// instructions of a DPP read: tests/test_isa.py audits the built code object).
+// instructions of a DPP read: tests/test_isa.py audits the built code object).  Partial
+// blocks: ctail_kernel (below) zeroes the unused steps' coefficients in memory first.
 template <int N>
 __device__ __forceinline__ void fmac_bc(double& t, double c, double p) {
     asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
@@ -1241,28 +1242,41 @@ template <int N>
 __device__ __forceinline__ double bc_mov(double v) {
     return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + N, 0xf, 0xf, false);
 }
-// step l of both rows: half h = l / 32, (even, odd) register e = l & 1, lane (l & 31) / 2.
-// PART: the coefficients were masked by VALU selects, so the broadcast goes through the
-// compiler's own v_mov_b64_dpp (it places the hazard wait states) instead of the fused form.
-template <bool PART, int L>
+// step l of both rows: half h = l / 32, (even, odd) register e = l & 1, lane (l & 31) / 2
+template <int L>
 __device__ __forceinline__ void dpp_step(double (&t)[2], const double (&c)[2][2][2], const double (&pr)[64]) {
     constexpr int h = L / 32, e = L & 1, n = (L & 31) >> 1;
-    if constexpr (PART) {
-        const double f0 = bc_mov<n>(c[0][h][e]), f1 = bc_mov<n>(c[1][h][e]);
-        t[0] = __builtin_fma(-f0, pr[L], t[0]);
-        t[1] = __builtin_fma(-f1, pr[L], t[1]);
-    } else {
-        fmac_bc<n>(t[0], c[0][h][e], pr[L]);
-        fmac_bc<n>(t[1], c[1][h][e], pr[L]);
-    }
+    fmac_bc<n>(t[0], c[0][h][e], pr[L]);
+    fmac_bc<n>(t[1], c[1][h][e], pr[L]);
 }
-template <bool PART, int L0, int... I>
+template <int L0, int... I>
 __device__ __forceinline__ void dpp_half(double (&t)[2], const double (&c)[2][2][2], const double (&pr)[64],
                                          std::integer_sequence<int, I...>) {
-    (dpp_step<PART, L0 + I>(t, c, pr), ...);
+    (dpp_step<L0 + I>(t, c, pr), ...);
 }
 
-template <bool NT, bool PART>
+// Form 21's partial blocks (kb < 64) run the full-block code: this kernel first sets the
+// unused steps l >= kb to fma(-(+0), +0, t) = t + (-0) = t (exact for every t): their
+// coefficients to +0 in C (every row, the objective row included) and their pivot rows
+// P[l] to +0.  Nothing else reads C[i][l >= kb] or P[l >= kb] of the block; the next block
+// rewrites both from step 0.
+__global__ __launch_bounds__(256) void ctail_kernel(const BlockDesc* __restrict__ bd, double* __restrict__ C,
+                                                    int64_t ldc, int64_t nrows, double* __restrict__ P,
+                                                    int64_t ld, int K) {
+    const int kb = bd->blk;
+    if (kb >= K) return;
+    const int w = K - kb;
+    const int64_t nc = nrows * w, np = (int64_t)w * ld;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nc + np;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        if (e < nc)
+            C[(e / w) * ldc + kb + e % w] = 0.0;
+        else
+            P[(int64_t)kb * ld + (e - nc)] = 0.0;
+    }
+}
+
+template <bool NT>
 __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ T, double* __restrict__ Tout,
                                                      int64_t ld, int64_t rows, int64_t width,
                                                      const BlockDesc* __restrict__ bd,
@@ -1273,16 +1287,13 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
     __shared__ int32_t cls[1024];
     const int kb = bd->blk;
     const bool outplace = Tout != T;
-    if ((kb == 0 && !outplace) || (PART ? kb == K : kb != K)) return;
+    if (kb == 0 && !outplace) return;   // full and partial blocks alike (ctail_kernel)
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const bool colok = j < width;
     const int jc = (int)(colok ? j : width - 1);
-    double pr[K];
+    double pr[K];   // all 64 rows: a partial block's P[l >= kb] is +0 (ctail_kernel)
 #pragma unroll
-    for (int l = 0; l < K; ++l) {
-        const double v = P[(int64_t)(l < kb ? l : 0) * ld + jc];
-        pr[l] = l < kb ? v : 0.0;
-    }
+    for (int l = 0; l < K; ++l) pr[l] = P[(int64_t)l * ld + jc];
     const int64_t i0 = (int64_t)blockIdx.y * rb;
     const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
     const int nr = (int)(iend - i0);
@@ -1306,8 +1317,7 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
     const int voff = jc * 8;
     const int soff_bad = 0x7fffff00;
     const int voff_st = colok ? voff : soff_bad;
-    const int n16 = threadIdx.x & 15;
-    const int coff = n16 * 16;
+    const int coff = (threadIdx.x & 15) * 16;
     auto dense_at = [&](int r0) {
         if (r0 + U > nr) return false;
         return cls[r0] == kDense && cls[r0 + 1] == kDense;
@@ -1320,11 +1330,6 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
             const d2 v = __builtin_bit_cast(d2, x);
             c[u][h][0] = v.x;
             c[u][h][1] = v.y;
-            if constexpr (PART) {   // steps >= kb: +0, so fma(-(+0), +0, t) = t for every t
-                const int s0 = h * 32 + 2 * n16;
-                c[u][h][0] = s0 < kb ? c[u][h][0] : 0.0;
-                c[u][h][1] = s0 + 1 < kb ? c[u][h][1] : 0.0;
-            }
         }
     };
     auto loadt = [&](double (&t)[U], int r0) {
@@ -1340,11 +1345,11 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
     auto group = [&](double (&t)[U], double (&tn)[U], int r0, int rn) {
         loadt(tn, rn);
         __builtin_amdgcn_sched_barrier(0);
-        dpp_half<PART, 0>(t, c, pr, std::make_integer_sequence<int, 32>{});
+        dpp_half<0>(t, c, pr, std::make_integer_sequence<int, 32>{});
         __builtin_amdgcn_sched_barrier(0);
         loadc(rn, 0);
         __builtin_amdgcn_sched_barrier(0);
-        dpp_half<PART, 32>(t, c, pr, std::make_integer_sequence<int, 32>{});
+        dpp_half<32>(t, c, pr, std::make_integer_sequence<int, 32>{});
         __builtin_amdgcn_sched_barrier(0);
         loadc(rn, 1);
         __builtin_amdgcn_sched_barrier(0);
@@ -1429,7 +1434,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
     nblocks = ratio_defer_blocks(g);
-    if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxDefer)) return hipErrorInvalidValue;
+    if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     const double* Ccp = prev_seal >= 0 ? prev->Cc : nullptr;
     const double* Pp = prev_seal >= 0 ? prev->P : nullptr;
     const int steps = prev_seal >= 0 ? 2 * d.K : d.K;   // at most kp + j replayed steps
@@ -1444,8 +1449,10 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
         DLP_RATIO_DEFER(16);
     else if (steps <= 32)
         DLP_RATIO_DEFER(32);
-    else
+    else if (steps <= 64)
         DLP_RATIO_DEFER(64);
+    else
+        DLP_RATIO_DEFER(128);   // lookahead at K = 64
 #undef DLP_RATIO_DEFER
     return hipGetLastError();
 }
@@ -1485,7 +1492,7 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                              int64_t log_cap, int nranks, hipStream_t s, const Defer* prev,
                              int prev_seal) {
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
-    if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxDefer)) return hipErrorInvalidValue;
+    if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
                                              d.P, prow_bits, pp, tol_dj, log, log_cap,
                                              nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
@@ -1554,7 +1561,8 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             return hipGetLastError();
         }
     }
-    if (d.form == 21 && K == 64 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31) &&
+    // (d.K == 64 exactly: the kernel addresses C with 64 steps per row, ldc == 64)
+    if (d.form == 21 && K == 64 && d.K == 64 && d.ldc == 64 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31) &&
         (int64_t)rb * d.ldc * 8 < ((int64_t)1 << 31)) {
         // DPP-coefficient pass (K = 64 blocks; 1 double per lane: 256-column tiles)
         if constexpr (K == 64) {
@@ -1562,10 +1570,10 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             if (occ > 0) dyn = (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t);
             const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
             if (g.rows > 0) {
-                pass_d_kernel<NT, false><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
-                                                                d.P, d.nzc, rb);
-                pass_d_kernel<NT, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
-                                                               d.P, d.nzc, rb);
+                const BlockDesc* bdc = bd;
+                ctail_kernel<<<1024, 256, 0, s>>>(bdc, d.C, d.ldc, g.rows + 1, d.P, g.ld, K);
+                pass_d_kernel<NT><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P,
+                                                         d.nzc, rb);
             }
             if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
             return hipGetLastError();

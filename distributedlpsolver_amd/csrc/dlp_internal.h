@@ -22,6 +22,7 @@ constexpr int32_t kNoIndex = 0x7fffffff;
 constexpr int kColqPad = 16;   // colq allocated with rows + 1 + kColqPad entries
 constexpr int32_t kStatusSkip = 5;   // DevState.status: redundant row, forced pivot skipped
 constexpr int kMaxDefer = 64;        // deferred rank-k update: at most 64 pivots per tableau pass
+constexpr int kMaxReplay = 2 * kMaxDefer;   // steps a selection replays (lookahead: the sealed block + its own)
 constexpr int kDeferTile = 512;      // deferred kernels: 256 lanes x 2 doubles per column tile
 
 // Pricing partial of one column tile of the objective row.

@@ -378,9 +378,12 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
             }
             s->cluster = s->cl_wg > 0;
         }
+        // streaming tableaus: 64-step blocks through the DPP-coefficient pass (form 21: C3
+        // 8.4 ms per 64-step pass = 0.131 ms per step against 0.197 for form 4's 32-step
+        // pass, 6,100 vs 4,500 pivots/s; profiles/r02j/)
         if (K == 0)
             K = (host_driven || tile != dlp::kDeferTile || tiny || s->cluster) ? 1
-                                                                             : (s->streaming ? 32 : 16);
+                                                                             : (s->streaming ? 64 : 16);
         if (s->cluster && K != 1) s->cluster = false;
         if (K > 1 && tile != dlp::kDeferTile) {
             set_error("defer > 1 needs a 512-column update variant");
@@ -398,7 +401,8 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         // profiles/r02c/) at K = 32 on a streaming tableau and K = 16 on a cache-resident one
         // (C2: pass 0.116 vs 0.128 ms for form 3, profiles/r02b/tune_c2_forms.txt); 1 double
         // x 4 rows elsewhere (K = 16 streaming: form 3 6.1 ms vs form 4 6.4, r01g)
-        s->d.form = ((K == 32 && s->streaming) || (K == 16 && !s->streaming)) ? 4 : 3;
+        s->d.form = (K == 64 && s->streaming) ? 21
+                    : ((K == 32 && s->streaming) || (K == 16 && !s->streaming)) ? 4 : 3;
     }
     g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block : auto_rows_per_block(s);
     g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
@@ -488,7 +492,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     // any) driven by the session, no per-phase timing, and room for a second tableau
     {
         const bool host_driven = nranks > 1 && !rccl;
-        bool ok = s->d.K > 1 && 2 * s->d.K <= dlp::kMaxDefer && dlp::lookahead_form(s->d.form) &&
+        bool ok = s->d.K > 1 && 2 * s->d.K <= dlp::kMaxReplay && dlp::lookahead_form(s->d.form) &&
                   !s->general && !s->cluster && !host_driven && opt->timing < 2;
         size_t freeb = 0, totalb = 0;
         if (ok && hipMemGetInfo(&freeb, &totalb) == hipSuccess)
@@ -499,7 +503,12 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         // hides (C3 17 GB: 4,492 -> 4,935 pivots/s).  Below that the chain, slowed by
         // the concurrent pass and by replaying two blocks, costs more than the pass it
         // hides (C2 268 MB: 39.0k -> 30.2k; profiles/r02h/)
-        const bool want = opt->lookahead == 1 || (opt->lookahead < 0 && tbytes >= ((size_t)4 << 30));
+        // Auto stays off at K = 64: the 128-step selection kernel (256 VGPRs) cannot share
+        // a CU with the form-21 pass (3 waves x 160 VGPRs per SIMD), so each selection
+        // waits for pass workgroups to drain (C3: 171 us per selection, 5,473 vs 6,100
+        // pivots/s without lookahead; profiles/r02j/)
+        const bool want = opt->lookahead == 1 ||
+                          (opt->lookahead < 0 && tbytes >= ((size_t)4 << 30) && s->d.K <= 32);
         if (ok && want) {
             if (hipMalloc(&s->Tb[1], tbytes) != hipSuccess) {
                 set_error("hipMalloc of the second tableau buffer failed");

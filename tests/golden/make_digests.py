@@ -7,10 +7,12 @@ for the GPU to reproduce.  Run in the build container (CPU only):
 
   c2  C2 4096 x 4096 seed 2 (dense family) solved to optimality by the oracle:
       pivot count, status, sha256 of the pivot log / x / y, objective bits.
-  c3  C3 32768 x 32768 seed 3: the exact pivot sequence of the default
-      bench.py run (5 warm-up + 20 timed blocks of K = 32 pivots, then a
+  c3  C3 32768 x 32768 seed 3: the exact pivot sequence of round 2's first
+      bench.py default (5 warm-up + 20 timed blocks of K = 32 pivots, then a
       20-pivot window = 820 pivots): sha256 of the log, the objective row and
       sampled constraint rows after those pivots.
+  c3_k64  the same LP through the current default (K = 64 blocks: 5 + 20 blocks
+      of 64 pivots, then the 20-pivot window = 1620 pivots).
 
 The digests hash little-endian fp64 / int32 bytes of the oracle's outputs
 (tests/oracle_py.py), so the GPU side compares bit for bit."""
@@ -28,6 +30,7 @@ import oracle_py as O  # noqa: E402
 
 OUT = os.path.join(HERE, "digests.json")
 C3_PIVOTS = 5 * 32 + 20 * 32 + 20
+C3_K64_PIVOTS = 5 * 64 + 20 * 64 + 20
 C3_ROWS = [0, 1, 777, 12345, 20000, 32767]
 
 
@@ -46,14 +49,14 @@ def c2():
             "oracle_seconds": time.time() - t0}
 
 
-def c3():
+def c3(pivots=C3_PIVOTS):
     m = n = 32768
     t0 = time.time()
     rows = np.array(C3_ROWS + [m], np.int64)   # + the objective row
-    log, out, basis = O.run_generated(m, n, 3, C3_PIVOTS, rows, nthreads=os.cpu_count() or 8)
+    log, out, basis = O.run_generated(m, n, 3, pivots, rows, nthreads=os.cpu_count() or 8)
     w = ((n + m + 1) + 15) // 16 * 16
     return {"m": m, "n": n, "seed": 3, "pivots": int(len(log)), "log_sha256": sha(log),
-            "log_prefix_sha256": {str(k): sha(log[:k]) for k in (160, 800)},
+            "log_prefix_sha256": {str(k): sha(log[:k]) for k in (160, 800, 820, 1600) if k <= len(log)},
             "objective_hex": float(log[-1]["objective"]).hex(),
             "rows": C3_ROWS, "width": w,
             "row_sha256": {str(i): sha(out[k, :w]) for k, i in enumerate(C3_ROWS)},
@@ -68,7 +71,7 @@ def main():
         with open(OUT) as f:
             d = json.load(f)
     for w in which:
-        d[w] = {"c2": c2, "c3": c3}[w]()
+        d[w] = {"c2": c2, "c3": c3, "c3_k64": lambda: c3(C3_K64_PIVOTS)}[w]()
         with open(OUT, "w") as f:
             json.dump(d, f, indent=1)
         print(w, json.dumps(d[w]), flush=True)

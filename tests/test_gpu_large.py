@@ -75,17 +75,20 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K):
+def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0):
     """k pivots in windows of ci (whole K-blocks, then a tail) through the auto
     geometry of the bench (deferred K, pass form, band rows, ld alignment);
     the whole pivot log, every pivot row, random rows and the objective row
     against the oracle on the same generated LP, byte for byte."""
     rng = np.random.default_rng(seed)
-    with dlp.Session(dlp.Problem.random(m, n, seed), check_interval=ci) as s:
+    with dlp.Session(dlp.Problem.random(m, n, seed), check_interval=ci, defer=defer) as s:
         occ, form, K = s.get_defer_tuning()
         assert K == want_K
+        if K == 64:
+            assert form == 21 and s.get_tuning()[1] == 256   # the bench's pass
+            assert not s.lookahead()   # auto off at K = 64 (DESIGN.md §13)
         if K == 32:
-            assert form == 4 and s.get_tuning()[1] == 256   # the bench's pass
+            assert form == 4 and s.get_tuning()[1] == 256   # round 2's first default
             assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
         done = 0
         while done < k:
@@ -112,10 +115,15 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K):
 
 
 def test_c3_full_blocks_bit_exact():
-    """C3 at the bench geometry: 2 full K = 32 blocks through the full-block
-    pass instance (form 4, 256-row bands, ld 66048, nt), then an 8-pivot
-    tail through the partial-block instance."""
-    _full_blocks_vs_oracle(32768, 32768, 3, 72, 64, 32)
+    """C3 at the bench geometry: 2 full K = 64 blocks through the form-21 pass
+    (DPP coefficients, 256-row bands, ld 66048, nt), then an 8-pivot tail (a
+    partial block: coefficients of the unused steps zeroed in memory)."""
+    _full_blocks_vs_oracle(32768, 32768, 3, 136, 128, 64)
+
+
+def test_c3_k32_lookahead_full_blocks_bit_exact():
+    """C3 with K = 32 (form 4, lookahead auto-on): 2 full blocks and an 8-pivot tail."""
+    _full_blocks_vs_oracle(32768, 32768, 3, 72, 64, 32, defer=32)
 
 
 def test_c2_full_blocks_bit_exact():
@@ -123,18 +131,19 @@ def test_c2_full_blocks_bit_exact():
     _full_blocks_vs_oracle(4096, 4096, 2, 40, 32, 16)
 
 
-def test_c3_bench_window_digest():
+@pytest.mark.parametrize("K", [64, 32])
+def test_c3_bench_window_digest(K):
     """The exact pivot sequence of the default bench.py run (5 warm-up + 20
-    timed blocks of 32 pivots, then the 20-pivot window) against digests of
-    the oracle's run committed in tests/golden/digests.json
-    (tests/golden/make_digests.py): log, objective, objective row and sampled
-    constraint rows after 820 pivots, bit for bit."""
-    g = load_golden("digests.json")["c3"]
+    timed blocks of K pivots, then the 20-pivot window; K = 64 is the default,
+    K = 32 with lookahead round 2's first) against digests of the oracle's run
+    committed in tests/golden/digests.json (tests/golden/make_digests.py): log,
+    objective, objective row and sampled constraint rows, bit for bit."""
+    g = load_golden("digests.json")["c3_k64" if K == 64 else "c3"]
     m, n = g["m"], g["n"]
     with dlp.Session(dlp.Problem.random(m, n, g["seed"]), check_interval=64 * 20, timing=1,
-                     max_pivots=64 * 25 + 22) as s:
-        assert s.get_defer_tuning()[2] == 32 and s.lookahead()
-        for k in (160, 640, 20):
+                     max_pivots=64 * 25 + 22, defer=0 if K == 64 else 32) as s:
+        assert s.get_defer_tuning()[2] == K and s.lookahead() == (K == 32)
+        for k in (5 * K, 20 * K, 20):
             st, d = s.run(k)
             assert st == L.RUNNING and d == k
         res = s.result()

@@ -34,7 +34,7 @@ def _check(res, ref):
     assert res.basis.tobytes() == ref.basis.tobytes()
 
 
-@pytest.mark.parametrize("K", [2, 5, 8, 16, 32])
+@pytest.mark.parametrize("K", [2, 5, 8, 16, 32, 64])
 @pytest.mark.parametrize("ci", [3, 16, 64, 100])
 def test_lookahead_full_solve(K, ci):
     """Full solve (353 pivots) against the oracle; windows of ci pivots, so blocks
@@ -78,6 +78,31 @@ def test_lookahead_tableau(K, rb, nt, form, ci):
         s.set_defer_tuning(0, form)
         assert s.lookahead()
         s.run(45)
+        Td = s.tableau()
+        ld = s.result().pivot_log
+    _same_log(ld, le)
+    assert Td.tobytes() == Te.tobytes()
+
+
+@pytest.mark.parametrize("form,rb,nt,ci", [(21, 256, 1, 64), (21, 37, 0, 100), (3, 64, 1, 64), (21, 1000, 1, 30)])
+def test_lookahead_k64_tableau(form, rb, nt, ci):
+    """K = 64 under lookahead: selections replay up to 127 steps (the sealed block in
+    flight + their own), the 128-step ratio kernel; two full blocks and a partial one,
+    windows ending inside blocks; whole tableau byte-equal to the eager session's."""
+    m, n, seed = 700, 1337, 7
+    k = 2 * 64 + 17
+    prob = dlp.Problem.random(m, n, seed)
+    with dlp.Session(prob, defer=1, check_interval=k) as e:
+        e.run(k)
+        Te = e.tableau()
+        le = e.result().pivot_log
+    with dlp.Session(prob, defer=64, check_interval=ci, rows_per_block=rb, nontemporal=nt,
+                     lookahead=1) as s:
+        s.set_defer_tuning(0, form)
+        assert s.lookahead()
+        done = 0
+        while done < k:
+            done += s.run(min(ci, k - done))[1]
         Td = s.tableau()
         ld = s.result().pivot_log
     _same_log(ld, le)
