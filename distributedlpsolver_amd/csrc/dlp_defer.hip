@@ -89,7 +89,30 @@ __device__ inline void release_go(DevState* st) {
     __hip_atomic_store(&st->go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int KMAX, bool FUSED>
+// Block reductions through an LDS tree (LEAN kernels: fewer VGPRs than the wave shuffles of
+// block_cand / block_price).  Both orders are total, so the winner is the same.
+template <typename T, typename Better>
+__device__ inline T block_tree(T v, T* s, Better better) {
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) {
+            const T o = s[threadIdx.x + h];
+            if (better(o, s[threadIdx.x])) s[threadIdx.x] = o;
+        }
+        __syncthreads();
+    }
+    const T r = s[0];
+    __syncthreads();
+    return r;
+}
+
+// LEAN (lookahead beside the form-21 pass): no register-resident chain (coefficients in
+// pairs during the replay) and LDS-tree block reductions, 23 VGPRs, so the kernel fits in
+// the 32 VGPRs per SIMD that three pass waves (3 x 160) leave free.  Same operations in
+// the same order.  (Staging the chain in LDS by LDS-DMA, 32 steps per round trip, measured
+// no faster beside the pass: 96 vs 95 us per selection, profiles/r02j/.)
+template <int KMAX, bool FUSED, bool LEAN = false>
 __device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
@@ -103,6 +126,14 @@ __device__ __forceinline__ void ratio_defer_body(
     __shared__ int s_last;
     __shared__ double s_pq[KMAX], s_pn[KMAX];
     __shared__ int32_t s_pl[KMAX];
+    __shared__ Cand s_ct[LEAN ? kRatioDeferThreads : 1];
+    __shared__ PricePart s_pt[LEAN ? kRatioDeferThreads : 1];
+    auto cand_red = [&](Cand v) {
+        if constexpr (LEAN)
+            return block_tree(v, s_ct, [](const Cand& x, const Cand& y) { return cand_better(x, y); });
+        else
+            return block_cand(v, lds_c);
+    };
     if (st->status != DLP_RUNNING) return;
 
     // replayed steps: the sealed previous block (lookahead: not yet applied to T, its kp
@@ -116,10 +147,13 @@ __device__ __forceinline__ void ratio_defer_body(
         s_pl[l] = l < kp ? st->seal[prev_seal].pl[l] : st->pl[l - kp];
     }
     const int64_t ic = i < rows ? i : rows;   // clamped: loads need no guard
-    double f[KMAX];
+    double f[LEAN ? 1 : KMAX];
+    if constexpr (!LEAN) {
 #pragma unroll
-    for (int l = 0; l < KMAX; ++l)
-        f[l] = (l < J) ? (l < kp ? Ccp[(int64_t)l * ldcc + ic] : Cc[(int64_t)(l - kp) * ldcc + ic]) : 0.0;
+        for (int l = 0; l < KMAX; ++l)
+            f[l] = (l < J) ? (l < kp ? Ccp[(int64_t)l * ldcc + ic] : Cc[(int64_t)(l - kp) * ldcc + ic]) : 0.0;
+    }
+    auto fld = [&](int l) { return l < kp ? Ccp[(int64_t)l * ldcc + ic] : Cc[(int64_t)(l - kp) * ldcc + ic]; };
     double r_in = 0.0;
     int32_t nz_in = 0, bvar = 0;
     if (i < rows && j > 0) nz_in = nzc[i];
@@ -130,7 +164,23 @@ __device__ __forceinline__ void ratio_defer_body(
 
     PricePart acc = pp_empty();
     for (int k = threadIdx.x; k < ntiles; k += blockDim.x) pp_combine(acc, pp[k]);
-    acc = block_price(acc, lds_pp);
+    if constexpr (LEAN) {
+        // the tree keeps one side per pair: pp_combine's outcome, as a "better" test
+        s_pt[threadIdx.x] = acc;
+        __syncthreads();
+        for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+            if ((int)threadIdx.x < h) {
+                PricePart x = s_pt[threadIdx.x];
+                pp_combine(x, s_pt[threadIdx.x + h]);
+                s_pt[threadIdx.x] = x;
+            }
+            __syncthreads();
+        }
+        acc = s_pt[0];
+        __syncthreads();
+    } else {
+        acc = block_price(acc, lds_pp);
+    }
     int32_t q;
     if (st->bland)
         q = acc.jbland;
@@ -150,16 +200,39 @@ __device__ __forceinline__ void ratio_defer_body(
     __syncthreads();
 
     Cand c = cand_empty();
-    if (i <= rows) {
-        double a = T[i * ld + q];
-        if (i < rows) {
+    double a = i <= rows ? T[i * ld + q] : 0.0;
+    double flast = 0.0;   // LEAN: C of step J-1 (the RHS cache's step)
+    if constexpr (LEAN) {
+        // pairs of coefficient loads per round trip (the register budget of this kernel)
+        if (i < rows)
+            for (int l0 = 0; l0 < J; l0 += 2) {
+                const double f0 = fld(l0), f1 = l0 + 1 < J ? fld(l0 + 1) : 0.0;
 #pragma unroll
-            for (int l = 0; l < KMAX; ++l) {
-                if (l < J) {
-                    if (i == s_pl[l])
-                        a = s_pq[l];
-                    else if (f[l] != 0.0)
-                        a = __builtin_fma(-f[l], s_pq[l], a);
+                for (int u = 0; u < 2; ++u) {
+                    const int l = l0 + u;
+                    const double fv = u ? f1 : f0;
+                    if (l < J) {
+                        if (i == s_pl[l])
+                            a = s_pq[l];
+                        else if (fv != 0.0)
+                            a = __builtin_fma(-fv, s_pq[l], a);
+                        flast = fv;
+                    }
+                }
+            }
+    }
+    if (i <= rows) {
+        if (i < rows) {
+            if constexpr (LEAN) {
+            } else {
+#pragma unroll
+                for (int l = 0; l < KMAX; ++l) {
+                    if (l < J) {
+                        if (i == s_pl[l])
+                            a = s_pq[l];
+                        else if (f[l] != 0.0)
+                            a = __builtin_fma(-f[l], s_pq[l], a);
+                    }
                 }
             }
         }
@@ -171,8 +244,12 @@ __device__ __forceinline__ void ratio_defer_body(
             if (J > 0) {
                 const int l = J - 1;
                 double fp = 0.0;   // f[j-1], selected without dynamic register indexing
+                if constexpr (LEAN) {
+                    fp = flast;
+                } else {
 #pragma unroll
-                for (int u = 0; u < KMAX; ++u) fp = (u == l) ? f[u] : fp;
+                    for (int u = 0; u < KMAX; ++u) fp = (u == l) ? f[u] : fp;
+                }
                 if (i == s_pl[l])
                     r = s_pn[l];
                 else if (fp != 0.0)
@@ -190,7 +267,7 @@ __device__ __forceinline__ void ratio_defer_body(
             }
         }
     }
-    c = block_cand(c, lds_c);
+    c = cand_red(c);
 
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)partials, (short)0, (int)(nblocks * sizeof(Cand)), 0x00020000);
@@ -214,7 +291,7 @@ __device__ __forceinline__ void ratio_defer_body(
         ov[1] = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(k * sizeof(Cand)) + 16, 0, kAuxSc1);
         if (cand_better(o, best)) best = o;
     }
-    best = block_cand(best, lds_c);
+    best = cand_red(best);
     if (threadIdx.x == 0) {
         st->ticket = 0;
         st->q = q;
@@ -241,6 +318,21 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     ratio_defer_body<KMAX, false>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                   ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                   tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal);
+}
+
+// The LEAN selection kernel, held to 32 VGPRs (lookahead at K = 64, beside the pass).
+template <int KMAX>
+__global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(32))) void ratio_lean_kernel(
+    const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
+    int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
+    DevState* st, double* __restrict__ C, int64_t ldc, double* __restrict__ Cc, int64_t ldcc,
+    const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
+    Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
+    dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
+    int prev_seal) {
+    ratio_defer_body<KMAX, false, true>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
+                                        ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
+                                        tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal);
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
@@ -277,6 +369,7 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
 // T0[p], divided by the pivot element (IEEE division).  fused (single rank):
 // commit_row as well.  Otherwise the owner writes the fp64 bits and every
 // other rank INT64_MIN for the int64 MAX exchange.
+template <bool LEAN = false>
 __global__ __launch_bounds__(256) void prow_defer_kernel(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
@@ -303,16 +396,18 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     pr.y = 0.0;
     if (pl >= 0 && j < ld) {
         d2 t = *(const d2*)(T + (int64_t)pl * ld + j);
-        // chunks of 8 pivot rows: loads issued back to back (row index clamped), then applied in order
-        for (int l0 = 0; l0 < S; l0 += 8) {
-            d2 pv[8];
+        // chunks of CH pivot rows: loads issued back to back (row index clamped), then applied
+        // in order (LEAN, lookahead beside the form-21 pass: 2 rows, 21 VGPRs)
+        constexpr int CH = LEAN ? 2 : 8;
+        for (int l0 = 0; l0 < S; l0 += CH) {
+            d2 pv[CH];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < CH; ++u) {
                 const int l = min(l0 + u, S - 1);
                 pv[u] = *(const d2*)((l < kp ? Pp + (int64_t)l * ld : P + (int64_t)(l - kp) * ld) + j);
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < CH; ++u) {
                 const int l = l0 + u;
                 if (l < S) {
                     if (pl == s_pl[l]) {
@@ -1451,8 +1546,11 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
         DLP_RATIO_DEFER(32);
     else if (steps <= 64)
         DLP_RATIO_DEFER(64);
-    else
-        DLP_RATIO_DEFER(128);   // lookahead at K = 64
+    else   // lookahead at K = 64, beside the form-21 pass
+        ratio_lean_kernel<128><<<nblocks, kRatioDeferThreads, 0, s>>>(
+            g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc,
+            d.ldcc, d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp,
+            Pp, prev_seal);
 #undef DLP_RATIO_DEFER
     return hipGetLastError();
 }
@@ -1493,10 +1591,15 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                              int prev_seal) {
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
-    prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
-                                             d.P, prow_bits, pp, tol_dj, log, log_cap,
-                                             nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
-                                             prev_seal >= 0 ? prev->P : nullptr, prev_seal);
+    if (prev_seal >= 0 && d.K > 32)   // lookahead at K = 64: beside the form-21 pass
+        prow_defer_kernel<true><<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
+                                                     d.P, prow_bits, pp, tol_dj, log, log_cap,
+                                                     nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal);
+    else
+        prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
+                                                 d.P, prow_bits, pp, tol_dj, log, log_cap,
+                                                 nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
+                                                 prev_seal >= 0 ? prev->P : nullptr, prev_seal);
     return hipGetLastError();
 }
 

@@ -503,12 +503,11 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         // hides (C3 17 GB: 4,492 -> 4,935 pivots/s).  Below that the chain, slowed by
         // the concurrent pass and by replaying two blocks, costs more than the pass it
         // hides (C2 268 MB: 39.0k -> 30.2k; profiles/r02h/)
-        // Auto stays off at K = 64: the 128-step selection kernel (256 VGPRs) cannot share
-        // a CU with the form-21 pass (3 waves x 160 VGPRs per SIMD), so each selection
-        // waits for pass workgroups to drain (C3: 171 us per selection, 5,473 vs 6,100
-        // pivots/s without lookahead; profiles/r02j/)
-        const bool want = opt->lookahead == 1 ||
-                          (opt->lookahead < 0 && tbytes >= ((size_t)4 << 30) && s->d.K <= 32);
+        // At K = 64 the selections replay up to 127 steps through the LEAN kernels (23 and
+        // 21 VGPRs), which fit beside the form-21 pass (3 waves x 160 VGPRs per SIMD); the
+        // 256-VGPR chain kernel waited for pass workgroups to drain instead (C3: lookahead
+        // 6,715 vs 5,970 pivots/s off; 5,473 with the fat kernel; profiles/r02j/)
+        const bool want = opt->lookahead == 1 || (opt->lookahead < 0 && tbytes >= ((size_t)4 << 30));
         if (ok && want) {
             if (hipMalloc(&s->Tb[1], tbytes) != hipSuccess) {
                 set_error("hipMalloc of the second tableau buffer failed");

@@ -86,7 +86,7 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0):
         assert K == want_K
         if K == 64:
             assert form == 21 and s.get_tuning()[1] == 256   # the bench's pass
-            assert not s.lookahead()   # auto off at K = 64
+            assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
         if K == 32:
             assert form == 4 and s.get_tuning()[1] == 256   # round 2's first default
             assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
@@ -142,7 +142,7 @@ def test_c3_bench_window_digest(K):
     m, n = g["m"], g["n"]
     with dlp.Session(dlp.Problem.random(m, n, g["seed"]), check_interval=64 * 20, timing=1,
                      max_pivots=64 * 25 + 22, defer=0 if K == 64 else 32) as s:
-        assert s.get_defer_tuning()[2] == K and s.lookahead() == (K == 32)
+        assert s.get_defer_tuning()[2] == K and s.lookahead()
         for k in (5 * K, 20 * K, 20):
             st, d = s.run(k)
             assert st == L.RUNNING and d == k
