@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <utility>
 
 #include "dlp_internal.h"
@@ -112,7 +113,7 @@ __device__ inline T block_tree(T v, T* s, Better better) {
 // the 32 VGPRs per SIMD that three pass waves (3 x 160) leave free.  Same operations in
 // the same order.  (Staging the chain in LDS by LDS-DMA, 32 steps per round trip, measured
 // no faster beside the pass: 96 vs 95 us per selection, profiles/r02j/.)
-template <int KMAX, bool FUSED, bool LEAN = false>
+template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4>
 __device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
@@ -203,14 +204,16 @@ __device__ __forceinline__ void ratio_defer_body(
     double a = i <= rows ? T[i * ld + q] : 0.0;
     double flast = 0.0;   // LEAN: C of step J-1 (the RHS cache's step)
     if constexpr (LEAN) {
-        // pairs of coefficient loads per round trip (the register budget of this kernel)
+        // LCH coefficient loads per round trip (the register budget of this kernel)
         if (i < rows)
-            for (int l0 = 0; l0 < J; l0 += 2) {
-                const double f0 = fld(l0), f1 = l0 + 1 < J ? fld(l0 + 1) : 0.0;
+            for (int l0 = 0; l0 < J; l0 += LCH) {
+                double fq[LCH];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
+                for (int u = 0; u < LCH; ++u) fq[u] = l0 + u < J ? fld(l0 + u) : 0.0;
+#pragma unroll
+                for (int u = 0; u < LCH; ++u) {
                     const int l = l0 + u;
-                    const double fv = u ? f1 : f0;
+                    const double fv = fq[u];
                     if (l < J) {
                         if (i == s_pl[l])
                             a = s_pq[l];
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
 }
 
 // The LEAN selection kernel, held to 32 VGPRs (lookahead at K = 64, beside the pass).
-template <int KMAX>
+template <int KMAX, int LCH>
 __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(32))) void ratio_lean_kernel(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
     int prev_seal) {
-    ratio_defer_body<KMAX, false, true>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
+    ratio_defer_body<KMAX, false, true, LCH>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                         ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                         tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal);
 }
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
         d2 t = *(const d2*)(T + (int64_t)pl * ld + j);
         // chunks of CH pivot rows: loads issued back to back (row index clamped), then applied
         // in order (LEAN, lookahead beside the form-21 pass: 2 rows, 21 VGPRs)
-        constexpr int CH = LEAN ? 2 : 8;
+        constexpr int CH = LEAN ? 4 : 8;
         for (int l0 = 0; l0 < S; l0 += CH) {
             d2 pv[CH];
 #pragma unroll
@@ -1547,10 +1550,18 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     else if (steps <= 64)
         DLP_RATIO_DEFER(64);
     else   // lookahead at K = 64, beside the form-21 pass
-        ratio_lean_kernel<128><<<nblocks, kRatioDeferThreads, 0, s>>>(
-            g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc,
-            d.ldcc, d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp,
-            Pp, prev_seal);
+    {
+        static const int lch = std::getenv("DLP_LEAN_LCH") ? std::atoi(std::getenv("DLP_LEAN_LCH")) : 4;
+#define DLP_RATIO_LEAN(L)                                                                                  \
+    ratio_lean_kernel<128, L><<<nblocks, kRatioDeferThreads, 0, s>>>(                                       \
+        g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
+        d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal)
+        if (lch == 8)   // tuning only (DLP_LEAN_LCH)
+            DLP_RATIO_LEAN(8);
+        else
+            DLP_RATIO_LEAN(4);
+#undef DLP_RATIO_LEAN
+    }
 #undef DLP_RATIO_DEFER
     return hipGetLastError();
 }
