@@ -141,7 +141,7 @@ typedef struct dlp_options {
                                 -tol_feas * (1 + max_i b'_i) (default 1e-9) */
     int32_t defer;           /* pivots per tableau pass (deferred rank-k update, results
                                 bit-identical to rank-1): 1 = eager rank-1 per pivot, 2..64 =
-                                block size, 0 = auto (default: 32 on a tableau > 1 GiB, 16
+                                block size, 0 = auto (default: 64 on a tableau > 1 GiB, 16
                                 from 32 MiB, eager below 32 MiB and for multi-rank sessions
                                 without an RCCL id, whose exchange the caller drives
                                 through dlp_session_step_*; a single-rank session driven
@@ -155,7 +155,8 @@ typedef struct dlp_options {
     int32_t lookahead;       /* deferred sessions: select block b+1 while the pass of block b
                                 runs, on a second tableau buffer (results unchanged, bit for
                                 bit; 2x the tableau memory): 1 = on where supported, 0 = off,
-                                -1 = auto (default: tableaus of >= 4 GiB that fit twice) */
+                                -1 = auto (default: tableaus of >= 4 GiB that fit twice; at
+                                K = 64 the selections replay up to 127 steps) */
     int32_t pad_;
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
@@ -303,8 +304,12 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
  *   each as {2 doubles x 2 rows, ring 4 (K <= 32); 2 x 2, ring 2 (K <= 32);
  *   1 x 4, ring 4; 1 x 4, ring 2};
  *   14 = form 4 for full blocks + the streamed partial-block kernel (K <= 32),
- *   15 = the same with the full-block kernel held to 3 waves per SIMD.
- * Default: 4 at K = 32 on a tableau > 1 GiB and at K = 16 below, else 3.
+ *   15 = the same with the full-block kernel held to 3 waves per SIMD,
+ *   20 = form 4 with a 3-deep row prefetch ring (K <= 32),
+ *   21 = DPP-broadcast coefficients, 1 double x 2 rows, K = 64 exactly (other K
+ *   run form 3).
+ * Default: 21 at K = 64 on a tableau > 1 GiB, 4 at K = 32 there and at K = 16
+ * below, else 3.
  * rows_per_block (set_tuning) is the pass's row band.  Results are
  * bit-identical for every setting. */
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
@@ -316,7 +321,7 @@ int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
 int dlp_session_set_fused_pivot(dlp_session* s, int on);
 /* *on = 1 when the session runs lookahead (dlp_options.lookahead): block b+1 selected
  * while the pass of block b runs on a second tableau buffer.  The step API and pass
- * forms other than 3, 4, 5 and 20 turn it off for the rest of the session. */
+ * forms other than 3, 4, 5, 20 and 21 turn it off for the rest of the session. */
 int dlp_session_get_lookahead(dlp_session* s, int* on);
 /* Current deferred-pass settings (K = 1: form -1). */
 int dlp_session_get_defer_tuning(dlp_session* s, int* occupancy, int* form, int* K);

@@ -180,8 +180,8 @@ def test_defer_update_stats():
     assert k == 8 and n == 5 and ms > 0
 
 
-@pytest.mark.parametrize("P,K", [(1, 8), (2, 4), (2, 16), (3, 32)])
-def test_defer_step_api_multi_rank_one_gpu(P, K):
+@pytest.mark.parametrize("P,K,form", [(1, 8, -1), (2, 4, -1), (2, 16, -1), (3, 32, -1), (2, 64, 21), (3, 64, 21)])
+def test_defer_step_api_multi_rank_one_gpu(P, K, form):
     """The deferred exchange path (ratio -> candidate all-gather -> select ->
     pivot-row MAX all-reduce -> commit, pass every K pivots) with P row-block
     sessions on one GPU and the host doing the exchanges: the same pivot log,
@@ -193,6 +193,9 @@ def test_defer_step_api_multi_rank_one_gpu(P, K):
     prob = dlp.Problem.random(m, n, seed)
     sess = [dlp.Session(prob, rank=r, nranks=P, defer=K) for r in range(P)]
     assert all(s.update_stats()[2] == K for s in sess)
+    if form >= 0:   # the multi-GPU C3 geometry's pass (K = 64, form 21) on every rank
+        for s in sess:
+            s.set_defer_tuning(0, form)
     status = L.RUNNING
     for _ in range(10_000):
         cands = np.concatenate([s.step_candidate() for s in sess])

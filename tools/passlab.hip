@@ -874,11 +874,295 @@ void launch_f4q(const Lab& L, int, int rb, hipStream_t s) {
     f4q_kernel<true, U, W, CL><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
 }
 
+// Pipelined stages with DPP coefficients: stage s (waves 4s..4s+3) applies steps
+// [32 s, 32 s + 32) with its P slice (32 x 2 columns) in VGPRs; a row's 32 coefficients of
+// the stage are ONE 16-B load per lane (lane n of each 16-lane row: steps 2n, 2n+1);
+// stage 0 loads rows from HBM, stage S-1 stores, groups handed on through LDS slots.
+template <int U, int... I>
+__device__ __forceinline__ void pstep_all(double (&t)[U][2], const double (&c)[U][2], const double (&pr)[32][2],
+                                          std::integer_sequence<int, I...>) {
+    // I = m * U + u: step m of the stage for row u
+    ((fmac_bc<((I / U) >> 1)>(t[I % U][0], c[I % U][(I / U) & 1], pr[I / U][0]),
+      fmac_bc<((I / U) >> 1)>(t[I % U][1], c[I % U][(I / U) & 1], pr[I / U][1])), ...);
+}
+template <bool NT, int S, int U>
+__global__ __launch_bounds__(256 * S) void piped_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                        int64_t ld, int64_t rows, int64_t width,
+                                                        const double* __restrict__ Cr, const double* __restrict__ P,
+                                                        int rb) {
+    constexpr int K = 32 * S;
+    __shared__ d2 slot[(S > 1 ? S - 1 : 1)][2][U][256];
+    const int st = S == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+    const int tid = threadIdx.x & 255;
+    const int64_t j = (int64_t)blockIdx.x * 512 + tid * 2;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 2;
+    double pr[32][2];
+#pragma unroll
+    for (int l = 0; l < 32; ++l) {
+        const d2 v = *(const d2*)(P + (int64_t)(st * 32 + l) * ld + jc);
+        pr[l][0] = v.x;
+        pr[l][1] = v.y;
+    }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int ng = (int)((iend - i0) / U);
+    const int n16 = threadIdx.x & 15;
+    auto loadc = [&](double (&c)[U][2], int g) {
+        const int gg = g < ng ? g : ng - 1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const d2 v = *(const d2*)(Cr + (i0 + (int64_t)gg * U + u) * K + st * 32 + 2 * n16);
+            c[u][0] = v.x;
+            c[u][1] = v.y;
+        }
+    };
+    auto load = [&](double (&t)[U][2], int g) {
+        const int gg = g < ng ? g : ng - 1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const d2 v = ldv<NT>(T + (i0 + (int64_t)gg * U + u) * ld + jc);
+            t[u][0] = v.x;
+            t[u][1] = v.y;
+        }
+    };
+    double ta[U][2], tb[U][2], ca[U][2], cb[U][2];
+    if (st == 0) load(ta, 0);
+    loadc(ca, 0 - 0);   // this stage's first group is g = 0 (reached at iteration st)
+    const int total = ng + S - 1;
+    for (int k = 0; k < total; k += 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kk = k + h;
+            double (&cur)[U][2] = h == 0 ? ta : tb;
+            double (&nxt)[U][2] = h == 0 ? tb : ta;
+            double (&cc)[U][2] = h == 0 ? ca : cb;
+            double (&cn)[U][2] = h == 0 ? cb : ca;
+            const int g = kk - st;
+            if (kk < total && g >= 0 && g < ng) {
+                if (st == 0) load(nxt, g + 1);
+                loadc(cn, g + 1);
+                if (st > 0) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const d2 v = slot[st - 1][g & 1][u][tid];
+                        cur[u][0] = v.x;
+                        cur[u][1] = v.y;
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                pstep_all<U>(cur, cc, pr, std::make_integer_sequence<int, 32 * U>{});
+                __builtin_amdgcn_sched_barrier(0);
+                if (st == S - 1) {
+                    if (colok)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            d2 v;
+                            v.x = cur[u][0];
+                            v.y = cur[u][1];
+                            stv<NT>(To + (i0 + (int64_t)g * U + u) * ld + j, v);
+                        }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        d2 v;
+                        v.x = cur[u][0];
+                        v.y = cur[u][1];
+                        slot[st][g & 1][u][tid] = v;
+                    }
+                }
+            } else if (kk < total && g < 0) {
+                // stages > 0 idle until their first group; keep the coefficient ping-pong aligned
+#pragma unroll
+                for (int u = 0; u < U; ++u) { cn[u][0] = cc[u][0]; cn[u][1] = cc[u][1]; }
+            }
+            if (S > 1 && kk < total) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    }
+}
+template <int S, int U>
+void launch_piped(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 511) / 512), (unsigned)((L.rows + rb - 1) / rb));
+    piped_kernel<true, S, U><<<grid, 256 * S, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
+// MFMA pass (v_mfma_f64_16x16x4f64 rounds as four sequential fmas in k order:
+// tools/mfma_probe.hip).  Workgroup = 4 waves on one tile of 16*NT columns; the tile's
+// P slab [K][16 NT] in LDS; wave w takes 16-row groups w, w+4, ... of the band.  Per
+// group: acc tiles = T (accumulator layout: lane l, reg i -> row l/16 + 4i, column l%16),
+// then for kblock b (steps 4b..4b+3) and tile t: acc[t] = mfma(-C frag, P frag, acc[t]).
+// Coefficients are read in the permuted layout Cm[row][q*(K/4) + b] = C[row][4b + q] so
+// that lane (r = l%16, q = l/16) reads its K/4 values contiguously.
+typedef double d4 __attribute__((ext_vector_type(4)));
+template <int K, int NT>
+__global__ __launch_bounds__(256) void mpass_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                    int64_t ld, int64_t rows, int64_t width,
+                                                    const double* __restrict__ Cm, const double* __restrict__ P,
+                                                    int rb) {
+    constexpr int W = 16 * NT, KB = K / 4;
+    __shared__ double Ps[K * W];
+    const int64_t c0 = (int64_t)blockIdx.x * W;
+    for (int e = threadIdx.x; e < K * W; e += 256) {
+        const int l = e / W, c = e % W;
+        const int64_t cc = c0 + c < width ? c0 + c : width - 1;
+        Ps[e] = P[(int64_t)l * ld + cc];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lr = lane & 15, lq = lane >> 4;
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int ng = (int)((iend - i0) / 16);
+    for (int g = w; g < ng; g += 4) {
+        const int64_t r0 = i0 + (int64_t)g * 16;
+        d4 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            const int64_t cc = col < width ? col : width - 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[t][i] = __builtin_nontemporal_load(T + (r0 + lq + 4 * i) * ld + cc);
+        }
+        double a[KB];
+        const double* cp = Cm + (r0 + lr) * K + lq * KB;
+#pragma unroll
+        for (int b = 0; b < KB; b += 2) {
+            const d2 v = *(const d2*)(cp + b);
+            a[b] = -v.x;
+            a[b + 1] = -v.y;
+        }
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const double bv = Ps[(4 * b + lq) * W + 16 * t + lr];
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[b], bv, acc[t], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            if (col < width)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(acc[t][i], To + (r0 + lq + 4 * i) * ld + col);
+        }
+    }
+}
+template <int K, int NT>
+void launch_mpass(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 16 * NT - 1) / (16 * NT)), (unsigned)((L.rows + rb - 1) / rb));
+    mpass_kernel<K, NT><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+// reference for the permuted coefficient layout
+__global__ void ref_m_kernel(const double* T, double* To, int64_t ld, int64_t rows, int64_t width, int K,
+                             const double* Cm, const double* P) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = blockIdx.y;
+    if (j >= width || i >= rows) return;
+    const int KB = K / 4;
+    double t = T[i * ld + j];
+    for (int l = 0; l < K; ++l) t = __builtin_fma(-Cm[i * K + (l % 4) * KB + l / 4], P[(int64_t)l * ld + j], t);
+    To[i * ld + j] = t;
+}
+
+// MFMA pass v2: the 4 waves of a workgroup share each 16-row group and take NT 16-column
+// tiles each (workgroup = 64 NT columns); P fragments (K/4 x NT doubles per lane) stay in
+// registers for the band; the group's coefficient rows (Cm, 16 x K doubles, contiguous) are
+// staged in LDS by LDS-DMA one group ahead (double buffer, rows padded by PAD doubles); the
+// next group's T tile is prefetched into registers.
+template <int K, int NT, int PAD>
+__global__ __launch_bounds__(256, 2) void mpass2_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                       int64_t ld, int64_t rows, int64_t width,
+                                                       const double* __restrict__ Cm, const double* __restrict__ P,
+                                                       int rb) {
+    constexpr int KB = K / 4, W = 16 * NT, RS = K + PAD;
+    __shared__ double As[2][16 * RS];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lr = lane & 15, lq = lane >> 4;
+    const int64_t c0 = (int64_t)blockIdx.x * (4 * W) + w * W;
+    double b[KB][NT];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            b[kb][t] = P[(int64_t)(4 * kb + lq) * ld + (col < width ? col : width - 1)];
+        }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int ng = (int)((iend - i0) / 16);
+    // stage the coefficients of group g into buffer g & 1: 16 rows of K doubles (K * 8 / 1024
+    // wave instructions per row), rows spread over the 4 waves
+    auto stage = [&](int g) {
+        const int gg = g < ng ? g : ng - 1;
+        const double* src = Cm + (i0 + (int64_t)gg * 16) * K;
+        constexpr int PER_ROW = K * 8 / 1024;   // 1 KiB pieces per row (K = 128: 1)
+        for (int pc = w; pc < 16 * PER_ROW; pc += 4) {
+            const int r = pc / PER_ROW, part = pc % PER_ROW;
+            __builtin_amdgcn_global_load_lds(src + r * K + part * 128 + lane * 2,
+                                             (__attribute__((address_space(3))) void*)&As[g & 1][r * RS + part * 128],
+                                             16, 0, 0);
+        }
+    };
+    auto loadt = [&](d4 (&acc)[NT], int g) {
+        const int gg = g < ng ? g : ng - 1;
+        const int64_t r0 = i0 + (int64_t)gg * 16;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            const int64_t cc = col < width ? col : width - 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[t][i] = __builtin_nontemporal_load(T + (r0 + lq + 4 * i) * ld + cc);
+        }
+    };
+    d4 ta[NT], tb[NT];
+    stage(0);
+    loadt(ta, 0);
+    for (int g = 0; g < ng; g += 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int gg = g + h;
+            if (gg >= ng) break;
+            d4 (&acc)[NT] = h == 0 ? ta : tb;
+            d4 (&nxt)[NT] = h == 0 ? tb : ta;
+            __syncthreads();   // everyone is done with buffer (gg + 1) & 1 (group gg - 1)
+            stage(gg + 1);
+            loadt(nxt, gg + 1);
+            // wait for this group's coefficients (and its T tile): everything but the loads just issued
+            constexpr int NEWV = NT * 4 + (K * 8 / 1024 * 16 + 3) / 4;
+            __builtin_amdgcn_s_waitcnt(0x3F70 | (NEWV & 0xF) | ((NEWV >> 4) << 14));
+            __syncthreads();
+            const double* a = &As[gg & 1][lr * RS + lq * KB];
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const double av = -a[kb];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[kb][t], acc[t], 0, 0, 0);
+            }
+            const int64_t r0 = i0 + (int64_t)gg * 16;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int64_t col = c0 + 16 * t + lr;
+                if (col < width)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(acc[t][i], To + (r0 + lq + 4 * i) * ld + col);
+            }
+        }
+    }
+}
+template <int K, int NT, int PAD>
+void launch_mpass2(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 64 * NT - 1) / (64 * NT)), (unsigned)((L.rows + rb - 1) / rb));
+    mpass2_kernel<K, NT, PAD><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
 struct Variant {
     const char* name;
     int K, rb;
     Launch fn;
     bool exact;   // checked against the reference
+    bool perm = false;   // coefficients in the MFMA-permuted layout
 };
 
 static bool check(const Variant& v) {
@@ -898,8 +1182,12 @@ static bool check(const Variant& v) {
     fill_kernel<<<1024, 256>>>(L.P, (int64_t)K * L.ld, 3);
     CK(hipMemset(L.To, 0, L.rows * L.ld * 8));
     CK(hipMemset(Tr, 0, L.rows * L.ld * 8));
-    ref_kernel<<<dim3((unsigned)((L.width + 255) / 256), (unsigned)L.rows), 256>>>(L.T, Tr, L.ld, L.rows, L.width,
-                                                                                  K, L.Cr, L.P);
+    if (v.perm)
+        ref_m_kernel<<<dim3((unsigned)((L.width + 255) / 256), (unsigned)L.rows), 256>>>(L.T, Tr, L.ld, L.rows,
+                                                                                        L.width, K, L.Cr, L.P);
+    else
+        ref_kernel<<<dim3((unsigned)((L.width + 255) / 256), (unsigned)L.rows), 256>>>(L.T, Tr, L.ld, L.rows, L.width,
+                                                                                      K, L.Cr, L.P);
     v.fn(L, K, v.rb < L.rows ? v.rb : 256, 0);
     CK(hipDeviceSynchronize());
     std::vector<double> a(L.rows * L.ld), b(L.rows * L.ld);
@@ -935,6 +1223,20 @@ int main(int argc, char** argv) {
         {"f4e K64 V1U2 w1", 64, 256, launch_f4e<1>, true},
         {"f4b K64 V1U2 w1", 64, 256, launch_f4b<1>, true},
         {"f4q K64 V1U2 w3", 64, 256, launch_f4q<2, 3>, true},
+        {"mpass2 K128 NT2 p2", 128, 256, launch_mpass2<128, 2, 2>, true, true},
+        {"mpass2 K128 NT2 p0", 128, 256, launch_mpass2<128, 2, 0>, true, true},
+        {"mpass2 K128 NT1 p2", 128, 256, launch_mpass2<128, 1, 2>, true, true},
+        {"mpass2 K64 NT4 p2", 64, 256, launch_mpass2<64, 4, 2>, true, true},
+        {"mpass2 K128 NT2 p2 rb512", 128, 512, launch_mpass2<128, 2, 2>, true, true},
+        {"mpass K64 NT4", 64, 256, launch_mpass<64, 4>, true, true},
+        {"mpass K128 NT4", 128, 256, launch_mpass<128, 4>, true, true},
+        {"mpass K64 NT2", 64, 256, launch_mpass<64, 2>, true, true},
+        {"mpass K128 NT2", 128, 256, launch_mpass<128, 2>, true, true},
+        {"piped K64 S2 U2", 64, 256, launch_piped<2, 2>, true},
+        {"piped K64 S2 U1", 64, 256, launch_piped<2, 1>, true},
+        {"piped K64 S2 U2 rb512", 64, 512, launch_piped<2, 2>, true},
+        {"piped K96 S3 U2", 96, 256, launch_piped<3, 2>, true},
+        {"piped K32 S1 U2", 32, 256, launch_piped<1, 2>, true},
         {"f4q K64 V1U2 w3 noload", 64, 256, launch_f4q<2, 3, 0>, false},
         {"f4q K64 V1U2 w3 b128", 64, 256, launch_f4q<2, 3, 2>, false},
         {"f4q K64 V1U3 w3 rb192", 64, 192, launch_f4q<3, 3>, true},
