@@ -49,6 +49,7 @@ WORKLOADS = {
     "c2": (4096, 4096, 2, "C2 dense LP 4096 x 4096 (+4096 slack): fp64 tableau 4097 x 8193"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP64_PEAK_TFS = 77.3   # measured v_fma_f64 peak on MI355X (tools/passlab.hip valu probe)
 
 
 def parse():
@@ -322,7 +323,13 @@ def main():
                                     f"nt {nt_used}, ld {ld_used})" if K == 1 else
                                     f"rank-{K} tableau pass, form {form} (rows/band {rb_used}, "
                                     f"nt {nt_used}, ld {ld_used}): {K} pivots per launch"),
-                         "launch_ms": upd_ms},
+                         "launch_ms": upd_ms,
+                         # the pass is also an fp64 FMA stream (K fmas per element): its share of
+                         # the measured vector fp64 peak (77.3 TF/s, profiles/r02j/lab8a.txt)
+                         "fp64_tflops": (2.0 * K * rows_local * (N1 - 1) / (upd_ms * 1e-3) / 1e12
+                                         if upd_ms > 0 else None),
+                         "fp64_frac": (2.0 * K * rows_local * (N1 - 1) / (upd_ms * 1e-3) / 1e12 / FP64_PEAK_TFS
+                                       if upd_ms > 0 else None)},
             "cpu_baseline": cpu,
             "geometry": geo,
         }
