@@ -172,14 +172,17 @@ def test_lookahead_off_for_streamed_form():
     _check(res, ref)
 
 
-@pytest.mark.parametrize("defer", [8, 32])
-def test_lookahead_rccl_exchange_single_rank(defer):
+@pytest.mark.parametrize("defer,form", [(8, -1), (32, -1), (64, 21), (64, 3)])
+def test_lookahead_rccl_exchange_single_rank(defer, form):
     """The RCCL path (candidate all-gather, select, MAX all-reduce, commit) with the
-    pass on the second stream, as bench.py --gpus N runs it."""
+    pass on the second stream, as bench.py --gpus N runs it (K = 64: the LEAN
+    selection kernels of the multi-GPU C3 geometry, 128-step replays)."""
     A, b, c = O.gen_dense(200, 400, 1)
     ref = O.solve_dense(A, b, c)
     with dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
                      defer=defer, check_interval=40, lookahead=1) as s:
+        if form >= 0:
+            s.set_defer_tuning(0, form)
         assert s.lookahead()
         st, _ = s.run(10 ** 6)
         res = s.result()

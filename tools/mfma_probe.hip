@@ -1,7 +1,8 @@
 // mfma_probe.hip — does v_mfma_f64_16x16x4f64 round like four sequential fmas (k = 0..3)?
 // Random A (16x4), B (4x16), C (16x16) with exponents over +-30; compares every element of
 // D = mfma(A, B, C) with fma(a3,b3, fma(a2,b2, fma(a1,b1, fma(a0,b0, c)))) (fwd), the reverse
-// order and a single rounding of the exact sum.  Layouts (gfx950, wave64): A[l%16][l/16],
+// order and a single rounding of the exact sum.  MFMA_DENORM=1: denormal-range operands,
+// signed zeros and the smallest denormal mixed in.  Layouts (gfx950, wave64): A[l%16][l/16],
 // B[l/16][l%16], C/D[l/16 + 4i][l%16] for the 4 doubles of lane l.
 //   build: hipcc --offload-arch=gfx950 -O2 -ffp-contract=off -o tools/bin/mfma_probe tools/mfma_probe.hip
 #include <hip/hip_runtime.h>
@@ -31,9 +32,16 @@ int main() {
     std::mt19937_64 g(1);
     std::uniform_real_distribution<double> u(-1, 1);
     std::uniform_int_distribution<int> e(-30, 30);
-    for (auto& x : A) x = std::ldexp(u(g), e(g));
-    for (auto& x : B) x = std::ldexp(u(g), e(g));
-    for (auto& x : C) x = std::ldexp(u(g), e(g) + 10);
+    const int mode = getenv("MFMA_DENORM") ? 1 : 0;
+    std::uniform_int_distribution<int> ed(-1040, -1000), ep(-20, 20);
+    for (auto& x : A) x = std::ldexp(u(g), mode ? ed(g) + 1000 : e(g));
+    for (auto& x : B) x = std::ldexp(u(g), mode ? -1000 - 10 + ep(g) / 4 : e(g));
+    for (auto& x : C) x = std::ldexp(u(g), mode ? ed(g) : e(g) + 10);
+    if (mode) {   // specials: signed zeros, infinities, NaN, denormals
+        for (size_t i = 0; i < C.size(); i += 97) C[i] = (i / 97) % 2 ? -0.0 : 0.0;
+        for (size_t i = 0; i < A.size(); i += 89) A[i] = (i / 89) % 3 == 0 ? -0.0 : 4.9e-324;
+        for (size_t i = 0; i < B.size(); i += 101) B[i] = (i / 101) % 2 ? 0.0 : -0.0;
+    }
     double *dA, *dB, *dC, *dD;
     hipMalloc(&dA, A.size() * 8); hipMalloc(&dB, B.size() * 8); hipMalloc(&dC, C.size() * 8); hipMalloc(&dD, D.size() * 8);
     hipMemcpy(dA, A.data(), A.size() * 8, hipMemcpyHostToDevice);
@@ -55,7 +63,7 @@ int main() {
                 for (int k = 0; k < 4; ++k) x += (long double)a[k] * (long double)B[t * 64 + k * 16 + j];
                 // pairwise: (c + (a0b0 + a1b1)) ... rough
                 double p01 = std::fma(a[0], B[t*64 + j], a[1] * B[t*64+16+j]);
-                seq_fwd += (memcmp(&d, &s, 8) == 0);
+                seq_fwd += (memcmp(&d, &s, 8) == 0) || (d != d && s != s);
                 seq_rev += (memcmp(&d, &r, 8) == 0);
                 double xe = (double)x;
                 exact1 += (memcmp(&d, &xe, 8) == 0);
