@@ -507,7 +507,12 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         // 21 VGPRs), which fit beside the form-21 pass (3 waves x 160 VGPRs per SIMD); the
         // 256-VGPR chain kernel waited for pass workgroups to drain instead (C3: lookahead
         // 6,715 vs 5,970 pivots/s off; 5,473 with the fat kernel; profiles/r02j/)
-        const bool want = opt->lookahead == 1 || (opt->lookahead < 0 && tbytes >= ((size_t)4 << 30));
+        // Multi-rank: auto off.  The per-pivot RCCL kernels of the exchange need more registers
+        // than the form-21 pass leaves free on a CU, so under lookahead each collective would
+        // wait for pass workgroups to drain, as the fat selection kernel did (forced on, the
+        // 1-rank RCCL path is tested: tests/test_gpu_lookahead.py)
+        const bool want = opt->lookahead == 1 ||
+                          (opt->lookahead < 0 && tbytes >= ((size_t)4 << 30) && nranks == 1);
         if (ok && want) {
             if (hipMalloc(&s->Tb[1], tbytes) != hipSuccess) {
                 set_error("hipMalloc of the second tableau buffer failed");
