@@ -196,12 +196,13 @@ __device__ __forceinline__ void ratio_defer_body(
         return;
     }
 
+    // T0[i][q] is requested before the P[l][q] loads and their barrier: both wait only for q
+    double a = i <= rows ? T[i * ld + q] : 0.0;
     for (int l = threadIdx.x; l < J; l += blockDim.x)
         s_pq[l] = l < kp ? Pp[(int64_t)l * ld + q] : P[(int64_t)(l - kp) * ld + q];
     __syncthreads();
 
     Cand c = cand_empty();
-    double a = i <= rows ? T[i * ld + q] : 0.0;
     double flast = 0.0;   // LEAN: C of step J-1 (the RHS cache's step)
     if constexpr (LEAN) {
         // LCH coefficient loads per round trip (the register budget of this kernel)
@@ -341,18 +342,20 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
 // pricing partial of this 512-column tile; objective value into the log.
 // Same per-element operations as the eager update kernel's objective band.
+// z / zq: the caller's early loads of T[rows][j..j+1] and C[rows][s] (PRE), else loaded here
+template <bool PRE = false>
 __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
                                   int64_t nprice, const DevState* st, const double* __restrict__ C,
                                   int64_t ldc, double* __restrict__ P, int s, int64_t j, d2 pr,
                                   PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
-                                  PricePart* lds_pp) {
+                                  PricePart* lds_pp, d2 zpre = d2{0.0, 0.0}, double zqpre = 0.0) {
     const int64_t width = (ncols + 16) & ~(int64_t)15;
     if (j < ld) *(d2*)(P + (int64_t)s * ld + j) = pr;
-    const double zq = C[rows * ldc + s];
+    const double zq = PRE ? zqpre : C[rows * ldc + s];
     PricePart acc = pp_empty();
     if (j < width) {
         double* zp = T + rows * ld + j;
-        d2 z = *(const d2*)zp;
+        d2 z = PRE ? zpre : *(const d2*)zp;
         if (zq != 0.0) {
             z.x = __builtin_fma(-zq, pr.x, z.x);
             z.y = __builtin_fma(-zq, pr.y, z.y);
@@ -387,18 +390,27 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     const int kp = prev_seal >= 0 ? st->seal[prev_seal].blk : 0;
     const int S = kp + s;
     const int32_t pl = st->p_local;
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    // everything that depends only on (p, s) is requested before the step-table barrier:
+    // T0[p][j..j+1] and, for the fused commit, the objective row and z_q
+    d2 t0 = d2{0.0, 0.0}, zpre = d2{0.0, 0.0};
+    double zqpre = 0.0;
+    if (pl >= 0 && j < ld) t0 = *(const d2*)(T + (int64_t)pl * ld + j);
+    if (fused) {
+        zqpre = C[rows * ldc + s];
+        if (j < ((ncols + 16) & ~(int64_t)15)) zpre = *(const d2*)(T + rows * ld + j);
+    }
     if (pl >= 0)
         for (int l = threadIdx.x; l < S; l += blockDim.x) {
             s_cp[l] = l < kp ? Cp[(int64_t)pl * ldc + l] : C[(int64_t)pl * ldc + (l - kp)];
             s_pl[l] = l < kp ? st->seal[prev_seal].pl[l] : st->pl[l - kp];
         }
     __syncthreads();
-    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
     d2 pr;
     pr.x = 0.0;
     pr.y = 0.0;
     if (pl >= 0 && j < ld) {
-        d2 t = *(const d2*)(T + (int64_t)pl * ld + j);
+        d2 t = t0;
         // chunks of CH pivot rows: loads issued back to back (row index clamped), then applied
         // in order (LEAN, lookahead beside the form-21 pass: 2 rows, 21 VGPRs)
         constexpr int CH = LEAN ? 4 : 8;
@@ -437,8 +449,8 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
         }
         return;
     }
-    commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
-               lds_pp);
+    commit_row<true>(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
+                     lds_pp, zpre, zqpre);
 }
 
 // Multi-rank: P[s] from the exchanged bits, then the objective row + pricing.
