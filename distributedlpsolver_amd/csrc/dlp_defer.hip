@@ -227,8 +227,7 @@ __device__ __forceinline__ void ratio_defer_body(
     }
     if (i <= rows) {
         if (i < rows) {
-            if constexpr (LEAN) {
-            } else {
+            if constexpr (!LEAN) {   // (LEAN replayed above)
 #pragma unroll
                 for (int l = 0; l < KMAX; ++l) {
                     if (l < J) {
