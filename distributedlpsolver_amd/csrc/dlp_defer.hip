@@ -240,6 +240,11 @@ __device__ __forceinline__ void ratio_defer_body(
             }
         }
         C[i * ldc + j] = a;
+        // block start: the row's coefficients of steps 1..K-1 := +0, so a pass over a partial
+        // block (kb < K steps) runs the full-block code: P[l >= kb] is +0 too (commit_row),
+        // and fma(-(+0), +0, t) = t + (-0) = t for every t
+        if (j == 0)
+            for (int64_t l = 1; l < ldc; ++l) C[i * ldc + l] = 0.0;
         Cc[(int64_t)j * ldcc + i] = a;
         if (i < rows) nzc[i] = (j == 0 ? 0 : nz_in) + (a != 0.0 ? 1 : 0);   // the pass's row class
         if (i < rows_elig) {
@@ -349,7 +354,11 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
                                   PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
                                   PricePart* lds_pp, d2 zpre = d2{0.0, 0.0}, double zqpre = 0.0) {
     const int64_t width = (ncols + 16) & ~(int64_t)15;
-    if (j < ld) *(d2*)(P + (int64_t)s * ld + j) = pr;
+    if (j < ld) {
+        *(d2*)(P + (int64_t)s * ld + j) = pr;
+        if (s == 0)   // block start: pivot rows 1..K-1 := +0 (see the ratio kernel's C tails)
+            for (int64_t l = 1; l < ldc; ++l) *(d2*)(P + l * ld + j) = d2{0.0, 0.0};
+    }
     const double zq = PRE ? zqpre : C[rows * ldc + s];
     PricePart acc = pp_empty();
     if (j < width) {
@@ -395,7 +404,7 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     d2 t0 = d2{0.0, 0.0}, zpre = d2{0.0, 0.0};
     double zqpre = 0.0;
     if (pl >= 0 && j < ld) t0 = *(const d2*)(T + (int64_t)pl * ld + j);
-    if (fused) {
+    if (fused && !LEAN) {   // (LEAN: within the 32 VGPRs that let it run beside the pass)
         zqpre = C[rows * ldc + s];
         if (j < ((ncols + 16) & ~(int64_t)15)) zpre = *(const d2*)(T + rows * ld + j);
     }
@@ -448,8 +457,8 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
         }
         return;
     }
-    commit_row<true>(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
-                     lds_pp, zpre, zqpre);
+    commit_row<!LEAN>(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
+                      lds_pp, zpre, zqpre);
 }
 
 // Multi-rank: P[s] from the exchanged bits, then the objective row + pricing.
@@ -555,7 +564,11 @@ __global__ __launch_bounds__(256) void pivot_defer_kernel(
         }
         // commit_row with z_q from the state (C[rows][s] is another block's store)
         const int64_t width = (ncols + 16) & ~(int64_t)15;
-        if (j < ld) *(d2*)(P + (int64_t)s * ld + j) = pr;
+        if (j < ld) {
+            *(d2*)(P + (int64_t)s * ld + j) = pr;
+            if (s == 0)   // block start: pivot rows 1..K-1 := +0 (commit_row)
+                for (int64_t l = 1; l < ldc; ++l) *(d2*)(P + l * ld + j) = d2{0.0, 0.0};
+        }
         const double zq = st->zq;
         PricePart acc = pp_empty();
         if (j < width) {
@@ -817,15 +830,17 @@ __device__ __forceinline__ void pass_s_body(const double* __restrict__ T, double
                                             const BlockDesc* __restrict__ bd,
                                             const double* __restrict__ C, int64_t ldc,
                                             const double* __restrict__ P,
-                                            const int32_t* __restrict__ nzc, int rb) {
+                                            const int32_t* __restrict__ nzc, int rb, int tails) {
     __shared__ int32_t cls[1024];
     const int kb = bd->blk;
     const bool outplace = Tout != T;
-    // two launches per pass: the full-block instance (kb == K) and the partial one
-    // (0 < kb < K: a window's last block, or one cut short by termination; kb == 0 out of
-    // place: a copy), so that neither carries the other's register pressure; exactly one
-    // of them runs
-    if ((kb == 0 && !outplace) || (PART ? kb == K : kb != K)) return;
+    // tails (the session's K is this instance's K): the block's unused steps were zeroed at
+    // its start (C and P tails: ratio kernel, commit_row), so the full-block instance runs
+    // partial blocks too, as one launch.  Otherwise two launches per pass: the full-block
+    // instance (kb == K) and the partial one (0 < kb < K: a window's last block, or one cut
+    // short by termination; kb == 0 out of place: a copy), so that neither carries the
+    // other's register pressure; exactly one of them runs
+    if ((kb == 0 && !outplace) || (PART ? kb == K : (kb != K && !tails))) return;
     const int64_t j = (int64_t)blockIdx.x * (256 * V) + threadIdx.x * V;
     const bool colok = j < width;
     const int64_t jc = colok ? j : width - V;
@@ -1022,8 +1037,8 @@ __global__ __launch_bounds__(256) void pass_s_kernel(const double* __restrict__ 
                                                      const BlockDesc* __restrict__ bd,
                                                      const double* __restrict__ C, int64_t ldc,
                                                      const double* __restrict__ P,
-                                                     const int32_t* __restrict__ nzc, int rb) {
-    pass_s_body<NT, K, V, U, PART, DEEP>(T, Tout, ld, rows, width, bd, C, ldc, P, nzc, rb);
+                                                     const int32_t* __restrict__ nzc, int rb, int tails) {
+    pass_s_body<NT, K, V, U, PART, DEEP>(T, Tout, ld, rows, width, bd, C, ldc, P, nzc, rb, tails);
 }
 
 // The same body held to 3 waves per SIMD (<= 168 VGPRs; form 4 alone takes 170, which
@@ -1032,8 +1047,8 @@ template <bool NT, int K, int V, int U, bool PART>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void pass_s3_kernel(
     const double* __restrict__ T, double* __restrict__ Tout, int64_t ld, int64_t rows, int64_t width,
     const BlockDesc* __restrict__ bd, const double* __restrict__ C, int64_t ldc,
-    const double* __restrict__ P, const int32_t* __restrict__ nzc, int rb) {
-    pass_s_body<NT, K, V, U, PART>(T, Tout, ld, rows, width, bd, C, ldc, P, nzc, rb);
+    const double* __restrict__ P, const int32_t* __restrict__ nzc, int rb, int tails) {
+    pass_s_body<NT, K, V, U, PART>(T, Tout, ld, rows, width, bd, C, ldc, P, nzc, rb, tails);
 }
 
 // Streamed form of the pass (forms 6-9): pass_s_body's per-element operations,
@@ -1340,7 +1355,7 @@ __global__ __launch_bounds__(256) void pass_r_kernel(double* __restrict__ T, int
 // accesses with one 32-bit column offset per lane: 166 VGPRs, 3 waves per SIMD.
 // Coefficient registers are written only by loads (no VALU write within two
 // instructions of a DPP read: tests/test_isa.py audits the built code object).  Partial
-// blocks: ctail_kernel (below) zeroes the unused steps' coefficients in memory first.
+// blocks run the same code: their unused steps were zeroed at block start (C and P tails).
 template <int N>
 __device__ __forceinline__ void fmac_bc(double& t, double c, double p) {
     asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
@@ -1364,27 +1379,6 @@ __device__ __forceinline__ void dpp_half(double (&t)[2], const double (&c)[2][2]
     (dpp_step<L0 + I>(t, c, pr), ...);
 }
 
-// Form 21's partial blocks (kb < 64) run the full-block code: this kernel first sets the
-// unused steps l >= kb to fma(-(+0), +0, t) = t + (-0) = t (exact for every t): their
-// coefficients to +0 in C (every row, the objective row included) and their pivot rows
-// P[l] to +0.  Nothing else reads C[i][l >= kb] or P[l >= kb] of the block; the next block
-// rewrites both from step 0.
-__global__ __launch_bounds__(256) void ctail_kernel(const BlockDesc* __restrict__ bd, double* __restrict__ C,
-                                                    int64_t ldc, int64_t nrows, double* __restrict__ P,
-                                                    int64_t ld, int K) {
-    const int kb = bd->blk;
-    if (kb >= K) return;
-    const int w = K - kb;
-    const int64_t nc = nrows * w, np = (int64_t)w * ld;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nc + np;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        if (e < nc)
-            C[(e / w) * ldc + kb + e % w] = 0.0;
-        else
-            P[(int64_t)kb * ld + (e - nc)] = 0.0;
-    }
-}
-
 template <bool NT>
 __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ T, double* __restrict__ Tout,
                                                      int64_t ld, int64_t rows, int64_t width,
@@ -1396,11 +1390,11 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
     __shared__ int32_t cls[1024];
     const int kb = bd->blk;
     const bool outplace = Tout != T;
-    if (kb == 0 && !outplace) return;   // full and partial blocks alike (ctail_kernel)
+    if (kb == 0 && !outplace) return;   // full and partial blocks alike (zeroed tails)
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const bool colok = j < width;
     const int jc = (int)(colok ? j : width - 1);
-    double pr[K];   // all 64 rows: a partial block's P[l >= kb] is +0 (ctail_kernel)
+    double pr[K];   // all 64 rows: a partial block's P[l >= kb] is +0 (zeroed at block start)
 #pragma unroll
     for (int l = 0; l < K; ++l) pr[l] = P[(int64_t)l * ld + jc];
     const int64_t i0 = (int64_t)blockIdx.y * rb;
@@ -1695,8 +1689,6 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             if (occ > 0) dyn = (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t);
             const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
             if (g.rows > 0) {
-                const BlockDesc* bdc = bd;
-                ctail_kernel<<<1024, 256, 0, s>>>(bdc, d.C, d.ldc, g.rows + 1, d.P, g.ld, K);
                 pass_d_kernel<NT><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P,
                                                          d.nzc, rb);
             }
@@ -1721,6 +1713,9 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
         if (dyn < cap) dyn = cap;
     }
     const dim3 grid(ntiles, (unsigned)bands);
+    // the session's K is this template's: partial blocks run the full-block instance (their
+    // unused steps were zeroed at block start), one launch per pass
+    const int tails = d.K == K ? 1 : 0;
     if (g.rows > 0) {
         if (form == 0) {
             if constexpr (K <= 32)   // 2 doubles per lane: P[0..K) in 4K VGPRs
@@ -1730,42 +1725,49 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
                 return hipErrorInvalidValue;
         } else if (form == 3) {
             pass_s_kernel<NT, K, 1, 4, false><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
-                                                                     d.C, d.ldc, d.P, d.nzc, rb);
-            pass_s_kernel<NT, K, 1, 4, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
-                                                                    d.C, d.ldc, d.P, d.nzc, rb);
+                                                                     d.C, d.ldc, d.P, d.nzc, rb, tails);
+            if (!tails)
+                pass_s_kernel<NT, K, 1, 4, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
+                                                                        d.C, d.ldc, d.P, d.nzc, rb, 0);
         } else if (form == 20) {
             if constexpr (K <= 32) {
                 pass_s_kernel<NT, K, 2, 2, false, true><<<grid, 256, dyn, s>>>(
-                    g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
-                pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
-                    g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
+                    g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb, tails);
+                if (!tails)
+                    pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
+                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb, 0);
             } else
                 return hipErrorInvalidValue;
         } else if (form == 4 || form == 14 || form == 15) {
             if constexpr (K <= 32) {
+                // form 14 keeps its streamed partial-block kernel, form 15 (the 3-waves build,
+                // which spills) its partial-block instance: its full-block build ran a partial
+                // C3-geometry block with a wrong tableau (tests/test_gpu_defer.py)
+                const int tl = (form == 14 || form == 15) ? 0 : tails;
                 if (form == 15)
                     pass_s3_kernel<NT, K, 2, 2, false><<<grid, 256, dyn, s>>>(
-                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
+                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb, tl);
                 else
                     pass_s_kernel<NT, K, 2, 2, false><<<grid, 256, dyn, s>>>(
-                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
+                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb, tl);
                 if (form >= 14 && K >= 16 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31)) {
                     // partial block through the streamed kernel's partial instance
                     const int nb = (int)bands;
                     if constexpr (K >= 16)
                         pass_r_kernel<NT, K, 2, 2, 4, true><<<dim3((unsigned)(ntiles * bands)), 256, dyn, s>>>(
                             g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb, ntiles, nb, 0);
-                } else {
+                } else if (!tl) {
                     pass_s_kernel<NT, K, 2, 2, true><<<grid, 256, dyn, s>>>(
-                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb);
+                        g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P, d.nzc, rb, 0);
                 }
             } else
                 return hipErrorInvalidValue;
         } else if (form == 5) {
             pass_s_kernel<NT, K, 1, 8, false><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
-                                                                     d.C, d.ldc, d.P, d.nzc, rb);
-            pass_s_kernel<NT, K, 1, 8, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
-                                                                    d.C, d.ldc, d.P, d.nzc, rb);
+                                                                     d.C, d.ldc, d.P, d.nzc, rb, tails);
+            if (!tails)
+                pass_s_kernel<NT, K, 1, 8, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
+                                                                        d.C, d.ldc, d.P, d.nzc, rb, 0);
         }
         else if (form == 1)
             pass1_kernel<NT, K, 2><<<grid, 256, dyn, s>>>(g.T, g.ld, g.rows, g.width, st, d.C,

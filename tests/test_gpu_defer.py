@@ -239,7 +239,7 @@ def test_auto_block_size_policy():
                                                 (1200, 700, 9, 128, 1, 3)])
 def test_pass_form21_dpp_full_blocks(m, n, seed, rb, nt, occ):
     """Form 21 (DPP-broadcast coefficients, K = 64): two full blocks and a partial one
-    (17 steps: the unused steps' coefficients and pivot rows zeroed by ctail_kernel), widths that are not a
+    (17 steps: the unused steps' coefficients and pivot rows zeroed at block start), widths that are not a
     multiple of the 256-column tile, bands from 37 to 1000 rows (the last one short),
     pivot rows inside the bands; whole tableau byte-equal to the eager session's."""
     k = 2 * 64 + 17

@@ -82,3 +82,42 @@ def test_fused_dpp_fma_has_no_valu_write_hazard():
             k -= 1
     # the form-21 full-block instances (nt and plain): 64 steps x 2 rows x 2 unrolled groups
     assert n_dpp >= 512, n_dpp
+
+
+def _vgpr_counts():
+    """{kernel symbol: .vgpr_count} from the AMDGPU metadata notes of the bundled code objects."""
+    if not os.path.exists(SO) or not os.path.exists(os.path.join(LLVM, "llvm-readelf")):
+        pytest.skip("libdlp.so or llvm-readelf missing")
+    d = tempfile.mkdtemp()
+    try:
+        shutil.copy(SO, os.path.join(d, "libdlp.so"))
+        subprocess.run([os.path.join(LLVM, "llvm-objdump"), "--offloading", "libdlp.so"], cwd=d,
+                       check=True, capture_output=True)
+        counts, name = {}, None
+        for f in sorted(os.listdir(d)):
+            if "amdgcn" in f and "gfx950" in f:
+                r = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", f], cwd=d, check=True,
+                                   capture_output=True, text=True)
+                for line in r.stdout.splitlines():
+                    line = line.strip()
+                    if line.startswith(".name:"):
+                        name = line.split(":", 1)[1].strip()
+                    elif line.startswith(".vgpr_count:") and name:
+                        counts[name] = int(line.split(":", 1)[1])
+        return counts
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def test_lookahead_kernels_fit_beside_the_form21_pass():
+    """Lookahead at K = 64 works only if the LEAN selection kernels share a CU with the
+    form-21 pass: 3 pass waves x 160 VGPRs per SIMD leave 32 of the 512.
+    A kernel that grows past those budgets silently serialises the chain behind the pass."""
+    c = _vgpr_counts()
+    def one(sub):
+        hits = [v for k, v in c.items() if sub in k]
+        assert hits, sub
+        return max(hits)
+    assert one("pass_d_kernel") <= 160, c
+    assert one("ratio_lean_kernelILi128ELi4E") <= 32
+    assert one("prow_defer_kernelILb1E") <= 32
