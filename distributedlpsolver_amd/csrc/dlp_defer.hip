@@ -1342,6 +1342,23 @@ __global__ __launch_bounds__(256) void pass_r_kernel(double* __restrict__ T, int
 }
 
 
+// Row classes of a band (pass_s_body's rule) for the 64-step passes: every row from nzc,
+// then each step's pivot row raised to the step index (LDS atomic max: the last step that
+// pivoted on the row wins; steps >= 0 exceed every class code).  One load per thread
+// instead of a scan of the step table per row.  The caller syncs.
+__device__ inline void classify_band(int32_t* cls, const BlockDesc* __restrict__ bd,
+                                     const int32_t* __restrict__ nzc, int64_t i0, int nr, int kb) {
+    for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+        const int nz = nzc[i0 + r];
+        cls[r] = nz == kb ? kDense : (nz == 0 ? kUntouched : kSparse);
+    }
+    __syncthreads();
+    for (int l = threadIdx.x; l < kb; l += blockDim.x) {
+        const int64_t r = (int64_t)bd->pl[l] - i0;
+        if (bd->pl[l] >= 0 && r >= 0 && r < nr) atomicMax(&cls[r], l);
+    }
+}
+
 // Form 21: the pass at K = 64 with the coefficients broadcast by DPP.  At 64 steps per
 // element the scalar coefficient path of forms 3-5 stalls: every chunk of 2 rows x 8
 // steps is a scalar load that misses to L2 (~800 cycles under the stream) against ~128
@@ -1400,13 +1417,7 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
     const int64_t i0 = (int64_t)blockIdx.y * rb;
     const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
     const int nr = (int)(iend - i0);
-    for (int r = threadIdx.x; r < nr; r += blockDim.x) {
-        const int nz = nzc[i0 + r];
-        int last = -1;
-        for (int l = 0; l < kb; ++l)
-            if (bd->pl[l] == (int32_t)(i0 + r)) last = l;
-        cls[r] = last >= 0 ? last : (nz == kb ? kDense : (nz == 0 ? kUntouched : kSparse));
-    }
+    classify_band(cls, bd, nzc, i0, nr, kb);
     __syncthreads();
     // band descriptors (the caller keeps rb * ld * 8 < 2^31): rows at soffset r * ld8;
     // stores of lanes past the width go out of range and are dropped
@@ -1504,6 +1515,158 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t), ro, voff_st, r * ld8, NT ? 2 : 0);
         }
         r += 1;
+    }
+}
+
+
+// Form 22: the K = 64 pass on the matrix cores.  v_mfma_f64_16x16x4f64 rounds exactly as
+// four sequential fmas in k order (tools/mfma_probe.hip: 51.2 M random elements, denormal
+// and signed-zero operands included), so T_tile := mfma(-C_frag, P_frag, T_tile) over the
+// 16 k-blocks of a block is the eager sequence t = fma(-C[i][l], P[l][c], t), l = 0..63.
+// Workgroup: 4 waves x NT 16-column tiles (64 NT columns) of a band; each wave keeps the
+// P fragments of its tiles (16 x NT doubles per lane) for the band; the 4 waves share
+// each 16-row group, whose coefficient rows are staged in LDS (rows padded to 66 doubles:
+// conflict-free A-fragment reads) by LDS-DMA with per-lane source addresses, one group
+// ahead, next to the next group's T tiles in registers.  Accumulator layout: lane l, reg i
+// = row l/16 + 4 i, column l%16.  Every group runs through the MFMAs; only rows of class
+// dense are stored, the rest (the block's pivot rows, sparse rows; copies of untouched
+// rows out of place) go through the generic replay afterwards.  Partial blocks run the
+// same code (tails zeroed at block start).
+typedef double d4 __attribute__((ext_vector_type(4)));
+template <bool NT_, int NT>
+__global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict__ T, double* __restrict__ Tout,
+                                                     int64_t ld, int64_t rows, int64_t width,
+                                                     const BlockDesc* __restrict__ bd,
+                                                     const double* __restrict__ C, int64_t ldc,
+                                                     const double* __restrict__ P,
+                                                     const int32_t* __restrict__ nzc, int rb) {
+    constexpr int K = 64, KB = K / 4, W = 16 * NT, RS = K + 2;
+    constexpr int NPC = (16 * RS + 127) / 128;   // 1 KiB LDS-DMA pieces per group
+    __shared__ int32_t cls[1024];
+    __shared__ double As[2][NPC * 128];
+    const int kb = bd->blk;
+    const bool outplace = Tout != T;
+    if (kb == 0 && !outplace) return;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lr = lane & 15, lq = lane >> 4;
+    const int64_t cw = (int64_t)blockIdx.x * (4 * W);   // the workgroup's first column
+    const int64_t c0 = cw + w * W;
+    double b[KB][NT];   // P fragments: rows 4 b + lq, column c0 + 16 t + lr
+#pragma unroll
+    for (int k4 = 0; k4 < KB; ++k4)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            b[k4][t] = P[(int64_t)(4 * k4 + lq) * ld + (col < width ? col : width - 1)];
+        }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    classify_band(cls, bd, nzc, i0, nr, kb);
+    const int ng = (nr + 15) / 16;
+    auto stage = [&](int g, int buf) {
+        const int gg = g < ng ? g : ng - 1;
+        for (int pc = w; pc < NPC; pc += 4) {
+            const int e0 = pc * 128 + 2 * lane;   // this lane's LDS doubles e0, e0 + 1
+            int r = e0 / RS, c = e0 % RS;
+            if (c >= K || r >= 16) {   // padding: any valid source
+                r = 0;
+                c = 0;
+            }
+            int64_t row = i0 + (int64_t)gg * 16 + r;
+            row = row < iend ? row : iend - 1;
+            __builtin_amdgcn_global_load_lds(C + row * ldc + c,
+                                             (__attribute__((address_space(3))) void*)&As[buf][pc * 128], 16, 0, 0);
+        }
+    };
+    auto loadt = [&](d4 (&acc)[NT], int g) {
+        const int gg = g < ng ? g : ng - 1;
+        const int64_t r0 = i0 + (int64_t)gg * 16;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            const int64_t cc = col < width ? col : width - 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int64_t row = r0 + lq + 4 * i;
+                row = row < iend ? row : iend - 1;
+                acc[t][i] = NT_ ? __builtin_nontemporal_load(T + row * ld + cc) : T[row * ld + cc];
+            }
+        }
+    };
+    d4 ta[NT], tb[NT];
+    stage(0, 0);
+    loadt(ta, 0);
+    constexpr int STG = (NPC + 3) / 4;   // staging instructions per wave per group
+    for (int g = 0; g < ng; g += 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int gg = g + h;
+            if (gg >= ng) break;
+            d4(&acc)[NT] = h == 0 ? ta : tb;
+            d4(&nxt)[NT] = h == 0 ? tb : ta;
+            __syncthreads();   // cls is complete; buffer (gg + 1) & 1 is free (group gg - 1 done)
+            stage(gg + 1, (gg + 1) & 1);
+            loadt(nxt, gg + 1);
+            // this group's staging and tile: all but the loads just issued
+            constexpr int NEWV = NT * 4 + STG;
+            __builtin_amdgcn_s_waitcnt(0x3F70 | (NEWV & 0xF) | ((NEWV >> 4) << 14));
+            __syncthreads();
+            const double* a = &As[gg & 1][lr * RS + lq];
+#pragma unroll
+            for (int k4 = 0; k4 < KB; ++k4) {
+                const double av = -a[4 * k4];
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[k4][t], acc[t], 0, 0, 0);
+            }
+            const int rl0 = gg * 16;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int64_t col = c0 + 16 * t + lr;
+                if (col < width)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int rl = rl0 + lq + 4 * i;
+                        if (rl < nr && cls[rl] == kDense) {
+                            double* q = Tout + (i0 + rl) * ld + col;
+                            if (NT_)
+                                __builtin_nontemporal_store(acc[t][i], q);
+                            else
+                                *q = acc[t][i];
+                        }
+                    }
+            }
+        }
+    }
+    // everything else, row by row (as pass_s_body's generic replay): the 256 threads as
+    // 2 row halves x the workgroup's 4 W columns
+    constexpr int WC = 4 * W;
+    const int64_t j = cw + (threadIdx.x % WC);
+    if (threadIdx.x >= 2 * WC || j >= width) return;
+    for (int r = threadIdx.x / WC; r < nr; r += 256 / WC) {
+        const int cl = cls[r];
+        if (cl == kDense || (cl == kUntouched && !outplace)) continue;
+        const double* row = T + (i0 + r) * ld;
+        double t;
+        if (cl == kUntouched) {
+            t = row[j];
+        } else {
+            int l = 0;
+            if (cl >= 0) {
+                t = P[(int64_t)cl * ld + j];
+                l = cl + 1;
+            } else {
+                t = row[j];
+            }
+            const double* cr = C + (i0 + r) * ldc;
+            for (; l < kb; ++l) {
+                const double f = cr[l];
+                if (f != 0.0) t = __builtin_fma(-f, P[(int64_t)l * ld + j], t);
+            }
+        }
+        Tout[(i0 + r) * ld + j] = t;
     }
 }
 
@@ -1680,6 +1843,22 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             return hipGetLastError();
         }
     }
+    if (d.form == 22 && K == 64 && d.K == 64 && d.ldc == 64 && rb <= 1024) {
+        // MFMA pass (K = 64 blocks; 128-column workgroups)
+        if constexpr (K == 64) {
+            size_t dyn = 0;
+            if (occ > 0) {
+                const size_t stat = 1024 * sizeof(int32_t) + 2 * 9 * 128 * sizeof(double);
+                dyn = (size_t)160 * 1024 / occ - stat;
+            }
+            const dim3 grid((unsigned)((g.width + 127) / 128), (unsigned)((g.rows + rb - 1) / rb));
+            if (g.rows > 0)
+                pass_m_kernel<NT, 2><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P,
+                                                             d.nzc, rb);
+            if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
+            return hipGetLastError();
+        }
+    }
     // (d.K == 64 exactly: the kernel addresses C with 64 steps per row, ldc == 64)
     if (d.form == 21 && K == 64 && d.K == 64 && d.ldc == 64 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31) &&
         (int64_t)rb * d.ldc * 8 < ((int64_t)1 << 31)) {
@@ -1697,8 +1876,8 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
         }
     }
     // streamed forms need K >= 16 (an even number of coefficient chunks): form 3 below
-    const int form = (d.form >= 6 && d.form != 14 && d.form != 15 && d.form != 20 && d.form != 21) ? 3
-                     : d.form == 21 ? 3 : d.form;
+    const int form = (d.form >= 6 && d.form != 14 && d.form != 15 && d.form != 20 && d.form != 21 && d.form != 22) ? 3
+                     : (d.form == 21 || d.form == 22) ? 3 : d.form;
     const int cols = (form == 0 || form == 4 || form >= 14) ? kDeferTile : 256;
     const int ntiles = (int)((g.width + cols - 1) / cols);
     const int64_t bands = (g.rows + rb - 1) / rb;
@@ -1790,7 +1969,9 @@ static hipError_t pass_k(const Geometry& g, const Defer& d, DevState* st, int rb
     return pass<NT, 64>(g, d, st, rb, occ, s, Tout, seal);
 }
 
-bool lookahead_form(int form) { return form == 3 || form == 4 || form == 5 || form == 20 || form == 21; }
+bool lookahead_form(int form) {
+    return form == 3 || form == 4 || form == 5 || form == 20 || form == 21 || form == 22;
+}
 
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
                               int rows_per_block, int occupancy, hipStream_t s, double* Tout,

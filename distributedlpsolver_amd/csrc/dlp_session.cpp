@@ -1724,7 +1724,7 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
 }
 
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
-    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 21) return DLP_ERR_ARG;
+    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 22) return DLP_ERR_ARG;
     if ((form == 0 || form == 4 || form == 6 || form == 7 || form == 10 || form == 11 || form == 14 ||
          form == 15 || form == 16 || form == 17 || form == 20) &&
         s->d.K > 32) {

@@ -307,7 +307,8 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
  *   15 = the same with the full-block kernel held to 3 waves per SIMD,
  *   20 = form 4 with a 3-deep row prefetch ring (K <= 32),
  *   21 = DPP-broadcast coefficients, 1 double x 2 rows, K = 64 exactly (other K
- *   run form 3).
+ *   run form 3),
+ *   22 = the same block on the matrix cores (v_mfma_f64_16x16x4f64), K = 64 exactly.
  * Default: 21 at K = 64 on a tableau > 1 GiB, 4 at K = 32 there and at K = 16
  * below, else 3.
  * rows_per_block (set_tuning) is the pass's row band.  Results are
@@ -321,7 +322,7 @@ int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
 int dlp_session_set_fused_pivot(dlp_session* s, int on);
 /* *on = 1 when the session runs lookahead (dlp_options.lookahead): block b+1 selected
  * while the pass of block b runs on a second tableau buffer.  The step API and pass
- * forms other than 3, 4, 5, 20 and 21 turn it off for the rest of the session. */
+ * forms other than 3, 4, 5, 20, 21 and 22 turn it off for the rest of the session. */
 int dlp_session_get_lookahead(dlp_session* s, int* on);
 /* Current deferred-pass settings (K = 1: form -1). */
 int dlp_session_get_defer_tuning(dlp_session* s, int* occupancy, int* form, int* K);

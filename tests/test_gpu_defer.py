@@ -180,7 +180,8 @@ def test_defer_update_stats():
     assert k == 8 and n == 5 and ms > 0
 
 
-@pytest.mark.parametrize("P,K,form", [(1, 8, -1), (2, 4, -1), (2, 16, -1), (3, 32, -1), (2, 64, 21), (3, 64, 21)])
+@pytest.mark.parametrize("P,K,form", [(1, 8, -1), (2, 4, -1), (2, 16, -1), (3, 32, -1), (2, 64, 21), (3, 64, 21),
+                                      (2, 64, 22)])
 def test_defer_step_api_multi_rank_one_gpu(P, K, form):
     """The deferred exchange path (ratio -> candidate all-gather -> select ->
     pivot-row MAX all-reduce -> commit, pass every K pivots) with P row-block
@@ -234,11 +235,12 @@ def test_auto_block_size_policy():
         assert s.update_stats()[2] == 16
 
 
+@pytest.mark.parametrize("form", [21, 22])
 @pytest.mark.parametrize("m,n,seed,rb,nt,occ", [(300, 520, 5, 64, 1, 0), (300, 520, 5, 256, 0, 0),
                                                 (700, 1337, 7, 1000, 1, 0), (129, 4000, 2, 37, 1, 2),
                                                 (1200, 700, 9, 128, 1, 3)])
-def test_pass_form21_dpp_full_blocks(m, n, seed, rb, nt, occ):
-    """Form 21 (DPP-broadcast coefficients, K = 64): two full blocks and a partial one
+def test_pass_form21_dpp_full_blocks(m, n, seed, rb, nt, occ, form):
+    """Forms 21 (DPP-broadcast coefficients) and 22 (MFMA), K = 64: two full blocks and a partial one
     (17 steps: the unused steps' coefficients and pivot rows zeroed at block start), widths that are not a
     multiple of the 256-column tile, bands from 37 to 1000 rows (the last one short),
     pivot rows inside the bands; whole tableau byte-equal to the eager session's."""
@@ -250,7 +252,7 @@ def test_pass_form21_dpp_full_blocks(m, n, seed, rb, nt, occ):
         le = e.result().pivot_log
     assert len(le) == k
     with dlp.Session(prob, defer=64, check_interval=64, rows_per_block=rb, nontemporal=nt) as s:
-        s.set_defer_tuning(occ, 21)
+        s.set_defer_tuning(occ, form)
         done = 0
         while done < k:
             done += s.run(min(64, k - done))[1]
@@ -260,8 +262,9 @@ def test_pass_form21_dpp_full_blocks(m, n, seed, rb, nt, occ):
     assert Td.tobytes() == Te.tobytes()
 
 
+@pytest.mark.parametrize("form", [21, 22])
 @pytest.mark.parametrize("K", [64, 40])
-def test_pass_form21_sparse_and_degenerate(K):
+def test_pass_form21_sparse_and_degenerate(K, form):
     """Form 21 on a sparse tableau (ad-allocation LP: untouched / sparse rows through
     the generic replay) and a degenerate one (Bland), full solves against the oracle;
     K = 40 runs form 3 (form 21 needs 64-step blocks)."""
@@ -269,14 +272,14 @@ def test_pass_form21_sparse_and_degenerate(K):
     M, b, c = O.adalloc_lp(200, 200, 0.1, 0.25)
     ref = O.solve_dense(M, b, c)
     with dlp.Session(p, defer=K) as s:
-        s.set_defer_tuning(0, 21)
+        s.set_defer_tuning(0, form)
         s.run(10 ** 6)
         res = s.result()
     _check(res, ref)
     A, b, c = O.gen_dense(128, 128, 3, degenerate=True)
     ref = O.solve_dense(A, b, c, pricing=0)
     with dlp.Session(dlp.Problem.dense(A, b, c), defer=K, check_interval=100) as s:
-        s.set_defer_tuning(0, 21)
+        s.set_defer_tuning(0, form)
         s.run(10 ** 6)
         res = s.result()
     _check(res, ref)

@@ -1157,6 +1157,195 @@ void launch_mpass2(const Lab& L, int, int rb, hipStream_t s) {
     mpass2_kernel<K, NT, PAD><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
 }
 
+// MFMA pass v3: as v2 with the coefficients staged 2 groups ahead in a 3-buffer LDS ring
+// and the T tiles prefetched 2 groups ahead in a 3-deep register ring: one barrier per group.
+template <int K, int NT, int PAD>
+__global__ __launch_bounds__(256, 2) void mpass3_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                       int64_t ld, int64_t rows, int64_t width,
+                                                       const double* __restrict__ Cm, const double* __restrict__ P,
+                                                       int rb) {
+    constexpr int KB = K / 4, W = 16 * NT, RS = K + PAD;
+    __shared__ double As[3][16 * RS];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lr = lane & 15, lq = lane >> 4;
+    const int64_t c0 = (int64_t)blockIdx.x * (4 * W) + w * W;
+    double b[KB][NT];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            b[kb][t] = P[(int64_t)(4 * kb + lq) * ld + (col < width ? col : width - 1)];
+        }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int ng = (int)((iend - i0) / 16);
+    constexpr int PER_ROW = K * 8 / 1024;
+    constexpr int STG = (16 * PER_ROW + 3) / 4;   // staging instructions per wave per group
+    auto stage = [&](int g, int buf) {
+        const int gg = g < ng ? g : ng - 1;
+        const double* src = Cm + (i0 + (int64_t)gg * 16) * K;
+        for (int pc = w; pc < 16 * PER_ROW; pc += 4) {
+            const int r = pc / PER_ROW, part = pc % PER_ROW;
+            __builtin_amdgcn_global_load_lds(src + r * K + part * 128 + lane * 2,
+                                             (__attribute__((address_space(3))) void*)&As[buf][r * RS + part * 128],
+                                             16, 0, 0);
+        }
+    };
+    auto loadt = [&](d4 (&acc)[NT], int g) {
+        const int gg = g < ng ? g : ng - 1;
+        const int64_t r0 = i0 + (int64_t)gg * 16;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            const int64_t cc = col < width ? col : width - 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[t][i] = __builtin_nontemporal_load(T + (r0 + lq + 4 * i) * ld + cc);
+        }
+    };
+    d4 tr[3][NT];
+    stage(0, 0);
+    loadt(tr[0], 0);
+    stage(1, 1);
+    loadt(tr[1], 1);
+    for (int g = 0; g < ng; g += 3) {
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+            const int gg = g + h;
+            if (gg >= ng) break;
+            // this group's staging + tile: everything but the last group's issue (one group's
+            // worth of loads) and its stores
+            constexpr int NEWV = NT * 4 + STG + NT * 4;
+            __builtin_amdgcn_s_waitcnt(0x3F70 | (NEWV & 0xF) | ((NEWV >> 4) << 14));
+            __syncthreads();   // group gg's coefficients are in; group gg-1's buffer is free
+            stage(gg + 2, (h + 2) % 3);
+            loadt(tr[(h + 2) % 3], gg + 2);
+            d4 (&acc)[NT] = tr[h];
+            const double* a = &As[h][lr * RS + lq * KB];
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const double av = -a[kb];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[kb][t], acc[t], 0, 0, 0);
+            }
+            const int64_t r0 = i0 + (int64_t)gg * 16;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int64_t col = c0 + 16 * t + lr;
+                if (col < width)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(acc[t][i], To + (r0 + lq + 4 * i) * ld + col);
+            }
+        }
+    }
+}
+template <int K, int NT, int PAD>
+void launch_mpass3(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 64 * NT - 1) / (64 * NT)), (unsigned)((L.rows + rb - 1) / rb));
+    mpass3_kernel<K, NT, PAD><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
+// MFMA pass v4 (the product candidate for K = 64): coefficients read row-major (C[row][l],
+// ldc = K), staged per 16-row group into LDS rows padded to RS = K + 2 doubles by LDS-DMA
+// with per-lane source addresses (the LDS side is lane-linear: lane L of piece q lands at
+// linear double 128 q + 2 L, so the source is the (row, column) that position means in the
+// padded layout); A fragment of lane (r, q) at kblock b = -As[r][4 b + q].  Coefficient
+// staging and T tiles one group ahead (register ring of 2), NT 16-column tiles per wave.
+template <int K, int NT>
+__global__ __launch_bounds__(256, 2) void mpass4_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                       int64_t ld, int64_t rows, int64_t width,
+                                                       const double* __restrict__ Cr, const double* __restrict__ P,
+                                                       int rb) {
+    constexpr int KB = K / 4, W = 16 * NT, RS = K + 2;
+    constexpr int NPC = (16 * RS + 127) / 128;   // 1 KiB pieces per group
+    __shared__ double As[2][NPC * 128];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lr = lane & 15, lq = lane >> 4;
+    const int64_t c0 = (int64_t)blockIdx.x * (4 * W) + w * W;
+    double b[KB][NT];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            b[kb][t] = P[(int64_t)(4 * kb + lq) * ld + (col < width ? col : width - 1)];
+        }
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    const int ng = (nr + 15) / 16;
+    auto stage = [&](int g, int buf) {
+        const int gg = g < ng ? g : ng - 1;
+        for (int pc = w; pc < NPC; pc += 4) {
+            const int e0 = pc * 128 + 2 * lane;
+            int r = e0 / RS, c = e0 % RS;
+            if (c >= K || r >= 16) { r = 0; c = 0; }   // padding: any valid source
+            int64_t row = i0 + (int64_t)gg * 16 + r;
+            row = row < iend ? row : iend - 1;
+            __builtin_amdgcn_global_load_lds(Cr + row * K + c,
+                                             (__attribute__((address_space(3))) void*)&As[buf][pc * 128], 16, 0, 0);
+        }
+    };
+    auto loadt = [&](d4 (&acc)[NT], int g) {
+        const int gg = g < ng ? g : ng - 1;
+        const int64_t r0 = i0 + (int64_t)gg * 16;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int64_t col = c0 + 16 * t + lr;
+            const int64_t cc = col < width ? col : width - 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int64_t row = r0 + lq + 4 * i;
+                row = row < iend ? row : iend - 1;
+                acc[t][i] = __builtin_nontemporal_load(T + row * ld + cc);
+            }
+        }
+    };
+    d4 ta[NT], tb[NT];
+    stage(0, 0);
+    loadt(ta, 0);
+    constexpr int STG = (NPC + 3) / 4;
+    for (int g = 0; g < ng; g += 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int gg = g + h;
+            if (gg >= ng) break;
+            d4 (&acc)[NT] = h == 0 ? ta : tb;
+            d4 (&nxt)[NT] = h == 0 ? tb : ta;
+            __syncthreads();   // buffer (gg + 1) & 1 is free (group gg - 1 is done)
+            stage(gg + 1, (gg + 1) & 1);
+            loadt(nxt, gg + 1);
+            constexpr int NEWV = NT * 4 + STG;
+            __builtin_amdgcn_s_waitcnt(0x3F70 | (NEWV & 0xF) | ((NEWV >> 4) << 14));
+            __syncthreads();
+            const double* a = &As[gg & 1][lr * RS + lq];
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const double av = -a[4 * kb];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[kb][t], acc[t], 0, 0, 0);
+            }
+            const int64_t r0 = i0 + (int64_t)gg * 16;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int64_t col = c0 + 16 * t + lr;
+                if (col < width)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (r0 + lq + 4 * i < iend)
+                            __builtin_nontemporal_store(acc[t][i], To + (r0 + lq + 4 * i) * ld + col);
+            }
+        }
+    }
+}
+template <int K, int NT>
+void launch_mpass4(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 64 * NT - 1) / (64 * NT)), (unsigned)((L.rows + rb - 1) / rb));
+    mpass4_kernel<K, NT><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
 struct Variant {
     const char* name;
     int K, rb;
@@ -1223,6 +1412,14 @@ int main(int argc, char** argv) {
         {"f4e K64 V1U2 w1", 64, 256, launch_f4e<1>, true},
         {"f4b K64 V1U2 w1", 64, 256, launch_f4b<1>, true},
         {"f4q K64 V1U2 w3", 64, 256, launch_f4q<2, 3>, true},
+        {"mpass4 K64 NT4", 64, 256, launch_mpass4<64, 4>, true},
+        {"mpass4 K64 NT4 rb512", 64, 512, launch_mpass4<64, 4>, true},
+        {"mpass4 K64 NT2", 64, 256, launch_mpass4<64, 2>, true},
+        {"mpass4 K64 NT4 rb250", 64, 250, launch_mpass4<64, 4>, true},
+        {"mpass3 K128 NT2 p2", 128, 256, launch_mpass3<128, 2, 2>, true, true},
+        {"mpass3 K128 NT2 p2 rb512", 128, 512, launch_mpass3<128, 2, 2>, true, true},
+        {"mpass3 K128 NT2 p2 rb1008", 128, 1008, launch_mpass3<128, 2, 2>, true, true},
+        {"mpass3 K128 NT1 p2 rb512", 128, 512, launch_mpass3<128, 1, 2>, true, true},
         {"mpass2 K128 NT2 p2", 128, 256, launch_mpass2<128, 2, 2>, true, true},
         {"mpass2 K128 NT2 p0", 128, 256, launch_mpass2<128, 2, 0>, true, true},
         {"mpass2 K128 NT1 p2", 128, 256, launch_mpass2<128, 1, 2>, true, true},
