@@ -1542,8 +1542,12 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
                                                      const int32_t* __restrict__ nzc, int rb) {
     constexpr int K = 64, KB = K / 4, W = 16 * NT, RS = K + 2;
     constexpr int NPC = (16 * RS + 127) / 128;   // 1 KiB LDS-DMA pieces per group
-    __shared__ int32_t cls[1024];
-    __shared__ double As[2][NPC * 128];
+    // ONE __shared__ object (the coefficient stages, then the row classes): with a second one
+    // beside the LDS-DMA target, hipcc waits vmcnt(0) before the class reads of the stores,
+    // draining the next group's prefetch every group (cdna_hip_programming.md, glds traps)
+    __shared__ double lds_all[2 * NPC * 128 + 512];
+    double(*As)[NPC * 128] = reinterpret_cast<double(*)[NPC * 128]>(lds_all);
+    int32_t* cls = reinterpret_cast<int32_t*>(lds_all + 2 * NPC * 128);
     const int kb = bd->blk;
     const bool outplace = Tout != T;
     if (kb == 0 && !outplace) return;
@@ -1606,13 +1610,15 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
             if (gg >= ng) break;
             d4(&acc)[NT] = h == 0 ? ta : tb;
             d4(&nxt)[NT] = h == 0 ? tb : ta;
-            __syncthreads();   // cls is complete; buffer (gg + 1) & 1 is free (group gg - 1 done)
+            // cls is complete; buffer (gg + 1) & 1 is free (group gg - 1 done).  Raw barriers: a
+            // __syncthreads() waits vmcnt(0), which would drain the prefetch issued below
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             stage(gg + 1, (gg + 1) & 1);
             loadt(nxt, gg + 1);
             // this group's staging and tile: all but the loads just issued
             constexpr int NEWV = NT * 4 + STG;
             __builtin_amdgcn_s_waitcnt(0x3F70 | (NEWV & 0xF) | ((NEWV >> 4) << 14));
-            __syncthreads();
+            asm volatile("s_barrier" ::: "memory");   // every wave's pieces of this group landed
             const double* a = &As[gg & 1][lr * RS + lq];
 #pragma unroll
             for (int k4 = 0; k4 < KB; ++k4) {

@@ -1314,12 +1314,12 @@ __global__ __launch_bounds__(256, 2) void mpass4_kernel(const double* __restrict
             if (gg >= ng) break;
             d4 (&acc)[NT] = h == 0 ? ta : tb;
             d4 (&nxt)[NT] = h == 0 ? tb : ta;
-            __syncthreads();   // buffer (gg + 1) & 1 is free (group gg - 1 is done)
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // raw: the prefetch stays in flight
             stage(gg + 1, (gg + 1) & 1);
             loadt(nxt, gg + 1);
             constexpr int NEWV = NT * 4 + STG;
             __builtin_amdgcn_s_waitcnt(0x3F70 | (NEWV & 0xF) | ((NEWV >> 4) << 14));
-            __syncthreads();
+            asm volatile("s_barrier" ::: "memory");
             const double* a = &As[gg & 1][lr * RS + lq];
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) {
