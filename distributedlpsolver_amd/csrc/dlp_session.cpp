@@ -142,6 +142,10 @@ namespace {
 int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
 
 int auto_rows_per_block(const dlp_session* s) { return s->streaming ? 8 : 4; }
+// deferred pass band rows: 64 on a cache-resident tableau, 256 streaming; 768 for the K = 64
+// streaming pass (form 21 reads P once per band: C3 7,227 / 7,361 / 7,433 / 7,683 pivots/s at
+// 256 / 512 / 768 / 1024 rows on one box, 768 best on two, profiles/r02q/)
+int auto_defer_rb(const dlp_session* s) { return !s->streaming ? 64 : (s->d.K == 64 ? 768 : 256); }
 
 // Row i of a general LP's standard-form tableau (include/dlp.h, "general LPs").
 void std_row(const dlp::StdForm& f, int64_t i, double* r) {
@@ -454,8 +458,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         HIP_TRY(hipMalloc(&s->d.nzc, sizeof(int32_t) * (s->rows + 1)));
         HIP_TRY(hipMemsetAsync(s->d.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
         HIP_TRY(hipMemsetAsync(s->d.P, 0, sizeof(double) * kt * s->ld, s->stream));
-        s->defer_rb = opt->rows_per_block > 0 ? std::min(opt->rows_per_block, 1024)
-                                              : (s->streaming ? 256 : 64);
+        s->defer_rb = opt->rows_per_block > 0 ? std::min(opt->rows_per_block, 1024) : auto_defer_rb(s);
     }
     HIP_TRY(hipMemsetAsync(s->prow_send, 0, sizeof(int64_t) * s->ld, s->stream));
 
@@ -1698,7 +1701,7 @@ int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_bloc
             set_error("a deferred session (defer > 1) needs a 512-column update variant");
             return DLP_ERR_ARG;
         }
-        s->defer_rb = rows_per_block > 0 ? std::min(rows_per_block, 1024) : (s->streaming ? 256 : 64);
+        s->defer_rb = rows_per_block > 0 ? std::min(rows_per_block, 1024) : auto_defer_rb(s);
     }
     s->opt.update_variant = update_variant;
     s->opt.nontemporal = nontemporal;

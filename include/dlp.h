@@ -311,7 +311,8 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
  *   22 = the same block on the matrix cores (v_mfma_f64_16x16x4f64), K = 64 exactly.
  * Default: 21 at K = 64 on a tableau > 1 GiB, 4 at K = 32 there and at K = 16
  * below, else 3.
- * rows_per_block (set_tuning) is the pass's row band.  Results are
+ * rows_per_block (set_tuning) is the pass's row band (0 = auto: 768 rows at
+ * K = 64 on a tableau > 1 GiB, 256 at smaller K there, 64 below).  Results are
  * bit-identical for every setting. */
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form);
 /* Deferred single-rank sessions (K <= 32): run the ratio test, the selection

@@ -85,7 +85,7 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0):
         occ, form, K = s.get_defer_tuning()
         assert K == want_K
         if K == 64:
-            assert form == 21 and s.get_tuning()[1] == 256   # the bench's pass
+            assert form == 21 and s.get_tuning()[1] == 768   # the bench's pass
             assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
         if K == 32:
             assert form == 4 and s.get_tuning()[1] == 256   # round 2's first default
@@ -116,7 +116,7 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0):
 
 def test_c3_full_blocks_bit_exact():
     """C3 at the bench geometry: 2 full K = 64 blocks through the form-21 pass
-    (DPP coefficients, 256-row bands, ld 66048, nt), then an 8-pivot tail (a
+    (DPP coefficients, 768-row bands, ld 66048, nt), then an 8-pivot tail (a
     partial block: coefficients of the unused steps zeroed in memory)."""
     _full_blocks_vs_oracle(32768, 32768, 3, 136, 128, 64)
 
