@@ -143,9 +143,14 @@ int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
 
 int auto_rows_per_block(const dlp_session* s) { return s->streaming ? 8 : 4; }
 // deferred pass band rows: 64 on a cache-resident tableau, 256 streaming; 768 for the K = 64
-// streaming pass (form 21 reads P once per band: C3 7,227 / 7,361 / 7,433 / 7,683 pivots/s at
-// 256 / 512 / 768 / 1024 rows on one box, 768 best on two, profiles/r02q/)
-int auto_defer_rb(const dlp_session* s) { return !s->streaming ? 64 : (s->d.K == 64 ? 768 : 256); }
+// streaming pass over >= 16k local rows (form 21 reads P once per band: C3 7,227 / 7,361 / 7,433
+// pivots/s at 256 / 512 / 768 rows on one box, 768 best on two, profiles/r02q/).  Fewer rows (a
+// rank of a multi-GPU C3) keep 256: at 4096 rows, 768-row bands would be 6 x 257 workgroups,
+// two rounds of the chip's 768 pass slots plus a few, a long tail
+int auto_defer_rb(const dlp_session* s) {
+    if (!s->streaming) return 64;
+    return s->d.K == 64 && s->rows >= 16384 ? 768 : 256;
+}
 
 // Row i of a general LP's standard-form tableau (include/dlp.h, "general LPs").
 void std_row(const dlp::StdForm& f, int64_t i, double* r) {
