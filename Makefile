@@ -21,7 +21,7 @@ build:
 build/%.o: $(CSRC)/%.hip $(CSRC)/dlp_internal.h $(CSRC)/dlp_device.h include/dlp.h | build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-build/%.o: $(CSRC)/%.cpp $(CSRC)/dlp_internal.h $(CSRC)/dlp_host.h include/dlp.h | build
+build/%.o: $(CSRC)/%.cpp $(CSRC)/dlp_internal.h $(CSRC)/dlp_host.h include/dlp.h include/distributed_solver/instance.h | build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIBDLP): $(OBJS)

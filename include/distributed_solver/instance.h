@@ -3,8 +3,11 @@
 //
 // Same constructor, GenerateInstance and RunMultiplicativeWeights signatures
 // as R/instance.h:41-53 (R/ = /root/reference/DistributedLPSolver/
-// DistributedLPSolver/), so a reference caller (R/main.cpp:44-64) compiles
-// unchanged against it.  What changes underneath: RunMultiplicativeWeights runs
+// DistributedLPSolver/), so the reference's caller R/main.cpp compiles and
+// links unchanged against it (tests/test_facade.py::test_reference_main_compiles).
+// As R/instance.h:11-18 does, it gives its includers <ext/hash_map>,
+// <fstream>, <iostream>, <string>, <vector> and `using namespace std;`
+// (R/main.cpp:71 writes `cout` and `endl` unqualified).  What changes underneath: RunMultiplicativeWeights runs
 // the reference's epsilon-approximate MW loop on the GPU (dlp_mw_*), and the
 // added RunSimplex solves the same LP EXACTLY with the MI355X dense-tableau
 // simplex.  The result the reference keeps private (solution_, R/instance.h:34)
@@ -12,19 +15,29 @@
 // Solution() / DualValue() / MWLog().
 #pragma once
 
+// <ext/hash_map> is libstdc++'s pre-C++11 hash table, the reference's
+// container (R/instance.h:11); silence its "deprecated header" warning here
+#ifndef _GLIBCXX_PERMIT_BACKWARD_HASH
+#define _GLIBCXX_PERMIT_BACKWARD_HASH
+#endif
+#include <ext/hash_map>
+#include <fstream>
+#include <iostream>
 #include <string>
 #include <unordered_map>
 #include <utility>
 #include <vector>
 
-#include "dlp.h"
+#include "../dlp.h"
+
+using namespace std;   // R/instance.h:18: the reference's includers rely on it
 
 namespace distributed_solver {
 
 // One advertiser's primal entries: impression -> (current x, running-average x),
-// the element type of the reference's solution_ (R/instance.h:34, a
-// __gnu_cxx::hash_map there).
-typedef std::unordered_map<int, std::pair<long double, long double>> PrimalRow;
+// the element type of the reference's solution_ and of its statics'
+// parameters (R/instance.h:34,55,57): the same __gnu_cxx::hash_map.
+typedef __gnu_cxx::hash_map<int, std::pair<long double, long double> > PrimalRow;
 
 class Instance {
   public:

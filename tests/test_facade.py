@@ -62,6 +62,41 @@ def test_rest_of_the_reference_surface(tmp_path):
             assert all(0.0 < float(v) <= 1.0 + 1e-6 for v in vals[1::2])
 
 
+REF_MAIN = "/root/reference/DistributedLPSolver/DistributedLPSolver/main.cpp"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_MAIN), reason="the reference is present in the build container only")
+@pytest.mark.parametrize("std", ["gnu++11", "c++17"])
+def test_reference_main_compiles(tmp_path, std):
+    """The reference's own caller, R/main.cpp, copied unchanged to a temp dir
+    (never into the repo), compiles and links against the facade + libdlp.so
+    with the facade directory as its only include path: it relies on
+    R/instance.h:11-18's includes and `using namespace std;` (R/main.cpp:71)
+    and on the copy-initialisation `Instance inst = Instance(...)` (:44)."""
+    src = tmp_path / "main.cpp"
+    src.write_bytes(open(REF_MAIN, "rb").read())
+    exe = tmp_path / "main"
+    r = subprocess.run(["g++", f"-std={std}", "-O1", "-w", "-I",
+                        os.path.join(ROOT, "include", "distributed_solver"), str(src),
+                        "-L", os.path.join(ROOT, "distributedlpsolver_amd"), "-ldlp",
+                        f"-Wl,-rpath,{os.path.join(ROOT, 'distributedlpsolver_amd')}", "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert exe.exists()
+
+
+def test_static_signatures_are_the_references():
+    """UpdateAvgPrimal / ResetCurrentPrimal take the reference's parameter type
+    (R/instance.h:55,57): vector<__gnu_cxx::hash_map<int, pair<long double,
+    long double>>>* (checked through the exported mangled names)."""
+    out = subprocess.run(["nm", "-DC", os.path.join(ROOT, "distributedlpsolver_amd", "libdlp.so")],
+                         capture_output=True, text=True, check=True).stdout
+    for fn in ("UpdateAvgPrimal(int, ", "ResetCurrentPrimal("):
+        lines = [ln for ln in out.splitlines() if "Instance::" + fn in ln]
+        assert lines, fn
+        assert "std::vector<__gnu_cxx::hash_map<int, std::pair<long double, long double>" in lines[0], lines[0]
+
+
 _LINE = r"status (\S+) pivots (\d+) objective (\S+) revenue (\S+) max_infeasibility (\S+)"
 
 
