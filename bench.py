@@ -16,7 +16,7 @@ deferred rank-K form: K pivots are selected (pricing, ratio
 test, pivot-row exchange) on replayed views of the resident tableau, then ONE
 HBM pass applies all K to every element, bit-identical to K rank-1 updates.
 So with --step-unit block (default) a step = K pivots + their tableau pass
-(K = 32 at C3), and S steps time S*K pivots, every one of them fully applied
+(K = 64 at C3), and S steps time S*K pivots, every one of them fully applied
 (a window never ends with pivots pending).  With --step-unit pivot a step is
 one pivot, and the window's last pass covers only its last partial block
 (DESIGN.md §6 explains the difference).  `value` is pivots/s either way.
@@ -61,8 +61,11 @@ def parse():
                     help="block: a step is K pivots + one rank-K tableau pass; pivot: one pivot")
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0,
-                    help="CPU baseline: time budget of each of the two oracle windows")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="CPU baseline: time budget of each oracle window (all CPUs, OMP share, 1)")
+    ap.add_argument("--no-eager-window", action="store_true",
+                    help="skip the eager rank-1 (defer = 1) roofline window on the same LP")
+    ap.add_argument("--eager-pivots", type=int, default=3)
     ap.add_argument("--no-pivot-window", action="store_true",
                     help="skip the extra --step-unit pivot window reported beside the main figure")
     ap.add_argument("--rows-per-block", type=int, default=0)
@@ -146,29 +149,68 @@ def cpu_info():
 
 def cpu_baseline(m, n, seed, budget_s):
     """The in-repo C++ oracle (same pivot rule, OpenMP over rows; test
-    infrastructure: the CPU comparator only) on the same LP: all threads this
-    process may use (capped by OMP_NUM_THREADS when the box sets it), then 1."""
+    infrastructure: the CPU comparator only) on the same LP, SURVEY.md §8(d):
+    every CPU this process may use (sched_getaffinity, passed to the oracle
+    explicitly, not inherited from OMP_NUM_THREADS), then the same LP continued
+    on OMP_NUM_THREADS threads (the box's per-GPU CPU share, when set) and on 1
+    thread.  `value` is the faster multi-thread run (threads_for_value says
+    which); every run is reported."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py  # test infrastructure: the CPU comparator only
     model, nproc, avail = cpu_info()
     omp = os.environ.get("OMP_NUM_THREADS")
-    threads = avail if not (omp and omp.isdigit() and int(omp) > 0) else min(avail, int(omp))
-    runs, gen = oracle_py.bench_windows(m, n, seed, [(threads, 100000, budget_s), (1, 100000, budget_s)],
-                                        gen_threads=threads)
-    (s_all, k_all), (s_one, k_one) = runs
+    share = int(omp) if (omp and omp.isdigit() and 0 < int(omp) < avail) else None
+    plan = [(avail, 100000, budget_s)] + ([(share, 100000, budget_s)] if share else []) + \
+           [(1, 100000, budget_s)]
+    runs, gen = oracle_py.bench_windows(m, n, seed, plan, gen_threads=avail)
+    for (secs, k), (thr, _, _) in zip(runs, plan):
+        if not (secs and k):
+            raise RuntimeError(f"CPU baseline sample too small: {k} pivots in {secs} s on {thr} threads "
+                               f"(the LP ended inside the sample)")
+    rate = {thr: k / secs for (secs, k), (thr, _, _) in zip(runs, plan)}
     where = (f"{model}; os.cpu_count() = {nproc}, {avail} usable by this process"
              + (f", OMP_NUM_THREADS = {omp}" if omp else ""))
-    if not (k_all and s_all and k_one and s_one):
-        raise RuntimeError(f"CPU baseline sample too small: {k_all} pivots in {s_all} s, "
-                           f"{k_one} in {s_one} s (the LP ended inside the sample)")
-    return {"value": k_all / s_all, "unit": "pivots/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "nproc": nproc, "cpus_usable": avail,
-            "sample": (f"in-repo C++ oracle (same pivot rule, eager rank-1, OpenMP over rows) on the same "
-                       f"LP {m}x{n} seed {seed}: 1 warm-up pivot, then {k_all} pivots in {s_all:.2f} s on "
-                       f"{threads} threads, then {k_one} pivots in {s_one:.2f} s on 1 thread ({where}); "
-                       f"host tableau generation {gen:.1f} s not timed"),
-            "single_thread": {"value": k_one / s_one, "unit": "pivots/s", "cores": 1,
-                              "pivots": k_one, "seconds": s_one}}
+    # value: the faster of the all-CPU and per-GPU-share runs (on a box whose cgroup grants this
+    # process a CPU share below its affinity mask, 256 threads run slower than 16); both kept
+    best = max((t for t in rate if t > 1), key=lambda t: rate[t], default=1)
+    out = {"value": rate[best], "unit": "pivots/s", "cores": best, "kind": "port",
+           "threads_for_value": best, "all_cpus": {"value": rate[avail], "unit": "pivots/s", "cores": avail},
+           "cpu_model": model, "nproc": nproc, "cpus_usable": avail,
+           "sample": (f"in-repo C++ oracle (same pivot rule, eager rank-1, OpenMP over rows) on the same "
+                      f"LP {m}x{n} seed {seed}: 1 warm-up pivot, then consecutive windows of <= {budget_s:g} s "
+                      f"each: " + ", ".join(f"{k} pivots in {secs:.2f} s on {thr} threads"
+                                            for (secs, k), (thr, _, _) in zip(runs, plan))
+                      + f" ({where}); host tableau generation {gen:.1f} s not timed"),
+           "single_thread": {"value": rate[1], "unit": "pivots/s", "cores": 1,
+                             "pivots": runs[-1][1], "seconds": runs[-1][0]}}
+    if share:
+        out["omp_share"] = {"value": rate[share], "unit": "pivots/s", "cores": share,
+                            "pivots": runs[1][1], "seconds": runs[1][0]}
+    return out
+
+
+def log_parity(workload, log):
+    """Self-check of the run: the pivot log against the committed digests of the oracle's run
+    of the same LP (tests/golden/digests.json, tests/golden/make_digests.py: sha256 of log
+    prefixes), at every committed prefix the run reached.  With N > 1 this is the row-block
+    exchange's parity evidence at the bench size (the log is replicated on every rank)."""
+    import hashlib
+    path = os.path.join(ROOT, "tests", "golden", "digests.json")
+    try:
+        with open(path) as f:
+            g = json.load(f).get("c3_k64" if workload == "c3" else workload)
+    except (OSError, ValueError):
+        return None
+    if not g or "log_prefix_sha256" not in g:
+        return None
+    got = {}
+    for k, h in g["log_prefix_sha256"].items():
+        if int(k) <= len(log):
+            got[k] = hashlib.sha256(log[:int(k)].tobytes()).hexdigest() == h
+    if g.get("pivots") == len(log):
+        got[str(len(log))] = hashlib.sha256(log.tobytes()).hexdigest() == g["log_sha256"]
+    return {"source": "tests/golden/digests.json (oracle, same LP)", "prefixes_checked": sorted(got, key=int),
+            "bit_identical": all(got.values()) if got else None}
 
 
 def main():
@@ -267,7 +309,32 @@ def main():
 
     res = sess.result()
     obj_after = res.objective
+    parity = log_parity(args.workload, res.pivot_log) if rank == 0 else None
     sess.close()
+
+    # the north star's own figure: the EAGER rank-1 update (defer = 1) on the same tableau,
+    # a short window of single-pivot launches timed by HIP events on the session stream
+    eager = None
+    if world == 1 and not args.no_eager_window and K > 1:
+        with dlp.Session(prob, device=local, check_interval=args.eager_pivots, timing=1, defer=1,
+                         max_pivots=args.eager_pivots + 1, log_pivots=1) as es:
+            es.run(1)   # warm-up pivot
+            es.reset_timings()
+            t2 = time.perf_counter()
+            st, done = es.run(args.eager_pivots)
+            torch.cuda.synchronize()
+            e_el = time.perf_counter() - t2
+            e_launch, e_ms, _ = es.update_stats()
+            e_var, e_rb, e_nt = es.get_tuning()
+            e_rows = es.rows
+        e_ms1 = e_ms / max(e_launch, 1)
+        e_bytes = 16.0 * (e_rows + 1) * N1
+        e_ach = e_bytes / (e_ms1 * 1e-3) / 1e9 if e_ms1 > 0 else None
+        eager = {"kernel": f"rank-1 update variant {e_var} (rows/band {e_rb}, nt {e_nt})",
+                 "pivots": done, "launches": e_launch, "launch_ms": e_ms1,
+                 "algorithmic_bytes_per_launch": e_bytes, "achieved": e_ach, "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": e_ach / HBM_PEAK_GBS if e_ach else None,
+                 "pivots_per_s": done / e_el if e_el > 0 else None}
 
     if rank == 0:
         kind = "update" if K == 1 else "pass"
@@ -286,7 +353,8 @@ def main():
             cpu = cpu_baseline(m, n, seed, args.cpu_seconds)
         value = timed / elapsed
         line = {
-            "metric": "simplex pivots/s (dense fp64 tableau, rank-1 update HBM roofline)",
+            "metric": ("simplex pivots/s + achieved HBM GB/s (dense fp64 tableau; roofline of the "
+                       + (f"rank-{K} tableau pass" if K > 1 else "rank-1 update") + ")"),
             "value": value,
             "unit": "pivots/s",
             "n_gpus": world,
@@ -330,6 +398,8 @@ def main():
                                          if upd_ms > 0 else None),
                          "fp64_frac": (2.0 * K * rows_local * (N1 - 1) / (upd_ms * 1e-3) / 1e12 / FP64_PEAK_TFS
                                        if upd_ms > 0 else None)},
+            "rank1_update_roofline": eager,
+            "pivot_log_vs_oracle": parity,
             "cpu_baseline": cpu,
             "geometry": geo,
         }

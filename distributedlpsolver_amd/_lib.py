@@ -146,6 +146,9 @@ SIGNATURES = [
     ("dlp_session_set_defer_tuning", C.c_int, [_P, C.c_int, C.c_int]),
     ("dlp_session_set_fused_pivot", C.c_int, [_P, C.c_int]),
     ("dlp_session_get_lookahead", C.c_int, [_P, C.POINTER(C.c_int)]),
+    ("dlp_session_set_exchange_timeout", C.c_int, [_P, C.c_double]),
+    ("dlp_session_abort", C.c_int, [_P]),
+    ("dlp_session_inject_fault", C.c_int, [_P, _I64]),
     ("dlp_session_get_defer_tuning", C.c_int,
      [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dlp_session_set_tuning", C.c_int, [_P, C.c_int, C.c_int, C.c_int]),

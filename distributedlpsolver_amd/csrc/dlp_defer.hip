@@ -121,7 +121,8 @@ __device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, int nblocks, const double* __restrict__ Ccp = nullptr,
-    const double* __restrict__ Pp = nullptr, int prev_seal = -1) {
+    const double* __restrict__ Pp = nullptr, int prev_seal = -1, const XPeers* xp = nullptr,
+    uint32_t xseq = 0) {
     __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
     __shared__ Cand lds_c[kRatioDeferThreads / 64];
     __shared__ int s_last;
@@ -305,6 +306,8 @@ __device__ __forceinline__ void ratio_defer_body(
         st->q = q;
         if (nranks == 1)
             do_select(st, best, q, basis, row_first, rows, pricing, log, log_cap, true);
+        else if (xp)
+            x_push_cand(xp, xseq, best);   // peer exchange: straight into every rank's slot
         else
             cand_out[0] = best;
         if constexpr (FUSED) {
@@ -322,10 +325,11 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
-    int prev_seal) {
+    int prev_seal, const XPeers* xp, uint32_t xseq) {
     ratio_defer_body<KMAX, false>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                   ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
-                                  tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal);
+                                  tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
+                                  xp, xseq);
 }
 
 // The LEAN selection kernel, held to 32 VGPRs (lookahead at K = 64, beside the pass).
@@ -337,10 +341,11 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
-    int prev_seal) {
+    int prev_seal, const XPeers* xp, uint32_t xseq) {
     ratio_defer_body<KMAX, false, true, LCH>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                         ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
-                                        tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal);
+                                        tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
+                                        xp, xseq);
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
@@ -388,7 +393,8 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
     int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
-    int fused, const double* __restrict__ Cp, const double* __restrict__ Pp, int prev_seal) {
+    int fused, const double* __restrict__ Cp, const double* __restrict__ Pp, int prev_seal,
+    const XPeers* xp, uint32_t xseq) {
     __shared__ PricePart lds_pp[4];
     __shared__ double s_cp[kMaxReplay];
     __shared__ int32_t s_pl[kMaxReplay];
@@ -446,6 +452,12 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
         pr.x = t.x / piv;
         pr.y = t.y / piv;
     }
+    if (!fused && xp) {   // peer exchange: the owner's row into every rank's row region
+        if (pl >= 0)      // (uniform per launch)
+            x_push_row_chunk(xp, xseq, j, ld, __builtin_bit_cast(uint64_t, pr.x),
+                             __builtin_bit_cast(uint64_t, pr.y));
+        return;
+    }
     if (!fused) {
         if (j < ld) {
             if (pl >= 0) {
@@ -464,17 +476,30 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
 // Multi-rank: P[s] from the exchanged bits, then the objective row + pricing.
 __global__ __launch_bounds__(256) void commit_defer_kernel(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
-    const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
+    DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
     const int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log,
-    int64_t log_cap) {
+    int64_t log_cap, const XPeers* xp, uint32_t xseq) {
     __shared__ PricePart lds_pp[4];
+    __shared__ int s_ok;
     if (st->status != DLP_RUNNING) return;
     const int s = st->blk - 1;
     const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
     d2 pr;
     pr.x = 0.0;
     pr.y = 0.0;
-    if (j < ld) pr = *(const d2*)(bits + j);
+    if (xp) {   // peer exchange: this chunk's flag, then the row from this rank's region
+        if (threadIdx.x == 0) s_ok = x_wait(xp, x_rflag(xp, xp->me, blockIdx.x), xseq) ? 1 : 0;
+        __syncthreads();
+        if (!s_ok) {
+            if (threadIdx.x == 0) st->status = kStatusXFail;
+            return;
+        }
+        const uint64_t* row = x_row(xp, xp->me);
+        if (j < ld) pr.x = __builtin_bit_cast(double, x_load(row + j));
+        if (j + 1 < ld) pr.y = __builtin_bit_cast(double, x_load(row + j + 1));
+    } else if (j < ld) {
+        pr = *(const d2*)(bits + j);
+    }
     commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
                lds_pp);
 }
@@ -1702,7 +1727,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               const PricePart* pp, DevState* st, Cand* partials, int nblocks,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
-                              const Defer* prev, int prev_seal) {
+                              const Defer* prev, int prev_seal, const XPeers* xp, uint32_t xseq) {
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
     nblocks = ratio_defer_blocks(g);
@@ -1714,7 +1739,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     ratio_defer_kernel<KM><<<nblocks, kRatioDeferThreads, 0, s>>>(                               \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, \
         d.Cc, d.ldcc, d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing,   \
-        log, log_cap, Ccp, Pp, prev_seal)
+        log, log_cap, Ccp, Pp, prev_seal, xp, xseq)
     if (steps <= 8)
         DLP_RATIO_DEFER(8);
     else if (steps <= 16)
@@ -1729,7 +1754,8 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
 #define DLP_RATIO_LEAN(L)                                                                                  \
     ratio_lean_kernel<128, L><<<nblocks, kRatioDeferThreads, 0, s>>>(                                       \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
-        d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal)
+        d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
+        xp, xseq)
         if (lch == 8)   // tuning only (DLP_LEAN_LCH)
             DLP_RATIO_LEAN(8);
         else
@@ -1773,27 +1799,31 @@ int fused_pivot_blocks(const Geometry& g) {
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
                              int64_t log_cap, int nranks, hipStream_t s, const Defer* prev,
-                             int prev_seal) {
+                             int prev_seal, const XPeers* xp, uint32_t xseq) {
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     if (prev_seal >= 0 && d.K > 32)   // lookahead at K = 64: beside the form-21 pass
         prow_defer_kernel<true><<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
                                                      d.P, prow_bits, pp, tol_dj, log, log_cap,
-                                                     nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal);
+                                                     nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal,
+                                                     nranks == 1 ? nullptr : xp, xseq);
     else
         prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
                                                  d.P, prow_bits, pp, tol_dj, log, log_cap,
                                                  nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
-                                                 prev_seal >= 0 ? prev->P : nullptr, prev_seal);
+                                                 prev_seal >= 0 ? prev->P : nullptr, prev_seal,
+                                                 nranks == 1 ? nullptr : xp, xseq);
     return hipGetLastError();
 }
 
-hipError_t launch_commit_defer(const Geometry& g, const Defer& d, const DevState* st,
+hipError_t launch_commit_defer(const Geometry& g, const Defer& d, DevState* st,
                                const int64_t* prow_bits, PricePart* pp, double tol_dj,
-                               dlp_pivot* log, int64_t log_cap, hipStream_t s) {
+                               dlp_pivot* log, int64_t log_cap, hipStream_t s, const XPeers* xp,
+                               uint32_t xseq) {
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     commit_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C,
-                                               d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap);
+                                               d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap, xp,
+                                               xseq);
     return hipGetLastError();
 }
 

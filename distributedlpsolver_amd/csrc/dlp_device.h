@@ -136,3 +136,89 @@ __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* ba
     st->npivots = k + 1;
 }
 
+
+// ------------------------------------------------------------- peer exchange
+// (dlp_internal.h, XPeers).  System-scope relaxed atomics: the stores are written
+// through to memory, the loads are served from memory (the blocks are uncached), so a
+// message written by another device (xGMI) or by another XCD is seen once its flag is.
+constexpr uint64_t kXWaitTicks = 30ull * 100000000ull;   // 30 s of the 100 MHz constant clock
+
+__device__ inline void x_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline uint64_t x_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Bounded wait for *flag == seq: false on timeout or when the host raised the abort word.
+__device__ inline bool x_wait(const XPeers* xp, const uint64_t* flag, uint64_t seq) {
+    if (x_load(flag) == seq) return true;
+    const uint64_t t0 = wall_clock64();
+    for (uint32_t it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        if (x_load(flag) == seq) return true;
+        if ((it & 255) == 0) {
+            if (xp->abort_word &&
+                __hip_atomic_load(xp->abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+                return false;
+            if (wall_clock64() - t0 > kXWaitTicks) return false;
+        }
+    }
+}
+__device__ inline uint64_t* x_cflag(const XPeers* xp, int rank, int parity, int sender) {
+    return xp->base[rank] + (int64_t)parity * xp->nranks + sender;
+}
+__device__ inline uint64_t* x_cslot(const XPeers* xp, int rank, int parity, int sender) {
+    return xp->base[rank] + xp->off_cslot + ((int64_t)parity * xp->nranks + sender) * 4;
+}
+__device__ inline uint64_t* x_rflag(const XPeers* xp, int rank, int64_t chunk) {
+    return xp->base[rank] + xp->off_rflag + chunk;
+}
+__device__ inline uint64_t* x_row(const XPeers* xp, int rank) { return xp->base[rank] + xp->off_row; }
+
+// One lane: this rank's candidate into slot [seq & 1][me] of every rank, then the flags.
+__device__ inline void x_push_cand(const XPeers* xp, uint32_t seq, const Cand& c) {
+    const int par = (int)(seq & 1u);
+    const uint64_t* cv = (const uint64_t*)&c;
+    for (int r = 0; r < xp->nranks; ++r) {
+        uint64_t* slot = x_cslot(xp, r, par, xp->me);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x_store(slot + k, cv[k]);
+    }
+    __threadfence_system();   // the slots reach memory before any flag
+    for (int r = 0; r < xp->nranks; ++r) x_store(x_cflag(xp, r, par, xp->me), seq);
+}
+
+// Workgroup (>= nranks lanes): the P candidates of exchange seq into lds[0..P); false
+// when a wait failed (every lane gets the same answer).
+__device__ inline bool x_gather_cands(const XPeers* xp, uint32_t seq, Cand* lds, int* s_ok) {
+    const int par = (int)(seq & 1u);
+    if (threadIdx.x == 0) *s_ok = 1;
+    __syncthreads();
+    for (int r = threadIdx.x; r < xp->nranks; r += blockDim.x) {
+        if (!x_wait(xp, x_cflag(xp, xp->me, par, r), seq)) {
+            *s_ok = 0;
+            continue;
+        }
+        const uint64_t* slot = x_cslot(xp, xp->me, par, r);
+        uint64_t* dst = (uint64_t*)&lds[r];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k] = x_load(slot + k);
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// Workgroup of 256 lanes, chunk = blockIdx.x (512 columns, 2 per lane from column j):
+// the owner's row values (v0, v1) into every rank's row region, then the chunk flags.
+__device__ inline void x_push_row_chunk(const XPeers* xp, uint32_t seq, int64_t j, int64_t ld,
+                                        uint64_t v0, uint64_t v1) {
+    if (j < ld)
+        for (int r = 0; r < xp->nranks; ++r) {
+            uint64_t* row = x_row(xp, r);
+            x_store(row + j, v0);
+            if (j + 1 < ld) x_store(row + j + 1, v1);
+        }
+    __threadfence_system();   // every lane's stores reach memory before the flags
+    __syncthreads();
+    for (int r = threadIdx.x; r < xp->nranks; r += blockDim.x) x_store(x_rflag(xp, r, blockIdx.x), seq);
+}

@@ -86,6 +86,30 @@ __host__ __device__ inline bool cand_better(const Cand& a, const Cand& b) {
     return a.basis_var < b.basis_var;
 }
 
+// Peer exchange: the row-block ranks exchange the pivot candidates and the
+// owner's pivot row by direct stores into each other's exchange blocks (xGMI peer writes
+// between devices; plain stores between sessions on one device), each message followed by
+// a tagged flag, instead of an RCCL all-gather + all-reduce.  One block per rank, in
+// uncached device memory, laid out identically on every rank (uint64 words):
+//   [0, 2P)                    candidate flags  cflag[parity][sender]  (= exchange seq)
+//   [off_cslot, +8P)           candidate slots  cslot[parity][sender]  (4 words = 32 B)
+//   [off_rflag, +nchunks)      pivot-row chunk flags (512 columns per chunk)
+//   [off_row, +ld)             the pivot row (fp64 bits), written by its owner
+// Every wait is bounded (kXWaitTicks of the 100 MHz constant clock, or the host's abort
+// word): a stall sets DevState.status = kStatusXFail and the host returns DLP_ERR_HIP.
+constexpr int kMaxRanks = 64;
+constexpr int kXChunk = 512;                       // pivot-row chunk (= prow / commit workgroup)
+constexpr int32_t kStatusXFail = 6;                // DevState.status: a peer exchange timed out
+struct XPeers {
+    uint64_t* base[kMaxRanks];   // every rank's exchange block as this device addresses it
+    const uint32_t* abort_word;  // host-pinned; nonzero ends every wait (dlp_session_abort)
+    int32_t nranks, me;
+    int64_t nchunks;
+    int64_t off_cslot, off_rflag, off_row;
+};
+// Block size (bytes) and offsets for nranks ranks and row length ld.
+size_t xblock_layout(int nranks, int64_t ld, XPeers* xp);
+
 // Deferred rank-k update (dlp_defer.hip).  Up to K pivots are selected against
 // the stale HBM tableau T0 through "replayed" views (column q and pivot row p
 // re-derived by applying the block's earlier steps, in order, with the same
@@ -137,11 +161,25 @@ hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* bas
                         const PricePart* pp, DevState* st, double* colq, Cand* partials,
                         int nblocks, Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                         int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s);
+// Peer exchange kernels (dlp_kernels.hip).  xcand_send: this rank's candidate (cand_send)
+// into every rank's slot (seq); the select kernel waits for and reduces the P slots when
+// given xp.  xrow_send: the owner's pivot-row bits (owner: st->p_local >= 0, or
+// owner_rank >= 0 for the carried row) into every rank's row region + chunk flags;
+// xrow_recv: wait for every chunk of this seq and copy the row to `out` (a plain buffer
+// for the eager kernels).
+hipError_t launch_xcand_send(const XPeers* xp, uint32_t seq, const Cand* cand_send, const DevState* st,
+                             hipStream_t s);
+hipError_t launch_xwait(const XPeers* xp, uint32_t seq, DevState* st, hipStream_t s);
+hipError_t launch_xrow_send(const XPeers* xp, uint32_t seq, const int64_t* bits, int64_t ld,
+                            const DevState* st, int owner_rank, int my_rank, hipStream_t s);
+hipError_t launch_xrow_recv(const XPeers* xp, uint32_t seq, int64_t ld, int64_t* out, DevState* st,
+                            hipStream_t s);
 int ratio_blocks(const Geometry& g);
 int ratio_defer_blocks(const Geometry& g);
 hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32_t* basis,
                          DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
-                         hipStream_t s, bool forced = false, bool track = false);
+                         hipStream_t s, bool forced = false, bool track = false,
+                         const XPeers* xp = nullptr, uint32_t seq = 0);
 // General LPs (Phase I -> II).  drive: forced-pivot candidate for global row
 // `row` (nranks == 1: also select + colq capture); gather_q: colq of st->q;
 // carry_out / carry_in: ship the carried objective row through the int64 MAX
@@ -162,7 +200,8 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               const PricePart* pp, DevState* st, Cand* partials, int nblocks,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
-                              const Defer* prev = nullptr, int prev_seal = -1);
+                              const Defer* prev = nullptr, int prev_seal = -1,
+                              const XPeers* xp = nullptr, uint32_t seq = 0);
 // nranks == 1: ratio test + selection + pivot row + objective row + pricing in ONE launch
 // (K <= 32; grid of fused_pivot_blocks(g), all of which must be resident at once).
 int fused_pivot_blocks(const Geometry& g);
@@ -172,14 +211,20 @@ hipError_t launch_pivot_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               hipStream_t s);
 // nranks == 1: P[s] + objective row + pricing partials + log in one pass;
 // nranks > 1: the owner's replayed pivot-row bits (others INT64_MIN) to prow_bits.
+// xp (peer exchange): the owner stores its row into every rank's row region + chunk
+// flags instead (non-owners write nothing).
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
                              int64_t log_cap, int nranks, hipStream_t s,
-                             const Defer* prev = nullptr, int prev_seal = -1);
+                             const Defer* prev = nullptr, int prev_seal = -1,
+                             const XPeers* xp = nullptr, uint32_t seq = 0);
 // nranks > 1, after the MAX all-reduce: P[s] from the exchanged bits + objective row + pricing.
-hipError_t launch_commit_defer(const Geometry& g, const Defer& d, const DevState* st,
+// xp: each workgroup first waits for its chunk's flag (seq), then reads the row region
+// with system-scope loads (prow_bits = this rank's row region).
+hipError_t launch_commit_defer(const Geometry& g, const Defer& d, DevState* st,
                                const int64_t* prow_bits, PricePart* pp, double tol_dj,
-                               dlp_pivot* log, int64_t log_cap, hipStream_t s);
+                               dlp_pivot* log, int64_t log_cap, hipStream_t s,
+                               const XPeers* xp = nullptr, uint32_t seq = 0);
 // The tableau pass: applies the block's st->blk steps to rows [0, rows), then blk = 0.
 // Lookahead (seal >= 0): the block st->seal[seal], read from g.T and written to Tout
 // (every row, untouched ones copied; blk is left alone).  Forms 3, 4, 5 and 20 only

@@ -151,10 +151,23 @@ __device__ inline void forced_select(DevState* st, const Cand& best, int32_t* ba
     do_select(st, best, best.pad0, basis, row_first, rows, pricing, log, log_cap);
 }
 
+// Peer exchange (xp != NULL): the P candidates come from this rank's exchange block, each
+// after its flag shows this exchange's seq (bounded wait; a stall -> kStatusXFail).
 __global__ void select_kernel(const Cand* cands, int nranks, int32_t* basis, DevState* st,
                               int64_t row_first, int64_t rows, int pricing, dlp_pivot* log,
-                              int64_t log_cap, int forced, int track) {
-    if (st->status != DLP_RUNNING || threadIdx.x != 0) return;
+                              int64_t log_cap, int forced, int track, const XPeers* xp,
+                              uint32_t seq) {
+    __shared__ Cand s_c[kMaxRanks];
+    __shared__ int s_ok;
+    if (st->status != DLP_RUNNING) return;   // uniform: every rank holds the same status
+    if (xp) {
+        if (!x_gather_cands(xp, seq, s_c, &s_ok)) {
+            if (threadIdx.x == 0) st->status = kStatusXFail;
+            return;
+        }
+        cands = s_c;
+    }
+    if (threadIdx.x != 0) return;
     Cand best = cand_empty();
     for (int r = 0; r < nranks; ++r)
         if (cand_better(cands[r], best)) best = cands[r];
@@ -162,6 +175,55 @@ __global__ void select_kernel(const Cand* cands, int nranks, int32_t* basis, Dev
         forced_select(st, best, basis, row_first, rows, pricing, log, log_cap);
     else
         do_select(st, best, st->q, basis, row_first, rows, pricing, log, log_cap, track != 0);
+}
+
+// ---- peer exchange, stand-alone kernels (the eager and Phase I -> II paths; the deferred
+// kernels push and wait inside their own launches)
+__global__ void xcand_send_kernel(const XPeers* xp, uint32_t seq, const Cand* cand_send,
+                                  const DevState* st) {
+    if (st->status != DLP_RUNNING || threadIdx.x != 0) return;
+    x_push_cand(xp, seq, cand_send[0]);
+}
+
+// Every rank's flag of candidate exchange seq (a barrier; the slots are not read).
+__global__ void xwait_kernel(const XPeers* xp, uint32_t seq, DevState* st) {
+    __shared__ Cand s_c[kMaxRanks];
+    __shared__ int s_ok;
+    if (st->status != DLP_RUNNING) return;
+    if (!x_gather_cands(xp, seq, s_c, &s_ok) && threadIdx.x == 0) st->status = kStatusXFail;
+}
+
+// Owner: st->p_local >= 0 (a pivot row), or my_rank == owner_rank (owner_rank >= 0: the
+// carried Phase II row, which travels while the status is "optimal" in phase 1).
+__global__ __launch_bounds__(256) void xrow_send_kernel(const XPeers* xp, uint32_t seq,
+                                                        const int64_t* __restrict__ bits, int64_t ld,
+                                                        const DevState* st, int owner_rank,
+                                                        int my_rank) {
+    if (owner_rank < 0 && st->status != DLP_RUNNING) return;
+    const bool owner = owner_rank >= 0 ? my_rank == owner_rank : st->p_local >= 0;
+    if (!owner) return;   // uniform per launch
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    uint64_t v0 = 0, v1 = 0;
+    if (j < ld) v0 = (uint64_t)bits[j];
+    if (j + 1 < ld) v1 = (uint64_t)bits[j + 1];
+    x_push_row_chunk(xp, seq, j, ld, v0, v1);
+}
+
+__global__ __launch_bounds__(256) void xrow_recv_kernel(const XPeers* xp, uint32_t seq, int64_t ld,
+                                                        int64_t* __restrict__ out, DevState* st,
+                                                        int carry) {
+    __shared__ int s_ok;
+    if (!carry && st->status != DLP_RUNNING) return;
+    if (threadIdx.x == 0) s_ok = x_wait(xp, x_rflag(xp, xp->me, blockIdx.x), seq) ? 1 : 0;
+    __syncthreads();
+    if (!s_ok) {
+        if (threadIdx.x == 0) st->status = kStatusXFail;
+        return;
+    }
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    const uint64_t* row = x_row(xp, xp->me);
+    if (j < ld) out[j] = (int64_t)x_load(row + j);
+    if (j + 1 < ld) out[j + 1] = (int64_t)x_load(row + j + 1);
 }
 
 // ---- general LPs: Phase I -> Phase II transition (include/dlp.h, "general LPs")
@@ -742,9 +804,51 @@ hipError_t launch_ratio(const Geometry& g, const int32_t* basis_in, int32_t* bas
 
 hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32_t* basis,
                          DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
-                         hipStream_t s, bool forced, bool track) {
+                         hipStream_t s, bool forced, bool track, const XPeers* xp, uint32_t seq) {
+    if (nranks > kMaxRanks) return hipErrorInvalidValue;
     select_kernel<<<1, 64, 0, s>>>(cands, nranks, basis, st, g.row_first, g.rows, pricing, log,
-                                   log_cap, forced ? 1 : 0, track ? 1 : 0);
+                                   log_cap, forced ? 1 : 0, track ? 1 : 0, xp, seq);
+    return hipGetLastError();
+}
+
+size_t xblock_layout(int nranks, int64_t ld, XPeers* xp) {
+    const int64_t P = nranks;
+    const int64_t nch = (ld + kXChunk - 1) / kXChunk;
+    const int64_t off_cslot = (2 * P + 7) / 8 * 8;
+    const int64_t off_rflag = off_cslot + 8 * P;
+    const int64_t off_row = (off_rflag + nch + 511) / 512 * 512;   // 4 KiB aligned
+    if (xp) {
+        xp->nranks = nranks;
+        xp->nchunks = nch;
+        xp->off_cslot = off_cslot;
+        xp->off_rflag = off_rflag;
+        xp->off_row = off_row;
+    }
+    return (size_t)(off_row + (ld + kXChunk - 1) / kXChunk * kXChunk) * sizeof(uint64_t);
+}
+
+hipError_t launch_xcand_send(const XPeers* xp, uint32_t seq, const Cand* cand_send, const DevState* st,
+                             hipStream_t s) {
+    xcand_send_kernel<<<1, 64, 0, s>>>(xp, seq, cand_send, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_xwait(const XPeers* xp, uint32_t seq, DevState* st, hipStream_t s) {
+    xwait_kernel<<<1, 64, 0, s>>>(xp, seq, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_xrow_send(const XPeers* xp, uint32_t seq, const int64_t* bits, int64_t ld,
+                            const DevState* st, int owner_rank, int my_rank, hipStream_t s) {
+    const int blocks = (int)((ld + kXChunk - 1) / kXChunk);
+    xrow_send_kernel<<<blocks, 256, 0, s>>>(xp, seq, bits, ld, st, owner_rank, my_rank);
+    return hipGetLastError();
+}
+
+hipError_t launch_xrow_recv(const XPeers* xp, uint32_t seq, int64_t ld, int64_t* out, DevState* st,
+                            hipStream_t s) {
+    const int blocks = (int)((ld + kXChunk - 1) / kXChunk);
+    xrow_recv_kernel<<<blocks, 256, 0, s>>>(xp, seq, ld, out, st, 0);
     return hipGetLastError();
 }
 

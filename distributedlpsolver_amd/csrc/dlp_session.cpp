@@ -10,6 +10,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -77,6 +79,27 @@ struct dlp_session {
     dlp::DevState* host_st = nullptr;   // pinned
     ncclComm_t comm = nullptr;
     bool use_rccl = false;
+    // how the exchange travels (exchange sessions): X_HOST = the caller (step API),
+    // X_RCCL = all-gather + MAX all-reduce, X_PEER = direct stores into the ranks'
+    // exchange blocks (dlp_sessions_connect / dlp_session_connect_ipc /
+    // dlp_session_set_exchange)
+    enum XMode { X_HOST = 0, X_RCCL = 1, X_PEER = 2 };
+    int xmode = X_HOST;
+    uint64_t* xblk = nullptr;            // this rank's exchange block (uncached device memory)
+    bool xblk_uncached = false;
+    dlp::XPeers* xpeers = nullptr;       // device copy of the peer table (X_PEER)
+    dlp::XPeers xpeers_host{};
+    std::vector<void*> ipc_open;         // peers' blocks opened through IPC
+    uint32_t* xabort = nullptr;          // pinned host word the device waits read (abort)
+    uint32_t xseq_c = 0, xseq_r = 0;     // exchange counters, identical on every rank
+    // failure containment on the exchange path: a window's wait polls the
+    // stream, the communicator's async error, the caller's / the in-process group's abort
+    // word and a stall limit, and aborts the communicator instead of blocking forever
+    std::atomic<int> abort_req{0};               // dlp_session_abort (any thread)
+    std::atomic<int>* group_failed = nullptr;    // solve_in_process: the first failed rank, -1
+    double stall_limit_s = 600.0;                // dlp_session_set_exchange_timeout (0 = none)
+    int64_t fault_after_polls = -1;              // dlp_session_inject_fault (tests)
+    int64_t npolls = 0;
     // deferred, single rank: one launch for ratio + selection + pivot row (opt-in: measured
     // equal to two launches, C2 24.7 vs 25.0 us/pivot, profiles/r02c/tune_*_fused.txt)
     bool fuse_pivot = false;
@@ -118,7 +141,8 @@ struct dlp_session {
     // the last tableau pass, pass geometry; update-kernel launch accounting
     dlp::Defer d;
     int since_flush = 0;
-    int defer_rb = 64, defer_occ = 0;   // pass band rows (128 when streaming), WG/CU cap
+    int defer_rb = 64, defer_occ = 0;   // pass band rows (auto_defer_rb), WG/CU cap
+    int defer_rb_req = 0;               // the caller's band rows (0 = auto: follows the form)
     std::vector<uint8_t> ev_flush;   // per timed slot: a pass ran in it
     int64_t upd_launches = 0;
     // lookahead: two tableau buffers; the pass of block b reads Tb[tcur]
@@ -146,10 +170,27 @@ int auto_rows_per_block(const dlp_session* s) { return s->streaming ? 8 : 4; }
 // streaming pass over >= 16k local rows (form 21 reads P once per band: C3 7,227 / 7,361 / 7,433
 // pivots/s at 256 / 512 / 768 rows on one box, 768 best on two, profiles/r02q/).  Fewer rows (a
 // rank of a multi-GPU C3) keep 256: at 4096 rows, 768-row bands would be 6 x 257 workgroups,
-// two rounds of the chip's 768 pass slots plus a few, a long tail
+// two rounds of the chip's 768 pass slots plus a few, a long tail.  Only the register-resident
+// forms (3/4/5/20/21/22) take tall bands: forms 0-2 stage the band's coefficients in LDS
+// (fit_defer_rb).
+bool tall_band_form(int form) {
+    return form == 3 || form == 4 || form == 5 || form == 20 || form == 21 || form == 22;
+}
+// Forms 0-2 hold the band's K coefficients per row + a row index in dynamic LDS and s_pl[K]
+// statically: K * rb * 8 + rb * 4 + K * 4 <= 160 KiB.  Bands only change the work split, never
+// the result (every element sees the same K-step sequence), so the clamp is exact.
+int fit_defer_rb(const dlp_session* s, int rb) {
+    if (s->d.form <= 2) {
+        const int K = std::max(s->d.K, 1);
+        const int cap = (160 * 1024 - 4 * K) / (8 * K + 4);
+        rb = std::min(rb, cap);
+    }
+    return std::max(1, std::min(rb, 1024));
+}
 int auto_defer_rb(const dlp_session* s) {
-    if (!s->streaming) return 64;
-    return s->d.K == 64 && s->rows >= 16384 ? 768 : 256;
+    if (!s->streaming) return fit_defer_rb(s, 64);
+    const bool tall = s->d.K == 64 && s->rows >= 16384 && tall_band_form(s->d.form);
+    return fit_defer_rb(s, tall ? 768 : 256);
 }
 
 // Row i of a general LP's standard-form tableau (include/dlp.h, "general LPs").
@@ -245,6 +286,10 @@ void free_session(dlp_session* s) {
     if (s->ev_pass) (void)hipEventDestroy(s->ev_pass);
     if (s->pstream) (void)hipStreamDestroy(s->pstream);
     if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
+    for (void* p : s->ipc_open) (void)hipIpcCloseMemHandle(p);
+    if (s->xblk) (void)hipFree(s->xblk);
+    if (s->xpeers) (void)hipFree(s->xpeers);
+    if (s->xabort) (void)hipHostFree(s->xabort);
     if (s->host_st) (void)hipHostFree(s->host_st);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -390,9 +435,12 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         // streaming tableaus: 64-step blocks through the DPP-coefficient pass (form 21: C3
         // 8.4 ms per 64-step pass = 0.131 ms per step against 0.197 for form 4's 32-step
         // pass, 6,100 vs 4,500 pivots/s; profiles/r02j/)
+        // a host-driven rank (the step API) takes the geometry the same rank would run over
+        // RCCL, so the multi-GPU split can be exercised without RCCL (general LPs stay eager)
         if (K == 0)
-            K = (host_driven || tile != dlp::kDeferTile || tiny || s->cluster) ? 1
-                                                                             : (s->streaming ? 64 : 16);
+            K = ((host_driven && s->general) || tile != dlp::kDeferTile || tiny || s->cluster)
+                    ? 1
+                    : (s->streaming ? 64 : 16);
         if (s->cluster && K != 1) s->cluster = false;
         if (K > 1 && tile != dlp::kDeferTile) {
             set_error("defer > 1 needs a 512-column update variant");
@@ -463,7 +511,8 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         HIP_TRY(hipMalloc(&s->d.nzc, sizeof(int32_t) * (s->rows + 1)));
         HIP_TRY(hipMemsetAsync(s->d.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
         HIP_TRY(hipMemsetAsync(s->d.P, 0, sizeof(double) * kt * s->ld, s->stream));
-        s->defer_rb = opt->rows_per_block > 0 ? std::min(opt->rows_per_block, 1024) : auto_defer_rb(s);
+        s->defer_rb_req = opt->rows_per_block > 0 ? opt->rows_per_block : 0;
+        s->defer_rb = s->defer_rb_req > 0 ? fit_defer_rb(s, s->defer_rb_req) : auto_defer_rb(s);
     }
     HIP_TRY(hipMemsetAsync(s->prow_send, 0, sizeof(int64_t) * s->ld, s->stream));
 
@@ -557,6 +606,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         NCCL_TRY(ncclCommInitRank(&s->comm, nranks, id, rank));
         s->use_rccl = true;
     }
+    s->xmode = s->use_rccl ? dlp_session::X_RCCL : dlp_session::X_HOST;
     s->ev_per_pivot = opt->timing == 1 ? 2 : (opt->timing >= 2 ? 5 : 0);
     if (s->ev_per_pivot) {
         s->ev.resize((size_t)s->ev_per_pivot * opt->check_interval);
@@ -668,10 +718,21 @@ int la_disable(dlp_session* s) {
     return DLP_OK;
 }
 
+// The exchange kernels' peer table (X_PEER) or NULL.
+inline const dlp::XPeers* xp_of(const dlp_session* s) {
+    return s->xmode == dlp_session::X_PEER ? s->xpeers : nullptr;
+}
+
 // One deferred pivot: replayed ratio test, exchange, replayed pivot row (+
 // objective row and pricing), and the pass when the block is full or `last`.
-int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
+// Three phases, so that dlp_sessions_run can interleave the ranks of one device
+// (every rank's phase p is enqueued before any rank's phase p + 1: a wait for a
+// peer's message is then always queued after the launch that sends it):
+//   0 ratio test (+ candidate send) | 1 select (+ wait) + pivot row (+ send) |
+//   2 commit (+ wait) + pass
+int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     const dlp_options& o = s->opt;
+    const dlp::XPeers* xp = xp_of(s);
     // timing 2: 5 events per pivot (every phase); timing 1: 2 events around the pass only
     hipEvent_t* ev = s->ev_per_pivot == 5 ? &s->ev[(size_t)slot * 5] : nullptr;
     hipEvent_t* evp = s->ev_per_pivot == 2 ? &s->ev[(size_t)slot * 2] : nullptr;
@@ -688,34 +749,44 @@ int enqueue_pivot_defer(dlp_session* s, int64_t slot, bool last) {
             pseal = 1 - s->cur;
         }
     }
-    if (ev) HIP_TRY(hipEventRecord(ev[0], s->stream));
-    if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) {
-        // single rank: ratio test, selection and pivot row in one launch
-        HIP_TRY(dlp::launch_pivot_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
-                                        s->ratio_blocks_max, o.tol_dj, o.tol_piv, o.pricing, s->log,
-                                        s->log_cap, s->stream));
-    } else {
-    HIP_TRY(dlp::launch_ratio_defer(gsel, *dcur, s->basis, s->pp, s->st, s->partials,
-                                    s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
-                                    o.tol_piv, o.pricing, s->log, s->log_cap, s->stream, dprev,
-                                    pseal));
-    if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
-    if (s->exchange) {
-        NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
-                               s->stream));
-        HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, o.pricing,
-                                   s->log, s->log_cap, s->stream, false, true));
+    if (phase == 0) {
+        if (ev) HIP_TRY(hipEventRecord(ev[0], s->stream));
+        if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) {
+            // single rank: ratio test, selection and pivot row in one launch
+            HIP_TRY(dlp::launch_pivot_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
+                                            s->ratio_blocks_max, o.tol_dj, o.tol_piv, o.pricing, s->log,
+                                            s->log_cap, s->stream));
+            return DLP_OK;
+        }
+        if (xp) s->xseq_c += 1;
+        HIP_TRY(dlp::launch_ratio_defer(gsel, *dcur, s->basis, s->pp, s->st, s->partials,
+                                        s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
+                                        o.tol_piv, o.pricing, s->log, s->log_cap, s->stream, dprev,
+                                        pseal, xp, s->xseq_c));
+        if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
+        if (s->xmode == dlp_session::X_RCCL)
+            NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
+                                   s->stream));
+        return DLP_OK;
     }
-    if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
-    HIP_TRY(dlp::launch_prow_defer(gsel, *dcur, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
-                                   s->log_cap, s->exchange ? 2 : 1, s->stream, dprev, pseal));
-    if (s->exchange) {
-        NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
-                               s->comm, s->stream));
+    if (phase == 1) {
+        if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) return DLP_OK;
+        if (s->exchange)
+            HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, o.pricing,
+                                       s->log, s->log_cap, s->stream, false, true, xp, s->xseq_c));
+        if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
+        if (xp) s->xseq_r += 1;
+        HIP_TRY(dlp::launch_prow_defer(gsel, *dcur, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
+                                       s->log_cap, s->exchange ? 2 : 1, s->stream, dprev, pseal, xp,
+                                       s->xseq_r));
+        if (s->xmode == dlp_session::X_RCCL)
+            NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
+                                   s->comm, s->stream));
+        return DLP_OK;
+    }
+    if (s->exchange)
         HIP_TRY(dlp::launch_commit_defer(gsel, *dcur, s->st, s->prow_recv, s->pp, o.tol_dj, s->log,
-                                         s->log_cap, s->stream));
-    }
-    }
+                                         s->log_cap, s->stream, xp, s->xseq_r));
     if (ev) HIP_TRY(hipEventRecord(ev[3], s->stream));
     s->since_flush += 1;
     const bool flush = last || s->since_flush >= s->d.K;
@@ -767,23 +838,36 @@ int enqueue_cluster(dlp_session* s, int64_t count) {
     return DLP_OK;
 }
 
-int enqueue_pivot(dlp_session* s, int64_t slot, bool last = true) {
-    if (s->d.K > 1) return enqueue_pivot_defer(s, slot, last);
+// One eager pivot in the same three phases (pivot_defer_phase).
+int pivot_eager_phase(dlp_session* s, int phase, int64_t slot) {
+    const dlp::XPeers* xp = xp_of(s);
     hipEvent_t* ev = s->ev_per_pivot ? &s->ev[(size_t)slot * s->ev_per_pivot] : nullptr;
     const bool all = s->ev_per_pivot == 5;
-    if (all) HIP_TRY(hipEventRecord(ev[0], s->stream));
-    CALL_TRY(enqueue_candidate(s));
-    if (all) HIP_TRY(hipEventRecord(ev[1], s->stream));
-    if (s->exchange) {
-        NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
-                               s->stream));
-        CALL_TRY(enqueue_select(s));
+    if (phase == 0) {
+        if (all) HIP_TRY(hipEventRecord(ev[0], s->stream));
+        CALL_TRY(enqueue_candidate(s));
+        if (xp) HIP_TRY(dlp::launch_xcand_send(xp, ++s->xseq_c, s->cand_send, s->st, s->stream));
+        if (all) HIP_TRY(hipEventRecord(ev[1], s->stream));
+        if (s->xmode == dlp_session::X_RCCL)
+            NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
+                                   s->stream));
+        return DLP_OK;
     }
-    if (all) HIP_TRY(hipEventRecord(ev[2], s->stream));
-    CALL_TRY(enqueue_prow(s));
-    if (s->exchange)
-        NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
-                               s->comm, s->stream));
+    if (phase == 1) {
+        if (s->exchange)
+            HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, s->opt.pricing,
+                                       s->log, s->log_cap, s->stream, false, false, xp, s->xseq_c));
+        if (all) HIP_TRY(hipEventRecord(ev[2], s->stream));
+        CALL_TRY(enqueue_prow(s));
+        if (xp)
+            HIP_TRY(dlp::launch_xrow_send(xp, ++s->xseq_r, s->prow_send, s->ld, s->st, -1, s->rank,
+                                          s->stream));
+        if (s->xmode == dlp_session::X_RCCL)
+            NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
+                                   s->comm, s->stream));
+        return DLP_OK;
+    }
+    if (xp) HIP_TRY(dlp::launch_xrow_recv(xp, s->xseq_r, s->ld, s->prow_recv, s->st, s->stream));
     if (all) HIP_TRY(hipEventRecord(ev[3], s->stream));
     if (s->ev_per_pivot == 2) HIP_TRY(hipEventRecord(ev[0], s->stream));
     CALL_TRY(enqueue_update(s));
@@ -792,8 +876,17 @@ int enqueue_pivot(dlp_session* s, int64_t slot, bool last = true) {
     return DLP_OK;
 }
 
+int pivot_phase(dlp_session* s, int phase, int64_t slot, bool last) {
+    return s->d.K > 1 ? pivot_defer_phase(s, phase, slot, last) : pivot_eager_phase(s, phase, slot);
+}
+
+int enqueue_pivot(dlp_session* s, int64_t slot, bool last = true) {
+    for (int ph = 0; ph < 3; ++ph) CALL_TRY(pivot_phase(s, ph, slot, last));
+    return DLP_OK;
+}
+
 // General LPs: forced drive-out pivot on global row `row` (same exchange shape
-// as a pivot: candidate all-gather, pivot-row MAX all-reduce).
+// as a pivot: candidate exchange, pivot-row exchange), in the same three phases.
 int enqueue_forced_candidate(dlp_session* s, int64_t row) {
     const dlp_options& o = s->opt;
     HIP_TRY(dlp::launch_drive(s->g, row, s->basis, s->st, o.tol_piv, s->cand_send,
@@ -804,21 +897,37 @@ int enqueue_forced_candidate(dlp_session* s, int64_t row) {
 int enqueue_forced_select(dlp_session* s) {
     if (s->exchange) {
         HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, s->opt.pricing,
-                                   s->log, s->log_cap, s->stream, true));
+                                   s->log, s->log_cap, s->stream, true, false, xp_of(s), s->xseq_c));
         HIP_TRY(dlp::launch_gather_q(s->g, s->st, s->colq, s->stream));
     }
     return enqueue_prow(s);
 }
-int enqueue_forced(dlp_session* s, int64_t row) {
-    CALL_TRY(enqueue_forced_candidate(s, row));
-    if (s->exchange)
-        NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
-                               s->stream));
-    CALL_TRY(enqueue_forced_select(s));
-    if (s->exchange)
-        NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
-                               s->comm, s->stream));
+int forced_phase(dlp_session* s, int phase, int64_t row) {
+    const dlp::XPeers* xp = xp_of(s);
+    if (phase == 0) {
+        CALL_TRY(enqueue_forced_candidate(s, row));
+        if (xp) HIP_TRY(dlp::launch_xcand_send(xp, ++s->xseq_c, s->cand_send, s->st, s->stream));
+        if (s->xmode == dlp_session::X_RCCL)
+            NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
+                                   s->stream));
+        return DLP_OK;
+    }
+    if (phase == 1) {
+        CALL_TRY(enqueue_forced_select(s));
+        if (xp)
+            HIP_TRY(dlp::launch_xrow_send(xp, ++s->xseq_r, s->prow_send, s->ld, s->st, -1, s->rank,
+                                          s->stream));
+        if (s->xmode == dlp_session::X_RCCL)
+            NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
+                                   s->comm, s->stream));
+        return DLP_OK;
+    }
+    if (xp) HIP_TRY(dlp::launch_xrow_recv(xp, s->xseq_r, s->ld, s->prow_recv, s->st, s->stream));
     return enqueue_update(s);
+}
+int enqueue_forced(dlp_session* s, int64_t row) {
+    for (int ph = 0; ph < 3; ++ph) CALL_TRY(forced_phase(s, ph, row));
+    return DLP_OK;
 }
 // Carried Phase II objective row -> objective row on every rank.
 int enqueue_carry_out(dlp_session* s) {
@@ -830,12 +939,35 @@ int enqueue_carry_in(dlp_session* s) {
     HIP_TRY(dlp::launch_price_init(s->g, s->pp, s->opt.tol_dj, s->opt.update_variant, s->stream));
     return DLP_OK;
 }
-int enqueue_carry(dlp_session* s) {
-    CALL_TRY(enqueue_carry_out(s));
-    if (s->exchange)
-        NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
-                               s->comm, s->stream));
+// Peer exchange: the carried row may only overwrite a rank's row region after that rank
+// has read the previous pivot row, so the carry starts with an empty candidate exchange
+// (a barrier: every rank's select-wait sees every rank's message).
+int carry_phase(dlp_session* s, int phase) {
+    const dlp::XPeers* xp = xp_of(s);
+    if (phase == 0) {
+        if (xp) {
+            HIP_TRY(hipMemsetAsync(s->cand_send, 0, sizeof(dlp::Cand), s->stream));
+            HIP_TRY(dlp::launch_xcand_send(xp, ++s->xseq_c, s->cand_send, s->st, s->stream));
+        }
+        return DLP_OK;
+    }
+    if (phase == 1) {
+        if (xp) HIP_TRY(dlp::launch_xwait(xp, s->xseq_c, s->st, s->stream));
+        CALL_TRY(enqueue_carry_out(s));
+        if (xp)
+            HIP_TRY(dlp::launch_xrow_send(xp, ++s->xseq_r, s->prow_send, s->ld, s->st, s->nranks - 1,
+                                          s->rank, s->stream));
+        if (s->xmode == dlp_session::X_RCCL)
+            NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
+                                   s->comm, s->stream));
+        return DLP_OK;
+    }
+    if (xp) HIP_TRY(dlp::launch_xrow_recv(xp, s->xseq_r, s->ld, s->prow_recv, s->st, s->stream));
     return enqueue_carry_in(s);
+}
+int enqueue_carry(dlp_session* s) {
+    for (int ph = 0; ph < 3; ++ph) CALL_TRY(carry_phase(s, ph));
+    return DLP_OK;
 }
 
 int poll(dlp_session* s);
@@ -878,13 +1010,80 @@ int finish_phase1(dlp_session* s) {
     return DLP_OK;
 }
 
+// Abort the RCCL communicator (its kernels in flight return) and fail the window.
+int abort_exchange(dlp_session* s, const std::string& why) {
+    if (s->xabort) __atomic_store_n(s->xabort, 1u, __ATOMIC_SEQ_CST);   // ends the device waits
+    if (s->comm) {
+        (void)ncclCommAbort(s->comm);   // frees the communicator; pending collectives exit
+        s->comm = nullptr;
+    }
+    s->use_rccl = false;
+    s->status = DLP_ERR_RCCL;
+    set_error("exchange aborted: " + why);
+    return DLP_ERR_RCCL;
+}
+
+// Wait for the session stream.  A single-GPU session blocks in hipStreamSynchronize; an
+// exchange session polls hipStreamQuery, so that a peer that never arrives (a failed rank,
+// a dead process) ends the wait: ncclCommGetAsyncError, the in-process group's failure word,
+// dlp_session_abort and a stall limit each abort the communicator and return DLP_ERR_RCCL.
+int wait_stream(dlp_session* s) {
+    if (s->fault_after_polls >= 0 && s->npolls++ >= s->fault_after_polls) {
+        s->fault_after_polls = -1;
+        (void)hipStreamSynchronize(s->stream);
+        if (s->exchange && s->xmode != dlp_session::X_HOST)
+            return abort_exchange(s, "injected fault (dlp_session_inject_fault)");
+        set_error("injected fault (dlp_session_inject_fault)");
+        return DLP_ERR_HIP;
+    }
+    if (!s->exchange || s->xmode == dlp_session::X_HOST) {
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        return DLP_OK;
+    }
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (int64_t spin = 0;; ++spin) {
+        const hipError_t e = hipStreamQuery(s->stream);
+        if (e == hipSuccess) return DLP_OK;
+        if (e != hipErrorNotReady) {
+            set_error(std::string("hipStreamQuery: ") + hipGetErrorString(e));
+            (void)abort_exchange(s, hipGetErrorString(e));
+            return DLP_ERR_HIP;
+        }
+        if (s->abort_req.load(std::memory_order_relaxed)) return abort_exchange(s, "dlp_session_abort");
+        if (s->group_failed) {
+            const int f = s->group_failed->load(std::memory_order_relaxed);
+            if (f >= 0 && f != s->rank) return abort_exchange(s, "rank " + std::to_string(f) + " failed");
+        }
+        if (s->comm && (spin & 63) == 0) {
+            ncclResult_t ae = ncclSuccess;
+            if (ncclCommGetAsyncError(s->comm, &ae) == ncclSuccess && ae != ncclSuccess &&
+                ae != ncclInProgress)
+                return abort_exchange(s, std::string("RCCL async error: ") + ncclGetErrorString(ae));
+        }
+        const double el = std::chrono::duration<double>(clk::now() - t0).count();
+        if (s->stall_limit_s > 0 && el > s->stall_limit_s)
+            return abort_exchange(s, "no progress for " + std::to_string(el) + " s");
+        if (spin < 2000)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 // Sync, read the device state, fold event timings of pivots that really ran.
 int poll(dlp_session* s) {
     const int64_t before = s->npivots;
     HIP_TRY(hipMemcpyAsync(s->host_st, s->st, sizeof(dlp::DevState), hipMemcpyDeviceToHost,
                            s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
+    CALL_TRY(wait_stream(s));
     s->npivots = s->host_st->npivots;
+    if (s->host_st->status == dlp::kStatusXFail) {
+        s->status = DLP_ERR_HIP;
+        set_error("peer exchange: a wait for another rank timed out or was aborted (rank " +
+                  std::to_string(s->rank) + ")");
+        return DLP_ERR_HIP;
+    }
     if (s->host_st->status != DLP_RUNNING && s->host_st->status != dlp::kStatusSkip &&
         s->status == DLP_RUNNING)
         s->status = s->host_st->status;
@@ -1095,19 +1294,26 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
     std::vector<dlp_session*> ss(P, nullptr);
     std::vector<int> rc(P, DLP_OK);
     std::vector<std::string> err(P);
+    // the first rank to fail; the others' waits see it and abort their communicators
+    // (wait_stream), so no thread stays blocked behind a collective that cannot complete
+    std::atomic<int> failed{-1};
     auto on_ranks = [&](auto&& fn) {
         std::vector<std::thread> th;
         for (int r = 0; r < P; ++r)
             th.emplace_back([&, r] {
                 rc[r] = fn(r);
-                if (rc[r] < 0) err[r] = dlp_last_error();
+                if (rc[r] < 0) {
+                    err[r] = dlp_last_error();
+                    int none = -1;
+                    failed.compare_exchange_strong(none, r);
+                }
             });
         for (auto& t : th) t.join();
-        for (int r = 0; r < P; ++r)
-            if (rc[r] < 0) {
-                set_error("rank " + std::to_string(r) + ": " + err[r]);
-                return rc[r];
-            }
+        const int f = failed.load();
+        if (f >= 0) {
+            set_error("rank " + std::to_string(f) + ": " + err[f]);
+            return rc[f];
+        }
         return DLP_OK;
     };
     int res = on_ranks([&](int r) {
@@ -1129,11 +1335,14 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
             return k;
         }
         comms[r] = nullptr;   // the session owns it now
+        s->group_failed = &failed;
         ss[r] = s;
         return DLP_OK;
     });
     if (res == DLP_OK) {
         res = on_ranks([&](int r) {
+            if (const char* e = std::getenv("DLP_TEST_FAIL_RANK"))   // tests: fail this rank's 2nd poll
+                if (std::atoi(e) == r) ss[r]->fault_after_polls = 1;
             int64_t done = 0;
             return dlp_session_run(ss[r], o.max_pivots, &done);
         });
@@ -1155,6 +1364,91 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
     for (auto c : comms)
         if (c) (void)ncclCommDestroy(c);
     return res;
+}
+
+// ---- peer exchange set-up ------------------------------------
+// This rank's exchange block (uncached device memory, zeroed: flags start below every seq)
+// and the pinned abort word its waits read.
+int ensure_xblock(dlp_session* s) {
+    if (s->xblk) return DLP_OK;
+    if (!s->exchange) {
+        set_error("the peer exchange needs a row-block rank session (nranks > 1 or an RCCL id)");
+        return DLP_ERR_STATE;
+    }
+    if (s->nranks > dlp::kMaxRanks) {
+        set_error("the peer exchange supports at most 64 ranks");
+        return DLP_ERR_UNSUPPORTED;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t bytes = dlp::xblock_layout(s->nranks, s->ld, &s->xpeers_host);
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess) {
+        s->xblk_uncached = true;
+    } else {
+        (void)hipGetLastError();
+        HIP_TRY(hipMalloc(&p, bytes));   // system-scope accesses keep it coherent either way
+    }
+    s->xblk = (uint64_t*)p;
+    HIP_TRY(hipMemset(s->xblk, 0, bytes));
+    if (!s->xabort) {
+        HIP_TRY(hipHostMalloc((void**)&s->xabort, 64, hipHostMallocCoherent | hipHostMallocMapped));
+        *s->xabort = 0;
+    }
+    if (!s->xpeers) HIP_TRY(hipMalloc(&s->xpeers, sizeof(dlp::XPeers)));
+    return DLP_OK;
+}
+
+// Install the peer table (bases[r] = rank r's block as this device addresses it).
+int install_peers(dlp_session* s, const std::vector<uint64_t*>& bases) {
+    dlp::XPeers& x = s->xpeers_host;
+    (void)dlp::xblock_layout(s->nranks, s->ld, &x);
+    for (int r = 0; r < dlp::kMaxRanks; ++r) x.base[r] = r < (int)bases.size() ? bases[r] : nullptr;
+    x.me = s->rank;
+    void* dabort = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dabort, s->xabort, 0));
+    x.abort_word = (const uint32_t*)dabort;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemcpy(s->xpeers, &x, sizeof(x), hipMemcpyHostToDevice));
+    s->xmode = dlp_session::X_PEER;
+    if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
+    if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
+    return DLP_OK;
+}
+
+int connect_ipc(dlp_session* s, const uint8_t* handles) {
+    CALL_TRY(ensure_xblock(s));
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    std::vector<uint64_t*> bases(s->nranks, nullptr);
+    for (int r = 0; r < s->nranks; ++r) {
+        if (r == s->rank) {
+            bases[r] = s->xblk;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)r * sizeof(hipIpcMemHandle_t), sizeof(h));
+        void* p = nullptr;
+        HIP_TRY(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        s->ipc_open.push_back(p);
+        bases[r] = (uint64_t*)p;
+    }
+    return install_peers(s, bases);
+}
+
+// Phase-interleaved multi-rank run (dlp_sessions_run): every rank's phase p before any
+// rank's phase p + 1, for every pivot, from one host thread.
+int sessions_phase(dlp_session* const* ss, int P, int phase, int64_t slot, bool last, int kind,
+                   int64_t row) {
+    for (int r = 0; r < P; ++r) {
+        HIP_TRY(hipSetDevice(ss[r]->device));
+        if (kind == 0)
+            CALL_TRY(pivot_phase(ss[r], phase, slot, last));
+        else if (kind == 1)
+            CALL_TRY(forced_phase(ss[r], phase, row));
+        else
+            CALL_TRY(carry_phase(ss[r], phase));
+    }
+    return DLP_OK;
 }
 
 }  // namespace
@@ -1498,8 +1792,9 @@ int dlp_comm_unique_id(void* out128) {
 
 int dlp_session_run(dlp_session* s, int64_t max_pivots, int64_t* pivots_done) {
     if (!s || max_pivots < 0) return DLP_ERR_ARG;
-    if (s->exchange && !s->use_rccl) {
-        set_error("session has no RCCL communicator: drive it with dlp_session_step_*");
+    if (s->exchange && s->xmode == dlp_session::X_HOST) {
+        set_error("session has no communicator: drive it with dlp_session_step_*, or connect the "
+                  "ranks (dlp_sessions_connect / dlp_session_connect_ipc)");
         return DLP_ERR_STATE;
     }
     HIP_TRY(hipSetDevice(s->device));
@@ -1706,7 +2001,8 @@ int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_bloc
             set_error("a deferred session (defer > 1) needs a 512-column update variant");
             return DLP_ERR_ARG;
         }
-        s->defer_rb = rows_per_block > 0 ? std::min(rows_per_block, 1024) : auto_defer_rb(s);
+        s->defer_rb_req = rows_per_block > 0 ? rows_per_block : 0;
+        s->defer_rb = s->defer_rb_req > 0 ? fit_defer_rb(s, s->defer_rb_req) : auto_defer_rb(s);
     }
     s->opt.update_variant = update_variant;
     s->opt.nontemporal = nontemporal;
@@ -1744,9 +2040,199 @@ int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
     if (form >= 0) {
         s->d.form = form;
         s->dslot[0].form = s->dslot[1].form = form;
+        // the band follows the form (auto), or is clamped to what the form's LDS holds
+        if (s->d.K > 1)
+            s->defer_rb = s->defer_rb_req > 0 ? fit_defer_rb(s, s->defer_rb_req) : auto_defer_rb(s);
     }
     if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
     if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
+    return DLP_OK;
+}
+
+int dlp_sessions_connect(dlp_session* const* ranks, int nranks) {
+    if (!ranks || nranks <= 0 || nranks > dlp::kMaxRanks) return DLP_ERR_ARG;
+    std::vector<dlp_session*> by(nranks, nullptr);
+    for (int k = 0; k < nranks; ++k) {
+        dlp_session* s = ranks[k];
+        if (!s || s->nranks != nranks || s->rank < 0 || s->rank >= nranks || by[s->rank]) {
+            set_error("dlp_sessions_connect: every rank session of the solve, once each");
+            return DLP_ERR_ARG;
+        }
+        by[s->rank] = s;
+    }
+    for (dlp_session* s : by) CALL_TRY(ensure_xblock(s));
+    // direct peer access between the devices involved (xGMI)
+    for (dlp_session* a : by)
+        for (dlp_session* b : by) {
+            if (a->device == b->device) continue;
+            int ok = 0;
+            HIP_TRY(hipDeviceCanAccessPeer(&ok, a->device, b->device));
+            if (!ok) {
+                set_error("device " + std::to_string(a->device) + " cannot access device " +
+                          std::to_string(b->device));
+                return DLP_ERR_UNSUPPORTED;
+            }
+            HIP_TRY(hipSetDevice(a->device));
+            const hipError_t e = hipDeviceEnablePeerAccess(b->device, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_TRY(e);
+            (void)hipGetLastError();
+        }
+    std::vector<uint64_t*> bases(nranks);
+    for (int r = 0; r < nranks; ++r) bases[r] = by[r]->xblk;
+    for (dlp_session* s : by) {
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        CALL_TRY(install_peers(s, bases));
+    }
+    return DLP_OK;
+}
+
+int dlp_session_exchange_handle(dlp_session* s, void* out64) {
+    if (!s || !out64) return DLP_ERR_ARG;
+    CALL_TRY(ensure_xblock(s));
+    hipIpcMemHandle_t h;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipIpcGetMemHandle(&h, s->xblk));
+    std::memcpy(out64, &h, sizeof(h));
+    return DLP_OK;
+}
+
+int dlp_session_connect_ipc(dlp_session* s, const void* handles) {
+    if (!s || !handles) return DLP_ERR_ARG;
+    if (!s->ipc_open.empty() || s->xmode == dlp_session::X_PEER) {
+        set_error("dlp_session_connect_ipc: already connected");
+        return DLP_ERR_STATE;
+    }
+    return connect_ipc(s, (const uint8_t*)handles);
+}
+
+int dlp_session_set_exchange(dlp_session* s, int mode) {
+    if (!s || (mode != DLP_XCHG_RCCL && mode != DLP_XCHG_PEER)) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    if (mode == DLP_XCHG_RCCL) {
+        if (!s->comm) {
+            set_error("the session has no RCCL communicator");
+            return DLP_ERR_STATE;
+        }
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        s->xmode = dlp_session::X_RCCL;
+        return DLP_OK;
+    }
+    if (s->xpeers_host.nranks == s->nranks && s->xpeers_host.base[s->rank] == s->xblk && s->xblk) {
+        s->xmode = dlp_session::X_PEER;   // connected before
+        return DLP_OK;
+    }
+    if (!s->comm) {
+        set_error("dlp_session_set_exchange(PEER) without a communicator: use dlp_sessions_connect "
+                  "or dlp_session_connect_ipc");
+        return DLP_ERR_STATE;
+    }
+    // every rank's IPC handle over the communicator itself (one all-gather at set-up)
+    CALL_TRY(ensure_xblock(s));
+    const size_t hb = sizeof(hipIpcMemHandle_t);
+    std::vector<uint8_t> all(hb * s->nranks);
+    uint8_t* dbuf = nullptr;
+    HIP_TRY(hipMalloc(&dbuf, hb * (s->nranks + 1)));
+    hipIpcMemHandle_t h;
+    HIP_TRY(hipIpcGetMemHandle(&h, s->xblk));
+    HIP_TRY(hipMemcpy(dbuf + hb * s->nranks, &h, hb, hipMemcpyHostToDevice));
+    const ncclResult_t nr = ncclAllGather(dbuf + hb * s->nranks, dbuf, hb, ncclUint8, s->comm, s->stream);
+    if (nr != ncclSuccess) {
+        (void)hipFree(dbuf);
+        set_error(std::string("ncclAllGather (IPC handles): ") + ncclGetErrorString(nr));
+        return DLP_ERR_RCCL;
+    }
+    CALL_TRY(wait_stream(s));
+    HIP_TRY(hipMemcpy(all.data(), dbuf, hb * s->nranks, hipMemcpyDeviceToHost));
+    HIP_TRY(hipFree(dbuf));
+    return connect_ipc(s, all.data());
+}
+
+int dlp_session_get_exchange(dlp_session* s, int* mode) {
+    if (!s || !mode) return DLP_ERR_ARG;
+    *mode = s->xmode;
+    return DLP_OK;
+}
+
+int dlp_sessions_run(dlp_session* const* ranks, int nranks, int64_t max_pivots, int64_t* pivots_done) {
+    if (!ranks || nranks <= 0 || max_pivots < 0) return DLP_ERR_ARG;
+    std::vector<dlp_session*> ss(ranks, ranks + nranks);
+    for (dlp_session* s : ss)
+        if (!s || s->nranks != nranks || s->cluster ||
+            (nranks > 1 && s->xmode != dlp_session::X_PEER)) {
+            set_error("dlp_sessions_run: the rank sessions of one solve, connected by dlp_sessions_connect");
+            return DLP_ERR_STATE;
+        }
+    dlp_session* s0 = ss[0];
+    const int64_t start = s0->npivots;
+    int64_t budget = std::min<int64_t>(max_pivots, s0->opt.max_pivots - s0->launched);
+    auto poll_all = [&]() -> int {
+        for (dlp_session* s : ss) {
+            HIP_TRY(hipSetDevice(s->device));
+            CALL_TRY(poll(s));
+        }
+        for (dlp_session* s : ss)
+            if (s->status != s0->status || s->npivots != s0->npivots) {
+                set_error("dlp_sessions_run: ranks diverged");
+                return DLP_ERR_STATE;
+            }
+        return DLP_OK;
+    };
+    while (s0->status == DLP_RUNNING && budget > 0) {
+        if (s0->drive_next < s0->drive.size() || s0->carry_pending) {   // Phase I -> II switch
+            while (s0->drive_next < s0->drive.size() && budget > 0) {
+                const int64_t row = s0->drive[s0->drive_next];
+                for (int ph = 0; ph < 3; ++ph) CALL_TRY(sessions_phase(ss.data(), nranks, ph, 0, true, 1, row));
+                for (dlp_session* s : ss) {
+                    s->drive_next += 1;
+                    s->launched += 1;
+                }
+                budget -= 1;
+            }
+            if (s0->drive_next == s0->drive.size() && s0->carry_pending) {
+                for (int ph = 0; ph < 3; ++ph) CALL_TRY(sessions_phase(ss.data(), nranks, ph, 0, true, 2, 0));
+                for (dlp_session* s : ss) {
+                    HIP_TRY(hipSetDevice(s->device));
+                    CALL_TRY(finish_phase1(s));
+                }
+            } else {
+                CALL_TRY(poll_all());
+            }
+            continue;
+        }
+        const int64_t chunk = std::min<int64_t>(budget, s0->opt.check_interval);
+        for (int64_t k = 0; k < chunk; ++k)
+            for (int ph = 0; ph < 3; ++ph)
+                CALL_TRY(sessions_phase(ss.data(), nranks, ph, k, k == chunk - 1, 0, 0));
+        for (dlp_session* s : ss) {
+            s->ev_pending = s->ev_per_pivot ? chunk : 0;
+            s->launched += chunk;
+        }
+        budget -= chunk;
+        CALL_TRY(poll_all());
+    }
+    if (pivots_done) *pivots_done = s0->npivots - start;
+    if (s0->status != DLP_RUNNING) return s0->status;
+    if (s0->launched >= s0->opt.max_pivots) return DLP_PIVOT_LIMIT;
+    return DLP_RUNNING;
+}
+
+int dlp_session_set_exchange_timeout(dlp_session* s, double seconds) {
+    if (!s || !(seconds >= 0.0)) return DLP_ERR_ARG;
+    s->stall_limit_s = seconds;
+    return DLP_OK;
+}
+
+int dlp_session_abort(dlp_session* s) {
+    if (!s) return DLP_ERR_ARG;
+    s->abort_req.store(1);
+    return DLP_OK;
+}
+
+int dlp_session_inject_fault(dlp_session* s, int64_t after_polls) {
+    if (!s || after_polls < 0) return DLP_ERR_ARG;
+    s->fault_after_polls = after_polls;
+    s->npolls = 0;
     return DLP_OK;
 }
 

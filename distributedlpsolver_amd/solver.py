@@ -303,6 +303,19 @@ class Session:
         L.check(L.lib().dlp_session_get_lookahead(self._h, C.byref(on)), "dlp_session_get_lookahead")
         return bool(on.value)
 
+    def set_exchange_timeout(self, seconds: float):
+        """RCCL sessions: abort the exchange after `seconds` without progress (0 = never)."""
+        L.check(L.lib().dlp_session_set_exchange_timeout(self._h, float(seconds)),
+                "dlp_session_set_exchange_timeout")
+
+    def abort(self):
+        """Request an abort of the RCCL exchange (any thread): the run returns DLP_ERR_RCCL."""
+        L.check(L.lib().dlp_session_abort(self._h), "dlp_session_abort")
+
+    def inject_fault(self, after_polls: int = 0):
+        """Tests: the (after_polls + 1)-th window wait fails as if the exchange had died."""
+        L.check(L.lib().dlp_session_inject_fault(self._h, int(after_polls)), "dlp_session_inject_fault")
+
     def set_defer_tuning(self, occupancy: int, form: int = -1):
         """Deferred pass: workgroups/CU cap (0 = none) and form (0 wide, 1/2 narrow x 2/4 rows;
         scalar-coefficient 3 = 1 double x 4 rows, 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows)."""

@@ -325,6 +325,43 @@ int dlp_session_set_fused_pivot(dlp_session* s, int on);
  * while the pass of block b runs on a second tableau buffer.  The step API and pass
  * forms other than 3, 4, 5, 20, 21 and 22 turn it off for the rest of the session. */
 int dlp_session_get_lookahead(dlp_session* s, int* on);
+/* ---- peer exchange -----------------------------------------------
+ * Instead of the RCCL all-gather of the candidates and the int64 MAX all-reduce of the
+ * pivot row, the ranks store their candidate into every rank's exchange block and the
+ * pivot-row owner stores its row into every rank's block (xGMI peer writes between
+ * devices), each message followed by a flag; the waits run inside the select / commit
+ * kernels and are bounded.  Results are bit-identical to every other exchange.
+ *   one process, any devices (incl. several ranks on ONE device):
+ *     dlp_sessions_connect(ranks) once; then dlp_session_run per rank on its own host
+ *     thread (distinct devices), or dlp_sessions_run(ranks) from one thread (required
+ *     when ranks share a device: it enqueues every rank's sends before any rank's waits);
+ *   one process per GPU: dlp_session_exchange_handle (64 B) on every rank, an all-gather
+ *     of the handles by the caller, dlp_session_connect_ipc(handles[nranks]); or, with
+ *     an RCCL id, dlp_session_set_exchange(s, DLP_XCHG_PEER) does that over RCCL.
+ * dlp_session_set_exchange switches between the two on a session that has both (every
+ * rank at the same point, between runs). */
+#define DLP_XCHG_HOST  0   /* caller-driven (dlp_session_step_*) */
+#define DLP_XCHG_RCCL  1
+#define DLP_XCHG_PEER  2
+int dlp_sessions_connect(dlp_session* const* ranks, int nranks);
+int dlp_session_exchange_handle(dlp_session* s, void* out64);
+int dlp_session_connect_ipc(dlp_session* s, const void* handles /* nranks x 64 B, rank order */);
+int dlp_session_set_exchange(dlp_session* s, int mode);
+int dlp_session_get_exchange(dlp_session* s, int* mode);
+int dlp_sessions_run(dlp_session* const* ranks, int nranks, int64_t max_pivots, int64_t* pivots_done);
+
+/* Failure containment on the RCCL exchange.  A session with a
+ * communicator never blocks in a wait that a peer must end: its window waits poll
+ * the stream, ncclCommGetAsyncError and an abort word; on an RCCL error, an abort
+ * request or `seconds` without progress (default 600; 0 = no limit) it calls
+ * ncclCommAbort and dlp_session_run returns DLP_ERR_RCCL (the session is then
+ * unusable; free it).  dlp_solve(n_gpus = N) aborts every rank's communicator
+ * when one rank fails and returns that rank's error.  dlp_session_abort may be
+ * called from any thread.  dlp_session_inject_fault (tests): the (after_polls+1)-th
+ * window wait fails as if the exchange had died. */
+int dlp_session_set_exchange_timeout(dlp_session* s, double seconds);
+int dlp_session_abort(dlp_session* s);
+int dlp_session_inject_fault(dlp_session* s, int64_t after_polls);
 /* Current deferred-pass settings (K = 1: form -1). */
 int dlp_session_get_defer_tuning(dlp_session* s, int* occupancy, int* form, int* K);
 int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,

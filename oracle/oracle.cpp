@@ -422,6 +422,25 @@ int oracle_run_generated(int kind, int64_t m, int64_t n, uint64_t seed, int64_t 
     return 0;
 }
 
+// Checkpointed run (tests/golden/make_digests.py: whole-tableau digests): the
+// generated LP pivoted through ascending stops[]; at each stop cb sees the whole
+// (m+1) x ld tableau (objective row last), the log so far and the basis.
+int oracle_run_generated_stops(int kind, int64_t m, int64_t n, uint64_t seed, int32_t nthreads,
+                               const int64_t* stops, int nstops, oracle_stop_cb cb, void* user) {
+    oracle_opts o{};
+    o.pricing = 0; o.tol_dj = 1e-9; o.tol_piv = 1e-9; o.nthreads = nthreads;
+    o.max_pivots = nstops > 0 ? stops[nstops - 1] : 0;
+    Tab t;
+    tab_init(t, m, n, 0, m, &o);
+    if (oracle_gen_tableau(kind, m, n, seed, 0, m, t.ld, t.T.data(), nthreads) != 0) return -1;
+    for (int s = 0; s < nstops; ++s) {
+        while ((int64_t)t.log.size() < stops[s])
+            if (pivot_once(t) != 4) return -6;   // the LP ended before the stop
+        cb((int64_t)t.log.size(), t.T.data(), t.ld, m + 1, t.log.data(), t.basis.data(), user);
+    }
+    return 0;
+}
+
 int oracle_bench_pivots(int kind, int64_t m, int64_t n, uint64_t seed, int64_t warmup, int64_t k,
                         int32_t nthreads, double* seconds, int64_t* done, double* gen_seconds) {
     using clk = std::chrono::steady_clock;

@@ -101,6 +101,13 @@ int oracle_run_generated(int kind, int64_t m, int64_t n, uint64_t seed, int64_t 
                          oracle_pivot* log, int64_t* npivots, const int64_t* rows_idx,
                          int64_t nrows, double* rows_out, int32_t* basis_out);
 
+/* Pivot the generated LP through the ascending stops[0..nstops); at each stop
+ * call cb(npivots, T, ld, rows = m+1 (objective row last), log, basis, user). */
+typedef void (*oracle_stop_cb)(int64_t npivots, const double* T, int64_t ld, int64_t rows,
+                               const oracle_pivot* log, const int32_t* basis, void* user);
+int oracle_run_generated_stops(int kind, int64_t m, int64_t n, uint64_t seed, int32_t nthreads,
+                               const int64_t* stops, int nstops, oracle_stop_cb cb, void* user);
+
 /* fp64 restatement of the reference's MW loop, sort mode (oracle_mw.cpp): T
  * iterations on the generated ad-allocation instance.  Per-iteration outputs
  * (length T): dual value, max average infeasibility (+ advertiser), min / max

@@ -31,3 +31,22 @@ def load_golden(name):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+def tableau_sha256(sessions, width, chunk=512):
+    """sha256 of a row-block tableau in global row order: every rank's constraint
+    rows (first `width` doubles each), then the objective row (replicated: every
+    rank's must be identical) — the stream tests/golden/make_digests.py hashes
+    for the oracle's tableau (c3_tableau)."""
+    import hashlib
+
+    import numpy as np
+    h = hashlib.sha256()
+    for s in sorted(sessions, key=lambda s: s.row_first):
+        for first in range(0, s.rows, chunk):
+            cnt = min(chunk, s.rows - first)
+            h.update(np.ascontiguousarray(s.read_rows(first, cnt)[:, :width]).tobytes())
+    objs = [np.ascontiguousarray(s.read_rows(s.rows, 1)[0, :width]).tobytes() for s in sessions]
+    assert all(o == objs[0] for o in objs), "replicated objective rows differ between ranks"
+    h.update(objs[0])
+    return h.hexdigest()

@@ -13,6 +13,11 @@ for the GPU to reproduce.  Run in the build container (CPU only):
       sampled constraint rows after those pivots.
   c3_k64  the same LP through the current default (K = 64 blocks: 5 + 20 blocks
       of 64 pivots, then the 20-pivot window = 1620 pivots).
+  c3_tableau  whole-tableau digests of the same LP: after 136
+      pivots (test_c3_full_blocks_bit_exact), 160 (the 8-rank row partition,
+      tests/test_gpu_c3_rowblock.py) and 1620 (the bench window): sha256 of all
+      32,769 rows (objective row last), each its first `width` doubles, streamed
+      in row order; plus the log prefix and basis digests at each stop.
 
 The digests hash little-endian fp64 / int32 bytes of the oracle's outputs
 (tests/oracle_py.py), so the GPU side compares bit for bit."""
@@ -64,6 +69,29 @@ def c3(pivots=C3_PIVOTS):
             "oracle_seconds": time.time() - t0}
 
 
+def tableau_sha(T, w, chunk=512):
+    h = hashlib.sha256()
+    for r in range(0, T.shape[0], chunk):
+        h.update(np.ascontiguousarray(T[r:r + chunk, :w]).tobytes())
+    return h.hexdigest()
+
+
+def c3_tableau(stops=(136, 160, C3_K64_PIVOTS)):
+    m = n = 32768
+    t0 = time.time()
+    w = ((n + m + 1) + 15) // 16 * 16
+    out = {"m": m, "n": n, "seed": 3, "width": w, "rows": m + 1, "stops": {}}
+
+    def at(k, T, log, basis):
+        out["stops"][str(k)] = {"log_sha256": sha(log), "tableau_sha256": tableau_sha(T, w),
+                                "basis_sha256": sha(basis), "objective_hex": float(log[-1]["objective"]).hex(),
+                                "oracle_seconds": time.time() - t0}
+        print(k, out["stops"][str(k)], flush=True)
+
+    O.run_generated_stops(m, n, 3, list(stops), at, nthreads=os.cpu_count() or 8)
+    return out
+
+
 def main():
     which = sys.argv[1:] or ["c2", "c3"]
     d = {}
@@ -71,7 +99,7 @@ def main():
         with open(OUT) as f:
             d = json.load(f)
     for w in which:
-        d[w] = {"c2": c2, "c3": c3, "c3_k64": lambda: c3(C3_K64_PIVOTS)}[w]()
+        d[w] = {"c2": c2, "c3": c3, "c3_k64": lambda: c3(C3_K64_PIVOTS), "c3_tableau": c3_tableau}[w]()
         with open(OUT, "w") as f:
             json.dump(d, f, indent=1)
         print(w, json.dumps(d[w]), flush=True)

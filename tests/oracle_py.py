@@ -299,6 +299,40 @@ def run_generated(m, n, seed, k, rows, degenerate=False, nthreads=8):
     return log[:npiv.value], out, basis
 
 
+STOP_CB = C.CFUNCTYPE(None, C.c_int64, C.POINTER(C.c_double), C.c_int64, C.c_int64, C.c_void_p,
+                      C.POINTER(C.c_int32), C.c_void_p)
+
+
+def run_generated_stops(m, n, seed, stops, fn, degenerate=False, nthreads=8):
+    """Pivot the generated LP through the ascending `stops`; at each one call
+    fn(npivots, T, log, basis) with zero-copy views of the oracle's whole
+    tableau ((m+1) x ld, objective row last), its pivot log and basis."""
+    L = lib()
+    if not getattr(L, "_stops_bound", False):
+        L.oracle_run_generated_stops.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_uint64, C.c_int32,
+                                                 _I64, C.c_int, STOP_CB, C.c_void_p]
+        L._stops_bound = True
+    errs = []
+
+    def _cb(k, T, ld_, rows, logp, basisp, _user):
+        try:
+            Tv = np.ctypeslib.as_array(T, shape=(rows, ld_))
+            lg = np.frombuffer((C.c_char * (32 * k)).from_address(logp), dtype=PIVOT_DTYPE) if k else \
+                np.zeros(0, PIVOT_DTYPE)
+            bs = np.ctypeslib.as_array(basisp, shape=(m,))
+            fn(int(k), Tv, lg, bs)
+        except Exception as e:  # noqa: BLE001 - re-raised after the C call returns
+            errs.append(e)
+
+    cb = STOP_CB(_cb)
+    st = np.ascontiguousarray(stops, dtype=np.int64)
+    rc = L.oracle_run_generated_stops(1 if degenerate else 0, m, n, seed, nthreads,
+                                      st.ctypes.data_as(_I64), len(st), cb, None)
+    if errs:
+        raise errs[0]
+    assert rc == 0, f"oracle_run_generated_stops rc={rc}"
+
+
 # ---- general LPs (include/dlp.h "general LPs", oracle/oracle_general.inc)
 INF = float("inf")
 

@@ -181,7 +181,7 @@ def test_defer_update_stats():
 
 
 @pytest.mark.parametrize("P,K,form", [(1, 8, -1), (2, 4, -1), (2, 16, -1), (3, 32, -1), (2, 64, 21), (3, 64, 21),
-                                      (2, 64, 22)])
+                                      (2, 64, 22), (4, 16, -1), (4, 64, 21), (8, 16, -1), (8, 64, 21)])
 def test_defer_step_api_multi_rank_one_gpu(P, K, form):
     """The deferred exchange path (ratio -> candidate all-gather -> select ->
     pivot-row MAX all-reduce -> commit, pass every K pivots) with P row-block
@@ -283,3 +283,41 @@ def test_pass_form21_sparse_and_degenerate(K, form):
         s.run(10 ** 6)
         res = s.result()
     _check(res, ref)
+
+
+def _chunk_digests(sess, rows, chunk=1024):
+    import hashlib
+    out = []
+    for first in range(0, rows + 1, chunk):
+        cnt = min(chunk, rows + 1 - first)
+        out.append(hashlib.sha256(np.ascontiguousarray(sess.read_rows(first, cnt)).tobytes()).hexdigest())
+    return out
+
+
+@pytest.mark.parametrize("form", [1, 2])
+def test_lds_forms_on_streaming_k64_geometry(form):
+    """on a streaming K = 64 session the auto band is 768 rows for the
+    register-resident forms; the LDS-staged forms 1 / 2 (K * rb * 8 + rb * 4 bytes of LDS)
+    must get a band that fits 160 KiB when the form is switched, and stay bit-identical:
+    2 full blocks + a 9-pivot tail, whole tableau (chunk digests) equal to the eager session's."""
+    m = n = 16384   # 16385 x 32784 doubles = 4.3 GB: streaming, >= 16k rows
+    k = 2 * 64 + 9
+    prob = dlp.Problem.random(m, n, 21)
+    with dlp.Session(prob, defer=64, check_interval=64) as s:
+        assert s.get_tuning()[1] == 768 and s.defer_form() == 21
+        s.set_defer_tuning(0, form)
+        rb = s.get_tuning()[1]
+        assert 64 * rb * 8 + rb * 4 + 64 * 4 <= 160 * 1024 and rb >= 256
+        done = 0
+        while done < k:
+            done += s.run(min(64, k - done))[1]
+        ld = s.result().pivot_log
+        dd = _chunk_digests(s, m)
+        s.set_defer_tuning(0, 21)   # back to the DPP form: the auto band follows
+        assert s.get_tuning()[1] == 768
+    with dlp.Session(prob, defer=1, check_interval=k) as e:
+        e.run(k)
+        le = e.result().pivot_log
+        de = _chunk_digests(e, m)
+    _same_log(ld, le)
+    assert dd == de

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle_py as O
-from conftest import load_golden
+from conftest import load_golden, tableau_sha256
 
 import distributedlpsolver_amd as dlp
 from distributedlpsolver_amd import _lib as L
@@ -75,7 +75,7 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0):
+def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0, tableau_digest=None):
     """k pivots in windows of ci (whole K-blocks, then a tail) through the auto
     geometry of the bench (deferred K, pass form, band rows, ld alignment);
     the whole pivot log, every pivot row, random rows and the objective row
@@ -101,6 +101,9 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0):
                                            rng.integers(0, m, 24), [0, m - 1]]))
         rows = np.stack([s.read_rows(int(i), 1)[0] for i in sample])
         obj_row = s.read_rows(m, 1)[0]
+        # the whole tableau (all m + 1 rows) against the oracle's committed digest
+        if tableau_digest is not None:
+            assert tableau_sha256([s], tableau_digest["width"]) == tableau_digest["tableau_sha256"]
     log, ref_rows, ref_basis = O.run_generated(m, n, seed, k, np.concatenate([sample, [m]]),
                                                nthreads=16)
     assert len(res.pivot_log) == k == len(log)
@@ -118,7 +121,9 @@ def test_c3_full_blocks_bit_exact():
     """C3 at the bench geometry: 2 full K = 64 blocks through the form-21 pass
     (DPP coefficients, 768-row bands, ld 66048, nt), then an 8-pivot tail (a
     partial block: coefficients of the unused steps zeroed in memory)."""
-    _full_blocks_vs_oracle(32768, 32768, 3, 136, 128, 64)
+    tab = load_golden("digests.json")["c3_tableau"]
+    _full_blocks_vs_oracle(32768, 32768, 3, 136, 128, 64,
+                           tableau_digest=dict(tab["stops"]["136"], width=tab["width"]))
 
 
 def test_c3_k32_lookahead_full_blocks_bit_exact():
@@ -149,6 +154,9 @@ def test_c3_bench_window_digest(K):
         res = s.result()
         rows = {str(i): s.read_rows(i, 1)[0, :g["width"]] for i in g["rows"]}
         obj_row = s.read_rows(m, 1)[0, :g["width"]]
+        if K == 64:   # the whole tableau after the bench window (all 32,769 rows)
+            tab = load_golden("digests.json")["c3_tableau"]
+            assert tableau_sha256([s], tab["width"]) == tab["stops"][str(g["pivots"])]["tableau_sha256"]
     assert len(res.pivot_log) == g["pivots"]
     for k, h in g["log_prefix_sha256"].items():
         assert _sha(res.pivot_log[:int(k)]) == h, f"log prefix {k}"

@@ -151,7 +151,7 @@ def test_empty_and_ragged_shapes():
     _check_equal(res, ref)
 
 
-@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
 def test_multi_rank_sessions_one_gpu(P):
     """P row-block sessions on one GPU, exchanged by the host (all-gather of
     the 32-B candidates, int64 MAX all-reduce of the pivot row): same log."""

@@ -38,7 +38,8 @@ def _worker(rank, world, port, m, n, seed, degenerate, q):
 
 
 @pytest.mark.parametrize("world,m,n,seed,degenerate", [(2, 40, 60, 1, False), (3, 50, 50, 5, True),
-                                                        (2, 64, 64, 5, True)])
+                                                        (2, 64, 64, 5, True), (4, 70, 90, 6, False),
+                                                        (4, 48, 64, 7, True)])
 def test_rowblock_gloo_matches_single_rank(world, m, n, seed, degenerate):
     A, b, c = O.gen_dense(m, n, seed, degenerate)
     ref = O.solve_dense(A, b, c)
