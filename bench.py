@@ -68,6 +68,11 @@ def parse():
     ap.add_argument("--eager-pivots", type=int, default=3)
     ap.add_argument("--no-pivot-window", action="store_true",
                     help="skip the extra --step-unit pivot window reported beside the main figure")
+    ap.add_argument("--exchange", default="rccl", choices=("rccl", "peer"),
+                    help="N > 1: the main window's row-block exchange (RCCL collectives, or owner-rooted "
+                         "peer stores into the ranks' exchange blocks)")
+    ap.add_argument("--alt-pivots", type=int, default=256,
+                    help="N > 1: pivots of the second window, run with the other exchange (0 = none)")
     ap.add_argument("--rows-per-block", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=-1, help="-1 = auto")
     ap.add_argument("--variant", type=int, default=-1, help="update-kernel variant, -1 = auto")
@@ -198,19 +203,58 @@ def log_parity(workload, log):
     path = os.path.join(ROOT, "tests", "golden", "digests.json")
     try:
         with open(path) as f:
-            g = json.load(f).get("c3_k64" if workload == "c3" else workload)
+            d = json.load(f)
     except (OSError, ValueError):
         return None
+    g = d.get("c3_k64" if workload == "c3" else workload)
     if not g or "log_prefix_sha256" not in g:
         return None
+    prefixes = dict(g["log_prefix_sha256"])
+    if workload == "c3":   # the whole-tableau stops carry log digests too (1876: the N > 1 second window)
+        for k, st in d.get("c3_tableau", {}).get("stops", {}).items():
+            prefixes.setdefault(k, st["log_sha256"])
     got = {}
-    for k, h in g["log_prefix_sha256"].items():
+    for k, h in prefixes.items():
         if int(k) <= len(log):
             got[k] = hashlib.sha256(log[:int(k)].tobytes()).hexdigest() == h
     if g.get("pivots") == len(log):
         got[str(len(log))] = hashlib.sha256(log.tobytes()).hexdigest() == g["log_sha256"]
     return {"source": "tests/golden/digests.json (oracle, same LP)", "prefixes_checked": sorted(got, key=int),
             "bit_identical": all(got.values()) if got else None}
+
+
+def alt_exchange_window(sess, dist, barrier_sync, args, L, torch):
+    """Switch every rank to the other exchange and time args.alt_pivots pivots.  The switch
+    to PEER all-gathers the exchange blocks' IPC handles over the session's communicator;
+    every rank's outcome is agreed (MIN all-reduce) before anything is timed, and the window
+    runs with a 60 s stall limit, so a broken path ends as an error field, never a hang."""
+    mode, name = (L.XCHG_PEER, "peer") if args.exchange == "rccl" else (L.XCHG_RCCL, "rccl")
+    out = {"exchange": name, "pivots": args.alt_pivots}
+    ok = 1
+    try:
+        sess.set_exchange(mode)
+        sess.set_exchange_timeout(60.0)
+    except L.DLPError as e:
+        ok, out["error"] = 0, str(e)
+    t = torch.tensor([ok], dtype=torch.int32, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if int(t.item()) == 0:
+        out.setdefault("error", "another rank failed to switch")
+        return out
+    barrier_sync()
+    t0 = time.perf_counter()
+    try:
+        st, done = sess.run(args.alt_pivots)
+    except L.DLPError as e:
+        out["error"] = str(e)
+        return out
+    barrier_sync()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    out.update({"done": done, "seconds": float(el.item())})
+    if done == args.alt_pivots:
+        out["pivots_per_s"] = done / out["seconds"]
+    return out
 
 
 def main():
@@ -223,6 +267,7 @@ def main():
 
     import torch
     import distributedlpsolver_amd as dlp
+    from distributedlpsolver_amd import _lib as L
 
     m, n, seed, desc = WORKLOADS[args.workload]
     if world > 1:
@@ -249,8 +294,9 @@ def main():
                        check_interval=64 * max(args.steps, args.warmup, 1), timing=args.timing,
                        nontemporal=args.nontemporal, update_variant=args.variant,
                        ld_align=args.ld_align, rows_per_block=args.rows_per_block,
-                       max_pivots=64 * (args.warmup + args.steps) + args.steps + 2, log_pivots=1,
-                       defer=args.defer, lookahead=args.lookahead)
+                       max_pivots=64 * (args.warmup + args.steps) + args.steps + args.alt_pivots + 2,
+                       log_pivots=1, defer=args.defer, lookahead=args.lookahead,
+                       exchange=(L.XCHG_PEER if args.exchange == "peer" else L.XCHG_RCCL) if world > 1 else 0)
     if args.occupancy >= 0 or args.form >= 0:
         if sess.update_stats()[2] > 1:
             sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 0, args.form)
@@ -310,6 +356,15 @@ def main():
     res = sess.result()
     obj_after = res.objective
     parity = log_parity(args.workload, res.pivot_log) if rank == 0 else None
+
+    # N > 1: the same LP continues for args.alt_pivots pivots through the OTHER exchange
+    # (RCCL collectives <-> owner-rooted peer stores), timed the same way, so that one
+    # scaling run measures both; a failure to switch or to run is reported, not fatal
+    alt = None
+    if dist is not None and args.alt_pivots > 0:
+        alt = alt_exchange_window(sess, dist, barrier_sync, args, L, torch)
+        if alt.get("pivots_per_s") and rank == 0:
+            alt["pivot_log_vs_oracle"] = log_parity(args.workload, sess.result().pivot_log)
     sess.close()
 
     # the north star's own figure: the EAGER rank-1 update (defer = 1) on the same tableau,
@@ -382,6 +437,8 @@ def main():
                                     if args.timing >= 2 else None),
             "update_launches": launches,
             "pivot_step_window": pw,
+            "exchange": args.exchange if world > 1 else None,
+            "alt_exchange_window": alt,
             "objective_after_run": obj_after,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None,

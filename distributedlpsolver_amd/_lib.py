@@ -20,6 +20,7 @@ GEN_DENSE, GEN_DEGENERATE = 0, 1
 MINIMIZE, MAXIMIZE = 1, -1
 BUF_CAND_SEND, BUF_CAND_RECV, BUF_PROW_SEND, BUF_PROW_RECV = 0, 1, 2, 3
 PHASE_RATIO, PHASE_EXCHANGE, PHASE_PROW, PHASE_UPDATE = 0, 1, 2, 3
+XCHG_HOST, XCHG_RCCL, XCHG_PEER = 0, 1, 2
 NUM_PHASES = 4
 
 
@@ -53,7 +54,7 @@ class Options(C.Structure):
         ("defer", C.c_int32),
         ("n_gpus", C.c_int32),
         ("lookahead", C.c_int32),
-        ("pad_", C.c_int32),
+        ("exchange", C.c_int32),
     ]
 
 
@@ -149,6 +150,12 @@ SIGNATURES = [
     ("dlp_session_set_exchange_timeout", C.c_int, [_P, C.c_double]),
     ("dlp_session_abort", C.c_int, [_P]),
     ("dlp_session_inject_fault", C.c_int, [_P, _I64]),
+    ("dlp_sessions_connect", C.c_int, [C.POINTER(_P), C.c_int]),
+    ("dlp_session_exchange_handle", C.c_int, [_P, C.c_void_p]),
+    ("dlp_session_connect_ipc", C.c_int, [_P, C.c_void_p]),
+    ("dlp_session_set_exchange", C.c_int, [_P, C.c_int]),
+    ("dlp_session_get_exchange", C.c_int, [_P, C.POINTER(C.c_int)]),
+    ("dlp_sessions_run", C.c_int, [C.POINTER(_P), C.c_int, _I64, C.POINTER(_I64)]),
     ("dlp_session_get_defer_tuning", C.c_int,
      [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dlp_session_set_tuning", C.c_int, [_P, C.c_int, C.c_int, C.c_int]),

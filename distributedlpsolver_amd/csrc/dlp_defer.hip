@@ -453,9 +453,12 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
         pr.y = t.y / piv;
     }
     if (!fused && xp) {   // peer exchange: the owner's row into every rank's row region
+        // (scalars first: hipcc of ROCm 7.2 compiles __builtin_bit_cast(T, v.y) of an
+        // ext_vector element as a cast of element 0; tests/test_isa.py guards this site)
+        const double px = pr.x, py = pr.y;
         if (pl >= 0)      // (uniform per launch)
-            x_push_row_chunk(xp, xseq, j, ld, __builtin_bit_cast(uint64_t, pr.x),
-                             __builtin_bit_cast(uint64_t, pr.y));
+            x_push_row_chunk(xp, xseq, j, ld, __builtin_bit_cast(uint64_t, px),
+                             __builtin_bit_cast(uint64_t, py));
         return;
     }
     if (!fused) {

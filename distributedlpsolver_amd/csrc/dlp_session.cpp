@@ -306,6 +306,10 @@ int validate_options(const dlp_options* o) {
         set_error("invalid tolerance / pivot limit / check interval");
         return DLP_ERR_ARG;
     }
+    if (o->exchange != 0 && o->exchange != DLP_XCHG_RCCL && o->exchange != DLP_XCHG_PEER) {
+        set_error("exchange must be 0, DLP_XCHG_RCCL or DLP_XCHG_PEER");
+        return DLP_ERR_ARG;
+    }
     return DLP_OK;
 }
 
@@ -548,9 +552,11 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     // lookahead: deferred, a pass form with an out-of-place instance, the exchange (if
     // any) driven by the session, no per-phase timing, and room for a second tableau
     {
+        // (a multi-rank session without an id: only when asked for, as it runs only once its
+        // ranks are connected by the peer exchange; the step API turns it off)
         const bool host_driven = nranks > 1 && !rccl;
         bool ok = s->d.K > 1 && 2 * s->d.K <= dlp::kMaxReplay && dlp::lookahead_form(s->d.form) &&
-                  !s->general && !s->cluster && !host_driven && opt->timing < 2;
+                  !s->general && !s->cluster && (!host_driven || opt->lookahead == 1) && opt->timing < 2;
         size_t freeb = 0, totalb = 0;
         if (ok && hipMemGetInfo(&freeb, &totalb) == hipSuccess)
             ok = freeb > tbytes + tbytes / 8 + ((size_t)1 << 30);
@@ -945,6 +951,10 @@ int enqueue_carry_in(dlp_session* s) {
 int carry_phase(dlp_session* s, int phase) {
     const dlp::XPeers* xp = xp_of(s);
     if (phase == 0) {
+        // the last drive-out pivot may have left the skip status (a redundant row): the
+        // carry runs whatever it is (carry_in sets "running" again), and the peer kernels
+        // below act only while running
+        HIP_TRY(dlp::launch_set_status(s->st, DLP_RUNNING, s->stream));
         if (xp) {
             HIP_TRY(hipMemsetAsync(s->cand_send, 0, sizeof(dlp::Cand), s->stream));
             HIP_TRY(dlp::launch_xcand_send(xp, ++s->xseq_c, s->cand_send, s->st, s->stream));
@@ -1339,6 +1349,9 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
         ss[r] = s;
         return DLP_OK;
     });
+    // owner-rooted peer exchange: every rank's block addressed directly (peer access between
+    // the devices, no IPC inside one process); the communicators stay for set-up only
+    if (res == DLP_OK && o.exchange == DLP_XCHG_PEER) res = dlp_sessions_connect(ss.data(), P);
     if (res == DLP_OK) {
         res = on_ranks([&](int r) {
             if (const char* e = std::getenv("DLP_TEST_FAIL_RANK"))   // tests: fail this rank's 2nd poll
@@ -1769,6 +1782,8 @@ int dlp_session_create_rank(const dlp_problem* prob, const dlp_options* opt, int
         set_error(std::string("session_init: ") + e.what());
         rc = DLP_ERR_OOM;
     }
+    if (rc == DLP_OK && uid && opt->exchange == DLP_XCHG_PEER)
+        rc = dlp_session_set_exchange(s, DLP_XCHG_PEER);   // collective over the new communicator
     if (rc != DLP_OK) {
         free_session(s);
         return rc;

@@ -316,6 +316,48 @@ class Session:
         """Tests: the (after_polls + 1)-th window wait fails as if the exchange had died."""
         L.check(L.lib().dlp_session_inject_fault(self._h, int(after_polls)), "dlp_session_inject_fault")
 
+    # owner-rooted peer exchange (include/dlp.h "peer exchange", DESIGN.md §5)
+    @staticmethod
+    def connect_peers(sessions) -> None:
+        """Connect the rank sessions of one solve that live in this process
+        (dlp_sessions_connect): candidates and the pivot row then travel by direct
+        stores into each rank's exchange block.  Ranks that share a device must be
+        run together with Session.run_ranks."""
+        arr = (C.c_void_p * len(sessions))(*[s._h for s in sessions])
+        L.check(L.lib().dlp_sessions_connect(arr, len(sessions)), "dlp_sessions_connect")
+
+    @staticmethod
+    def run_ranks(sessions, max_pivots: int) -> tuple[int, int]:
+        """dlp_sessions_run: every connected rank from this thread, phase-interleaved."""
+        arr = (C.c_void_p * len(sessions))(*[s._h for s in sessions])
+        done = C.c_int64()
+        st = L.lib().dlp_sessions_run(arr, len(sessions), max_pivots, C.byref(done))
+        L.check(st, "dlp_sessions_run", ok=(L.OK, L.INFEASIBLE, L.UNBOUNDED, L.PIVOT_LIMIT, L.RUNNING))
+        return st, done.value
+
+    def exchange_handle(self) -> bytes:
+        """64-B IPC handle of this rank's exchange block (one process per GPU)."""
+        buf = C.create_string_buffer(64)
+        L.check(L.lib().dlp_session_exchange_handle(self._h, buf), "dlp_session_exchange_handle")
+        return buf.raw
+
+    def connect_ipc(self, handles) -> None:
+        """Every rank's exchange_handle(), in rank order (gathered by the caller)."""
+        raw = b"".join(handles)
+        if len(raw) != 64 * self.nranks:
+            raise ValueError("connect_ipc needs nranks 64-byte handles")
+        buf = C.create_string_buffer(raw, len(raw))
+        L.check(L.lib().dlp_session_connect_ipc(self._h, buf), "dlp_session_connect_ipc")
+
+    def set_exchange(self, mode: int) -> None:
+        """L.XCHG_RCCL or L.XCHG_PEER (PEER over a communicator: an all-gather of IPC handles)."""
+        L.check(L.lib().dlp_session_set_exchange(self._h, int(mode)), "dlp_session_set_exchange")
+
+    def get_exchange(self) -> int:
+        m = C.c_int()
+        L.check(L.lib().dlp_session_get_exchange(self._h, C.byref(m)), "dlp_session_get_exchange")
+        return m.value
+
     def set_defer_tuning(self, occupancy: int, form: int = -1):
         """Deferred pass: workgroups/CU cap (0 = none) and form (0 wide, 1/2 narrow x 2/4 rows;
         scalar-coefficient 3 = 1 double x 4 rows, 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows)."""

@@ -157,7 +157,11 @@ typedef struct dlp_options {
                                 bit; 2x the tableau memory): 1 = on where supported, 0 = off,
                                 -1 = auto (default: tableaus of >= 4 GiB that fit twice; at
                                 K = 64 the selections replay up to 127 steps) */
-    int32_t pad_;
+    int32_t exchange;        /* row-block exchange of dlp_solve(n_gpus = N) and of rank sessions
+                                created with an RCCL id: 0 (default) or DLP_XCHG_RCCL = RCCL
+                                candidate all-gather + pivot-row MAX all-reduce; DLP_XCHG_PEER =
+                                owner-rooted peer stores (dlp_sessions_connect in process; the
+                                IPC handles all-gathered over the communicator per process) */
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
  * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;

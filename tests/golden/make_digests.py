@@ -15,7 +15,8 @@ for the GPU to reproduce.  Run in the build container (CPU only):
       of 64 pivots, then the 20-pivot window = 1620 pivots).
   c3_tableau  whole-tableau digests of the same LP: after 136
       pivots (test_c3_full_blocks_bit_exact), 160 (the 8-rank row partition,
-      tests/test_gpu_c3_rowblock.py) and 1620 (the bench window): sha256 of all
+      tests/test_gpu_c3_rowblock.py), 1620 (the bench window) and 1876 (+ the
+      bench's 256-pivot second-exchange window at N > 1): sha256 of all
       32,769 rows (objective row last), each its first `width` doubles, streamed
       in row order; plus the log prefix and basis digests at each stop.
 
@@ -76,7 +77,7 @@ def tableau_sha(T, w, chunk=512):
     return h.hexdigest()
 
 
-def c3_tableau(stops=(136, 160, C3_K64_PIVOTS)):
+def c3_tableau(stops=(136, 160, C3_K64_PIVOTS, C3_K64_PIVOTS + 256)):
     m = n = 32768
     t0 = time.time()
     w = ((n + m + 1) + 15) // 16 * 16

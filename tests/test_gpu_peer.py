@@ -1,0 +1,271 @@
+"""GPU: the owner-rooted peer exchange (include/dlp.h "peer exchange", DESIGN.md §5;
+VERDICT r02 #4).  Instead of an RCCL all-gather of the 32-B candidates and an
+int64 MAX all-reduce of the 528 KB pivot row, every rank stores its candidate into
+every rank's exchange block and the pivot-row owner stores its row into every
+rank's block, each message followed by a flag the select / commit kernels wait
+for (bounded).  This replaces the reference's distribution layer
+(R/global_problem.cpp:270-274) on the row-block partition of SURVEY.md §8(e).
+
+On one GPU the ranks are sessions of one process on the same device (same-device
+pointers, dlp_sessions_connect + dlp_sessions_run) or two processes on the same
+device (IPC handles of the exchange blocks, dlp_session_connect_ipc).  Every case
+is compared with the oracle bit for bit (pivot log, objective, x, y) — the
+exchange moves bits and never changes a decision."""
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import load_golden, tableau_sha256
+from general_lp import fixture_lp, lp_arrays
+
+import distributedlpsolver_amd as dlp
+from distributedlpsolver_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_log(got, ref):
+    assert len(got) == len(ref), (len(got), len(ref))
+    g, r = np.ascontiguousarray(got), np.ascontiguousarray(ref)
+    if g.tobytes() != r.tobytes():
+        for k in range(len(r)):
+            if g[k].tobytes() != r[k].tobytes():
+                raise AssertionError(f"pivot {k}: gpu {g[k]} oracle {r[k]}")
+
+
+def _check(res, ref):
+    assert res.status == ref.status
+    _same_log(res.pivot_log, ref.pivot_log)
+    assert np.float64(res.objective).tobytes() == np.float64(ref.objective).tobytes()
+    assert res.x.tobytes() == ref.x.tobytes()
+    assert res.y.tobytes() == ref.y.tobytes()
+    np.testing.assert_array_equal(res.basis, ref.basis)
+
+
+def _peer_ranks(prob, P, **opts):
+    sess = [dlp.Session(prob, rank=r, nranks=P, **opts) for r in range(P)]
+    dlp.Session.connect_peers(sess)
+    assert all(s.get_exchange() == L.XCHG_PEER for s in sess)
+    return sess
+
+
+@pytest.mark.parametrize("P,K,form", [(2, 1, -1), (3, 1, -1), (8, 1, -1), (2, 16, -1), (3, 32, -1),
+                                      (4, 16, -1), (8, 16, -1), (2, 64, 21), (4, 64, 21), (8, 64, 21)])
+def test_peer_exchange_dense(P, K, form):
+    m, n, seed = 150, 170, 4
+    A, b, c = O.gen_dense(m, n, seed)
+    ref = O.solve_dense(A, b, c)
+    sess = _peer_ranks(dlp.Problem.random(m, n, seed), P, defer=K, check_interval=37)
+    try:
+        if form >= 0:
+            for s in sess:
+                s.set_defer_tuning(0, form)
+        st, done = dlp.Session.run_ranks(sess, 10 ** 6)
+        assert st == L.OK and done == ref.num_pivots
+        _check(dlp.Session.merged_result(sess), ref)
+        for s in sess:   # every rank's replicated log and objective row
+            r = s.result()
+            _same_log(r.pivot_log, ref.pivot_log)
+            assert r.y.tobytes() == ref.y.tobytes()
+    finally:
+        for s in sess:
+            s.close()
+
+
+@pytest.mark.parametrize("P,K", [(3, 1), (2, 16)])
+def test_peer_exchange_degenerate_bland(P, K):
+    """Degenerate LP (Bland after degenerate pivots, exact ties on the ratio)."""
+    A, b, c = O.gen_dense(96, 128, 6, True)
+    ref = O.solve_dense(A, b, c)
+    sess = _peer_ranks(dlp.Problem.random(96, 128, 6, True), P, defer=K)
+    try:
+        st, _ = dlp.Session.run_ranks(sess, 10 ** 6)
+        assert st == ref.status
+        _check(dlp.Session.merged_result(sess), ref)
+    finally:
+        for s in sess:
+            s.close()
+
+
+def test_peer_exchange_lookahead_and_windows():
+    """Lookahead forced on (selection of block b+1 beside pass b) and windows that end
+    inside blocks, resumed: the peer sequence numbers continue across runs."""
+    A, b, c = O.gen_dense(150, 170, 4)
+    ref = O.solve_dense(A, b, c)
+    sess = _peer_ranks(dlp.Problem.random(150, 170, 4), 2, defer=16, lookahead=1, check_interval=7)
+    try:
+        assert all(s.lookahead() for s in sess)
+        total = 0
+        while True:
+            st, done = dlp.Session.run_ranks(sess, 23)
+            total += done
+            if st != L.PIVOT_LIMIT and st != L.RUNNING:
+                break
+        assert st == L.OK and total == ref.num_pivots
+        _check(dlp.Session.merged_result(sess), ref)
+    finally:
+        for s in sess:
+            s.close()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("name", ["lpgen_2d_20x20_eq", "enzo_c_infeasible", "basic_artificial_vars"])
+def test_peer_exchange_general(P, name):
+    """General LPs: forced drive-out pivots and the carried Phase II objective row
+    travel through the same exchange blocks."""
+    cs = next(c for c in load_golden("general.json") if c["name"] == name)
+    lp = fixture_lp(cs)
+    ref = O.solve_general(lp)
+    sess = _peer_ranks(dlp.Problem.general(*lp_arrays(lp)), P)
+    try:
+        st, _ = dlp.Session.run_ranks(sess, 10 ** 6)
+        assert st == ref.status
+        res = dlp.Session.merged_result(sess)
+        _same_log(res.pivot_log, ref.pivot_log)
+        assert res.phase1_pivots == ref.phase1_pivots
+        assert np.float64(res.objective).tobytes() == np.float64(ref.objective).tobytes()
+        assert res.x.tobytes() == ref.x.tobytes() and res.y.tobytes() == ref.y.tobytes()
+    finally:
+        for s in sess:
+            s.close()
+
+
+@pytest.mark.parametrize("defer", [1, 16])
+def test_solve_n_gpus_peer_exchange(defer):
+    """dlp_solve(n_gpus = 1, exchange = PEER): the in-process multi-device path
+    with the peer exchange instead of the RCCL collectives."""
+    A, b, c = O.gen_dense(200, 400, 1)
+    ref = O.solve_dense(A, b, c)
+    res = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, defer=defer, exchange=L.XCHG_PEER, small_lp=-1)
+    _check(res, ref)
+
+
+@pytest.mark.parametrize("defer", [1, 16])
+def test_rccl_session_switches_exchange(defer):
+    """A 1-rank RCCL session: set_exchange(PEER) all-gathers the IPC handles over its
+    communicator; switching back and forth between windows keeps the result exact."""
+    A, b, c = O.gen_dense(200, 400, 1)
+    ref = O.solve_dense(A, b, c)
+    with dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
+                     defer=defer, check_interval=16, exchange=L.XCHG_PEER) as s:
+        assert s.get_exchange() == L.XCHG_PEER
+        s.run(50)
+        s.set_exchange(L.XCHG_RCCL)
+        s.run(50)
+        s.set_exchange(L.XCHG_PEER)
+        st, _ = s.run(10 ** 6)
+        assert st == L.OK
+        _check(s.result(), ref)
+
+
+def test_peer_wait_is_bounded():
+    """A rank that never runs: the other rank's select kernel waits for its
+    candidate; the host stall limit raises the abort word, the device wait ends and
+    the run returns an error instead of hanging."""
+    prob = dlp.Problem.random(120, 150, 4)
+    sess = _peer_ranks(prob, 2, defer=1)
+    try:
+        sess[0].set_exchange_timeout(2.0)
+        t0 = time.time()
+        with pytest.raises(L.DLPError) as e:
+            sess[0].run(100)   # rank 1 never enqueues anything
+        assert e.value.status in (L.ERR_RCCL, L.ERR_HIP)
+        assert time.time() - t0 < 30
+    finally:
+        for s in sess:
+            s.close()
+
+
+def test_c3_row_partition_peer_exchange_one_gpu():
+    """BASELINE.json C3 (32768 x 32768) as the 8-GPU split runs it, on ONE MI355X:
+    8 rank sessions (4,096 local rows each; K = 64, form 21, 256-row bands), the
+    exchange through the peer blocks, 160 pivots (two full blocks + a 32-pivot tail),
+    against the oracle's committed digests: pivot log, basis, objective and the
+    whole tableau."""
+    g = load_golden("digests.json")
+    tab = g["c3_tableau"]
+    k, P = 160, 8
+    want = tab["stops"][str(k)]
+    prob = dlp.Problem.random(tab["m"], tab["n"], tab["seed"])
+    sess = [dlp.Session(prob, rank=r, nranks=P, defer=64, check_interval=64) for r in range(P)]
+    try:
+        for s in sess:
+            assert s.get_defer_tuning()[1:] == (21, 64) and s.get_tuning()[1] == 256
+        dlp.Session.connect_peers(sess)
+        st, done = dlp.Session.run_ranks(sess, k)
+        assert done == k
+        for s in sess:
+            lg = s.result().pivot_log
+            assert len(lg) == k
+            import hashlib
+            assert hashlib.sha256(np.ascontiguousarray(lg).tobytes()).hexdigest() == want["log_sha256"]
+        merged = dlp.Session.merged_result(sess)
+        import hashlib
+        assert hashlib.sha256(np.ascontiguousarray(merged.basis).tobytes()).hexdigest() == want["basis_sha256"]
+        assert float(merged.objective).hex() == want["objective_hex"]
+        assert tableau_sha256(sess, tab["width"]) == want["tableau_sha256"]
+    finally:
+        for s in sess:
+            s.close()
+
+
+# ---- two processes on one GPU: IPC handles of the exchange blocks ---------------------
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ipc_worker(rank, world, port, m, n, seed, defer, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s = dlp.Session(dlp.Problem.random(m, n, seed), rank=rank, nranks=world, defer=defer,
+                        check_interval=29)
+        hs = [None] * world
+        dist.all_gather_object(hs, s.exchange_handle())
+        s.connect_ipc(hs)
+        s.set_exchange_timeout(60.0)
+        st, done = s.run(10 ** 6)
+        res = s.result()
+        q.put((rank, st, done, np.ascontiguousarray(res.pivot_log).tobytes(), res.objective,
+               res.x.tobytes(), res.y.tobytes()))
+        dist.barrier()   # no rank frees its block while a peer may still read it
+        s.close()
+    except Exception as e:   # reported to the parent, which fails the test
+        q.put((rank, "error", repr(e), None, None, None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("defer", [1, 16])
+def test_peer_exchange_two_processes_ipc(defer):
+    import torch.multiprocessing as mp
+    m, n, seed, world = 120, 150, 4, 2
+    A, b, c = O.gen_dense(m, n, seed)
+    ref = O.solve_dense(A, b, c)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ipc_worker, args=(r, world, port, m, n, seed, defer, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=110) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, st, done, log, obj, x, y in out:
+        assert st != "error", done
+        assert st == L.OK and done == ref.num_pivots
+        assert log == np.ascontiguousarray(ref.pivot_log).tobytes()
+        assert obj == ref.objective and y == ref.y.tobytes()
+    xs = np.sum([np.frombuffer(o[5]) for o in out], axis=0)
+    assert xs.tobytes() == ref.x.tobytes()
+    assert all(p.exitcode == 0 for p in procs)

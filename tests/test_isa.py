@@ -121,3 +121,51 @@ def test_lookahead_kernels_fit_beside_the_form21_pass():
     assert one("pass_d_kernel") <= 160, c
     assert one("ratio_lean_kernelILi128ELi4E") <= 32
     assert one("prow_defer_kernelILb1E") <= 32
+
+
+def _functions(text):
+    """{symbol: [instruction lines]} of the disassembly."""
+    funcs, cur = {}, None
+    for line in text.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line.strip())
+        if m:
+            cur = funcs.setdefault(m.group(1), [])
+            continue
+        line = line.split("//")[0].strip()
+        if cur is not None and line and not line.endswith(":"):
+            cur.append(line)
+    return funcs
+
+
+def test_peer_row_push_stores_both_halves():
+    """hipcc (ROCm 7.2) compiles __builtin_bit_cast(T, v.y) of an ext_vector element as a
+    cast of element 0.  In the deferred pivot-row kernel that made the peer exchange push
+    the even column's value into both words of every column pair (found by
+    tests/test_gpu_peer.py).  The kernel now copies the elements to scalars first: its
+    two system-scope row stores (columns j and j + 1) must store different registers."""
+    funcs = _functions(_disasm())
+    checked = 0
+    for name, ins in funcs.items():
+        if "prow_defer_kernel" not in name:
+            continue
+        st = [i for i in ins if i.startswith(("flat_store_dwordx2", "global_store_dwordx2")) and "sc0 sc1" in i]
+        hi = [i for i in st if "offset:8" in i]
+        lo = [i for i in st if "offset:8" not in i]
+        assert hi and lo, (name, st)
+        data = lambda i: i.split(None, 1)[1].split(",")[1].strip()
+        assert {data(i) for i in hi}.isdisjoint({data(i) for i in lo}), (name, st)
+        checked += 1
+    assert checked >= 2, checked
+
+
+def test_no_bit_cast_of_a_vector_element_in_kernels():
+    """Source guard for the same compiler behaviour: no __builtin_bit_cast of a .x/.y/.z/.w
+    element or a subscripted element of an ext_vector value in the kernel sources."""
+    pat = re.compile(r"__builtin_bit_cast\(\s*\w+\s*,\s*[\w\[\]]+\.[xyzw]\s*\)")
+    csrc = os.path.join(ROOT, "distributedlpsolver_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")):
+            with open(os.path.join(csrc, f)) as fh:
+                for k, line in enumerate(fh, 1):
+                    code = line.split("//")[0]
+                    assert not pat.search(code), f"{f}:{k}: {line.strip()}"

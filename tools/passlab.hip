@@ -1346,6 +1346,115 @@ void launch_mpass4(const Lab& L, int, int rb, hipStream_t s) {
     mpass4_kernel<K, NT><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
 }
 
+// ---- f4r: form 21's compute (P[0..64) of one column per lane in VGPRs, 2 rows per
+// group, coefficients broadcast by v_fmac_f64_dpp) with the rows AND the coefficient rows
+// of each group staged per wave in an LDS ring of D groups by LDS-DMA
+// (global_load_lds_dwordx4 from inline asm: the compiler does not count it, the kernel
+// waits with its own counted vmcnt), so D groups of loads are in flight per wave instead
+// of one group in registers.  Ring slot (2 KB): rows r0, r0+1 x the wave's 64 columns
+// (lane l's 16 B = row l / 32, columns 2 (l % 32) .. +1), then the two rows' 64
+// coefficients each (lane l: row l / 32, steps 2 (l % 32) .. +1).
+__device__ __forceinline__ void glds16(const void* g, uint32_t m0) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <int D>
+__device__ __forceinline__ void vmwait_group(int g) {
+    // newer than group g's two DMAs: 2 (D - 1 - g) prologue DMAs + 4 per finished group,
+    // 4 (D - 1) in the steady state (2 stores + 2 DMAs per group)
+    if (g >= D - 1) { vmwait<4 * (D - 1)>(); return; }
+    switch (g) {
+        case 0: vmwait<2 * (D - 1)>(); break;
+        case 1: vmwait<2 * (D - 1) + 2>(); break;
+        case 2: vmwait<2 * (D - 1) + 4>(); break;
+        case 3: vmwait<2 * (D - 1) + 6>(); break;
+        case 4: vmwait<2 * (D - 1) + 8>(); break;
+        case 5: vmwait<2 * (D - 1) + 10>(); break;
+        default: vmwait<2 * (D - 1) + 12>(); break;
+    }
+}
+template <int L>
+__device__ __forceinline__ void rstep(double (&t)[2], const double (&c)[2][2][2], const double (&pr)[64]) {
+    constexpr int h = L / 32, e = L & 1, n = (L & 31) >> 1;
+    fmac_bc<n>(t[0], c[0][h][e], pr[L]);
+    fmac_bc<n>(t[1], c[1][h][e], pr[L]);
+}
+template <int L0, int... I>
+__device__ __forceinline__ void rhalf(double (&t)[2], const double (&c)[2][2][2], const double (&pr)[64],
+                                      std::integer_sequence<int, I...>) {
+    (rstep<L0 + I>(t, c, pr), ...);
+}
+template <bool NT, int D, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void f4r_kernel(
+    const double* __restrict__ T, double* __restrict__ To, int64_t ld, int64_t rows, int64_t width,
+    const double* __restrict__ Cr, const double* __restrict__ P, int rb) {
+    constexpr int K = 64;
+    extern __shared__ double ring[];   // [4 waves][D slots][256 doubles]
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool colok = j < width;
+    const int jc = (int)(colok ? j : width - 1);
+    double pr[K];
+#pragma unroll
+    for (int l = 0; l < K; ++l) pr[l] = P[(int64_t)l * ld + jc];
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    const int ng = nr / 2;   // (the lab's bands have even row counts)
+    const int64_t wc = (int64_t)blockIdx.x * 256 + w * 64 + 2 * (lane & 31);
+    const int64_t wcc = wc < ld - 1 ? wc : ld - 2;
+    const double* tsrc = T + (i0 + (lane >> 5)) * ld + wcc;
+    const double* csrc = Cr + (i0 + (lane >> 5)) * K + 2 * (lane & 31);
+    double* wbase = ring + (size_t)w * D * 256;
+    const uint32_t lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)wbase;
+    // a uniform descriptor (a per-lane one becomes a waterfall loop of stores, which would
+    // break the counted waits); lanes past the width aim out of range and are dropped
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(To + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
+    const int voff = colok ? jc * 8 : 0x7fffff00;
+    const int rowb = (int)(ld * 8);
+    auto dma = [&](int g, int s) {
+        const int gg = g < ng ? g : ng - 1;
+        glds16(tsrc + (int64_t)gg * 2 * ld, __builtin_amdgcn_readfirstlane(lbase + s * 2048));
+        glds16(csrc + (int64_t)gg * 2 * K, __builtin_amdgcn_readfirstlane(lbase + s * 2048 + 1024));
+    };
+#pragma unroll
+    for (int s = 0; s < D; ++s) dma(s, s);
+    int s = 0;
+    for (int g = 0; g < ng; ++g) {
+        vmwait_group<D>(g);
+        const double* sl = wbase + s * 256;
+        double t[2];
+        t[0] = sl[lane];
+        t[1] = sl[64 + lane];
+        double c[2][2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const d2 v = *(const d2*)(sl + 128 + u * 64 + h * 32 + 2 * (lane & 15));
+                c[u][h][0] = v.x;
+                c[u][h][1] = v.y;
+            }
+        rhalf<0>(t, c, pr, std::make_integer_sequence<int, 32>{});
+        rhalf<32>(t, c, pr, std::make_integer_sequence<int, 32>{});
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const double v = t[u];
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), ro, voff, (2 * g + u) * rowb, NT ? 2 : 0);
+        }
+        dma(g + D, s);
+        s = s + 1 == D ? 0 : s + 1;
+    }
+}
+template <int D, int W>
+void launch_f4r(const Lab& L, int, int rb, hipStream_t s) {
+    dim3 grid((unsigned)((L.width + 255) / 256), (unsigned)((L.rows + rb - 1) / rb));
+    f4r_kernel<true, D, W><<<grid, 256, (size_t)4 * D * 2048, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+}
+
 struct Variant {
     const char* name;
     int K, rb;
@@ -1402,6 +1511,13 @@ int main(int argc, char** argv) {
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
     const char* only = argc > 4 ? argv[4] : nullptr;
     std::vector<Variant> vs = {
+        {"f4r K64 D2 w3", 64, 768, launch_f4r<2, 3>, true},
+        {"f4r K64 D3 w3", 64, 768, launch_f4r<3, 3>, true},
+        {"f4r K64 D4 w3", 64, 768, launch_f4r<4, 3>, true},
+        {"f4r K64 D5 w3", 64, 768, launch_f4r<5, 3>, true},
+        {"f4r K64 D6 w3", 64, 768, launch_f4r<6, 3>, true},
+        {"f4r K64 D4 w3 rb256", 64, 256, launch_f4r<4, 3>, true},
+        {"f4r K64 D6 w2", 64, 768, launch_f4r<6, 2>, true},
         {"f4d K32 V2U2 mov", 32, 256, launch_f4d<32, 2, 2, false>, true},
         {"f4d K32 V2U2 asm", 32, 256, launch_f4d<32, 2, 2, true>, true},
         {"f4d K32 V2U4 asm", 32, 256, launch_f4d<32, 2, 4, true>, true},

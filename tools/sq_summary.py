@@ -5,7 +5,7 @@
 
 Launches doing no work (a deferred pass is launched as a full-block and a
 partial-block instance, exactly one of which works) are dropped: SQ_WAVE_CYCLES
-under 5 % of the largest.  Fractions are of SQ_WAVE_CYCLES (quad-cycles; the
+(else SQ_INSTS_VALU, else SQ_WAVES) under 5 % of the largest.  Fractions are of SQ_WAVE_CYCLES (quad-cycles; the
 three SQ states WAIT_ANY, WAIT_INST_ANY and ACTIVE_INST_ANY are disjoint:
 MI355X_MICROARCH.md §rocprofv3 PMC slots)."""
 import collections
@@ -29,11 +29,14 @@ def main():
                 key = (path, row.get("Dispatch_Id") or row.get("Correlation_Id"))
                 per[key][row["Counter_Name"]] = per[key].get(row["Counter_Name"], 0.0) + \
                     float(row["Counter_Value"])
-    launches = [v for v in per.values() if "SQ_WAVE_CYCLES" in v]
+    ref = next((k for k in ("SQ_WAVE_CYCLES", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_BUSY_CYCLES")
+                if any(k in v for v in per.values())), None) or \
+        next(iter(sorted({k for v in per.values() for k in v})), None)
+    launches = [v for v in per.values() if ref in v]
     if not launches:
         raise SystemExit(f"no launches of {sub!r} under {d}")
-    top = max(v["SQ_WAVE_CYCLES"] for v in launches)
-    launches = [v for v in launches if v["SQ_WAVE_CYCLES"] >= 0.05 * top]
+    top = max(v[ref] for v in launches)
+    launches = [v for v in launches if v[ref] >= 0.05 * top]
     keys = sorted({k for v in launches for k in v})
     out = {"kernel": name, "launches": len(launches)}
     for k in keys:
