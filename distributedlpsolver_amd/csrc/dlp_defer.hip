@@ -1424,6 +1424,23 @@ __device__ __forceinline__ void dpp_half(double (&t)[2], const double (&c)[2][2]
     (dpp_step<L0 + I>(t, c, pr), ...);
 }
 
+// Generic replay of one row of class cl (a pivot row at step cl >= 0: start from P[cl]; a
+// sparse row: skip the steps whose coefficient is 0) over the 64 steps, P[0..64) of the
+// lane's column in registers (unrolled: no dynamic register index), the row's coefficients
+// from f(l) (uniform).  The tails of a partial block have f == 0 and are skipped.
+template <typename F>
+__device__ __forceinline__ double replay_row(double t, int cl, const double (&pr)[64], F f) {
+#pragma unroll
+    for (int l = 0; l < 64; ++l) {
+        const double c = f(l);
+        if (l == cl)
+            t = pr[l];
+        else if (l > cl && c != 0.0)
+            t = __builtin_fma(-c, pr[l], t);
+    }
+    return t;
+}
+
 template <bool NT>
 __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ T, double* __restrict__ Tout,
                                                      int64_t ld, int64_t rows, int64_t width,
@@ -1528,21 +1545,179 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
             __builtin_amdgcn_raw_buffer_store_b64(x, ro, voff_st, r * ld8, NT ? 2 : 0);
         } else if (cl != kUntouched) {
             const double* cr = C + (i0 + r) * ldc;
-            double t;
-            int l = 0;
-            if (cl >= 0) {
-                t = P[(int64_t)cl * ld + jc];
-                l = cl + 1;
-            } else {
+            double t = 0.0;
+            if (cl < 0)
                 t = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rt, voff, r * ld8, NT ? 2 : 0));
-            }
-            for (; l < kb; ++l) {
-                const double f = cr[l];
-                if (f != 0.0) t = __builtin_fma(-f, P[(int64_t)l * ld + jc], t);
-            }
+            t = replay_row(t, cl, pr, [&](int l) { return cr[l]; });
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t), ro, voff_st, r * ld8, NT ? 2 : 0);
         }
         r += 1;
+    }
+}
+
+// Form 23: form 21's arithmetic (P[0..64) of one column per lane in 128 VGPRs, the
+// coefficients broadcast by v_fmac_f64_dpp) with the tableau rows and their coefficient
+// rows staged through an LDS ring instead of registers.  Form 21 holds one 2-row group
+// ahead in registers: 1 KB in flight per wave, so the stream is latency-bound (4.2 TB/s).
+// Here each wave keeps D groups of U rows in flight by LDS-DMA (global_load_lds_dwordx4:
+// no VGPRs): ring slot = U rows x the wave's 64 columns, then the U rows' 64 coefficients
+// (DMA k: rows 2k, 2k+1, lane l's 16 B = row 2k + l / 32, columns / steps 2 (l % 32), +1).
+// The DMAs are issued from inline asm so that hipcc does not count them (it would wait
+// vmcnt(0) before the next LDS read, draining the ring: cdna_hip_programming.md, glds);
+// the kernel waits with its own counted vmcnt, which relies on every group issuing exactly
+// U DMAs and U stores (rows with nothing to store aim a store out of range).  Groups whose
+// U rows are all dense run the chains from LDS; any other group replays row by row
+// (replay_row: T and the coefficients from the slot, P from the registers).  Lab:
+// 7.3-7.5 ms per C3 pass against form 21's 8.2-8.5 (tools/passlab.hip f4r, bit-exact).
+__device__ __forceinline__ void glds16(const void* g, uint32_t m0) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// newer than group g's U DMAs: U per prologue group still to come and 2 U (U stores + U
+// DMAs) per finished group: U (D - 1) + U g while g < D - 1, then 2 U (D - 1)
+template <int D, int U>
+__device__ __forceinline__ void vmwait_group(int g) {
+    static_assert(D <= 8 && 2 * U * (D - 1) <= 63, "vmcnt holds 6 bits");
+    if (g >= D - 1) {
+        vmwait<2 * U * (D - 1)>();
+        return;
+    }
+    switch (g) {
+        case 0: vmwait<U * (D - 1)>(); break;
+        case 1: vmwait<U * (D - 1) + U>(); break;
+        case 2: vmwait<U * (D - 1) + 2 * U>(); break;
+        case 3: vmwait<U * (D - 1) + 3 * U>(); break;
+        case 4: vmwait<U * (D - 1) + 4 * U>(); break;
+        case 5: vmwait<U * (D - 1) + 5 * U>(); break;
+        default: vmwait<U * (D - 1) + 6 * U>(); break;
+    }
+}
+template <int U, int L>
+__device__ __forceinline__ void ring_step(double (&t)[U], const double (&c)[U][2], const double (&pr)[64]) {
+    constexpr int e = L & 1, n = (L & 31) >> 1;
+#pragma unroll
+    for (int u = 0; u < U; ++u) fmac_bc<n>(t[u], c[u][e], pr[L]);
+}
+template <int U, int L0, int... I>
+__device__ __forceinline__ void ring_half(double (&t)[U], const double (&c)[U][2], const double (&pr)[64],
+                                          std::integer_sequence<int, I...>) {
+    (ring_step<U, L0 + I>(t, c, pr), ...);
+}
+
+template <bool NT, int U, int D>
+__global__ __launch_bounds__(256) void pass_q_kernel(const double* __restrict__ T, double* __restrict__ Tout,
+                                                     int64_t ld, int64_t rows, int64_t width,
+                                                     const BlockDesc* __restrict__ bd,
+                                                     const double* __restrict__ C, int64_t ldc,
+                                                     const double* __restrict__ P,
+                                                     const int32_t* __restrict__ nzc, int rb) {
+    constexpr int K = 64, SLOT = 128 * U;   // doubles per ring slot
+    static_assert(U % 2 == 0, "one DMA carries two rows");
+    __shared__ int32_t cls[1024];
+    extern __shared__ double ring[];   // [4 waves][D slots][SLOT]
+    const int kb = bd->blk;
+    const bool outplace = Tout != T;
+    if (kb == 0 && !outplace) return;   // full and partial blocks alike (zeroed tails)
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool colok = j < width;
+    const int jc = (int)(colok ? j : width - 1);
+    double pr[K];   // all 64 rows: a partial block's P[l >= kb] is +0 (zeroed at block start)
+#pragma unroll
+    for (int l = 0; l < K; ++l) pr[l] = P[(int64_t)l * ld + jc];
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int nr = (int)(iend - i0);
+    classify_band(cls, bd, nzc, i0, nr, kb);
+    __syncthreads();
+    // the P loads complete here, before the ring starts (else hipcc waits for them, and
+    // with them for everything, at the top of every group)
+#pragma unroll
+    for (int l = 0; l < K; ++l) asm volatile("" ::"v"(pr[l]));
+    const int ng = (nr + U - 1) / U;
+    // DMA sources: this lane's row of each DMA (row 2k + lane / 32 of a group, clamped to the
+    // band) and its 16 B of the wave's 64 columns (clamped inside the row stride) / of the
+    // row's 64 coefficients
+    const int64_t wc = (int64_t)blockIdx.x * 256 + w * 64 + 2 * (lane & 31);
+    const int64_t wcc = wc < ld - 1 ? wc : ld - 2;
+    const double* tsrc = T + i0 * ld + wcc;
+    const double* csrc = C + i0 * ldc + 2 * (lane & 31);
+    double* wbase = ring + (size_t)w * D * SLOT;
+    const uint32_t lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)wbase;
+    auto dma = [&](int g, int s) {
+        const int gg = g < ng ? g : ng - 1;
+#pragma unroll
+        for (int k = 0; k < U / 2; ++k) {
+            int r = gg * U + 2 * k + (lane >> 5);
+            r = r < nr ? r : nr - 1;
+            glds16(tsrc + (int64_t)r * ld, __builtin_amdgcn_readfirstlane(lbase + s * SLOT * 8 + k * 1024));
+        }
+#pragma unroll
+        for (int k = 0; k < U / 2; ++k) {
+            int r = gg * U + 2 * k + (lane >> 5);
+            r = r < nr ? r : nr - 1;
+            glds16(csrc + (int64_t)r * ldc,
+                   __builtin_amdgcn_readfirstlane(lbase + s * SLOT * 8 + U * 512 + k * 1024));
+        }
+    };
+    // band descriptor (the caller keeps rb * ld * 8 < 2^31): rows at soffset r * ld8; stores
+    // of lanes past the width, and of rows with nothing to store, go out of range (dropped)
+    const int ld8 = (int)(ld * 8);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Tout + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
+    const int voff_st = colok ? jc * 8 : 0x7fffff00;
+    auto store = [&](double v, int r, bool keep) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), ro, keep ? voff_st : 0x7fffff00,
+                                              (r < nr ? r : 0) * ld8, NT ? 2 : 0);
+    };
+#pragma unroll
+    for (int s = 0; s < D; ++s) dma(s, s);
+    int s = 0;
+    for (int g = 0; g < ng; ++g) {
+        vmwait_group<D, U>(g);
+        const double* sl = wbase + s * SLOT;
+        const int r0 = g * U;
+        bool dense = r0 + U <= nr;
+#pragma unroll
+        for (int u = 0; u < U; ++u) dense = dense && cls[r0 + u < nr ? r0 + u : 0] == kDense;
+        if (dense) {   // (uniform)
+            double t[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) t[u] = sl[u * 64 + lane];
+            double c[U][2];
+            auto loadc = [&](int h) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const d2 v = *(const d2*)(sl + U * 64 + u * 64 + h * 32 + 2 * (lane & 15));
+                    c[u][0] = v.x;
+                    c[u][1] = v.y;
+                }
+            };
+            loadc(0);
+            ring_half<U, 0>(t, c, pr, std::make_integer_sequence<int, 32>{});
+            loadc(1);
+            ring_half<U, 32>(t, c, pr, std::make_integer_sequence<int, 32>{});
+#pragma unroll
+            for (int u = 0; u < U; ++u) store(t[u], r0 + u, true);
+        } else {
+            // generic replay, row by row (form 21's); exactly U stores for the counted waits
+            for (int u = 0; u < U; ++u) {
+                const int r = r0 + u;
+                const int cl = r < nr ? cls[r] : kUntouched;
+                double t = sl[u * 64 + lane];
+                if (cl == kUntouched) {
+                    store(t, r, outplace && r < nr);
+                    continue;
+                }
+                const double* cr = sl + U * 64 + u * 64;   // the row's coefficients (broadcast reads)
+                t = replay_row(t, cl, pr, [&](int l) { return cr[l]; });
+                store(t, r, true);
+            }
+        }
+        dma(g + D, s);
+        s = s + 1 == D ? 0 : s + 1;
     }
 }
 
@@ -1914,9 +2089,26 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             return hipGetLastError();
         }
     }
+    if (d.form == 23 && K == 64 && d.K == 64 && d.ldc == 64 && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31) &&
+        rb <= 1024) {
+        // LDS-ring DPP pass (K = 64 blocks; 256-column tiles): 2 rows per group, 4 groups in
+        // flight per wave: 32 KiB of ring + 4 KiB of row classes per workgroup, so three pass
+        // workgroups leave the lookahead chain's LDS free on a CU
+        if constexpr (K == 64) {
+            constexpr int U = 2, D = 4;
+            size_t dyn = (size_t)4 * D * 128 * U * sizeof(double);
+            if (occ > 0) dyn = std::max(dyn, (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t));
+            const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
+            if (g.rows > 0) {
+                pass_q_kernel<NT, U, D><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
+                                                              d.P, d.nzc, rb);
+            }
+            if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
+            return hipGetLastError();
+        }
+    }
     // streamed forms need K >= 16 (an even number of coefficient chunks): form 3 below
-    const int form = (d.form >= 6 && d.form != 14 && d.form != 15 && d.form != 20 && d.form != 21 && d.form != 22) ? 3
-                     : (d.form == 21 || d.form == 22) ? 3 : d.form;
+    const int form = (d.form >= 6 && d.form != 14 && d.form != 15 && d.form != 20) ? 3 : d.form;
     const int cols = (form == 0 || form == 4 || form >= 14) ? kDeferTile : 256;
     const int ntiles = (int)((g.width + cols - 1) / cols);
     const int64_t bands = (g.rows + rb - 1) / rb;
@@ -2009,7 +2201,7 @@ static hipError_t pass_k(const Geometry& g, const Defer& d, DevState* st, int rb
 }
 
 bool lookahead_form(int form) {
-    return form == 3 || form == 4 || form == 5 || form == 20 || form == 21 || form == 22;
+    return form == 3 || form == 4 || form == 5 || form == 20 || form == 21 || form == 22 || form == 23;
 }
 
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,

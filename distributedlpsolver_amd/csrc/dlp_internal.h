@@ -227,8 +227,9 @@ hipError_t launch_commit_defer(const Geometry& g, const Defer& d, DevState* st,
                                const XPeers* xp = nullptr, uint32_t seq = 0);
 // The tableau pass: applies the block's st->blk steps to rows [0, rows), then blk = 0.
 // Lookahead (seal >= 0): the block st->seal[seal], read from g.T and written to Tout
-// (every row, untouched ones copied; blk is left alone).  Forms 3, 4, 5 and 20 only
-// (lookahead_form).
+// (every row, untouched ones copied; blk is left alone).  Only the forms with an
+// out-of-place instance: lookahead_form() is the single source of truth (3, 4, 5, 20, 21,
+// 22, 23).
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
                               int rows_per_block, int occupancy, hipStream_t s,
                               double* Tout = nullptr, int seal = -1);

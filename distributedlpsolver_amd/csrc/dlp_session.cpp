@@ -165,6 +165,20 @@ namespace {
 
 int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
 
+// DLP_TRACE_CREATE=1: milliseconds of each stage of session creation / free on stderr
+// (tools/c1_overhead.py; diagnostics only)
+struct StageClock {
+    bool on = std::getenv("DLP_TRACE_CREATE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "dlp stage %-22s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
 int auto_rows_per_block(const dlp_session* s) { return s->streaming ? 8 : 4; }
 // deferred pass band rows: 64 on a cache-resident tableau, 256 streaming; 768 for the K = 64
 // streaming pass over >= 16k local rows (form 21 reads P once per band: C3 7,227 / 7,361 / 7,433
@@ -174,7 +188,7 @@ int auto_rows_per_block(const dlp_session* s) { return s->streaming ? 8 : 4; }
 // forms (3/4/5/20/21/22) take tall bands: forms 0-2 stage the band's coefficients in LDS
 // (fit_defer_rb).
 bool tall_band_form(int form) {
-    return form == 3 || form == 4 || form == 5 || form == 20 || form == 21 || form == 22;
+    return form == 3 || form == 4 || form == 5 || form == 20 || form == 21 || form == 22 || form == 23;
 }
 // Forms 0-2 hold the band's K coefficients per row + a row index in dynamic LDS and s_pl[K]
 // statically: K * rb * 8 + rb * 4 + K * 4 <= 160 KiB.  Bands only change the work split, never
@@ -265,8 +279,10 @@ void host_tableau(const dlp_problem* p, int64_t row_first, int64_t rows, int64_t
 
 void free_session(dlp_session* s) {
     if (!s) return;
+    StageClock clk;
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    clk.mark("free: sync");
     if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
     if (s->graph) (void)hipGraphDestroy(s->graph);
     for (auto e : s->ev) (void)hipEventDestroy(e);
@@ -291,7 +307,9 @@ void free_session(dlp_session* s) {
     if (s->xpeers) (void)hipFree(s->xpeers);
     if (s->xabort) (void)hipHostFree(s->xabort);
     if (s->host_st) (void)hipHostFree(s->host_st);
+    clk.mark("free: buffers");
     if (s->stream) (void)hipStreamDestroy(s->stream);
+    clk.mark("free: stream");
     delete s;
 }
 
@@ -377,12 +395,14 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         return DLP_ERR_NODEVICE;
     }
     if (s->device < 0 || s->device >= ndev) { set_error("device ordinal out of range"); return DLP_ERR_ARG; }
+    StageClock clk;
     HIP_TRY(hipSetDevice(s->device));
     // the pivot chain runs at the highest stream priority: under lookahead its small
     // launches share the device with the pass (pstream, lowest priority)
     int prio_least = 0, prio_greatest = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
     HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_greatest));
+    clk.mark("create: stream");
 
     const int64_t rows_total = s->rows + 1;
     dlp::Geometry& g = s->g;
@@ -473,6 +493,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         return DLP_ERR_OOM;
     }
     g.T = s->T;
+    clk.mark("create: plan + tableau");
     if (s->cluster) {
         HIP_TRY(hipMalloc(&s->cl_gran, sizeof(uint64_t) * dlp::cluster_granules(s->m, s->cl_wg)));
     }
@@ -519,6 +540,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         s->defer_rb = s->defer_rb_req > 0 ? fit_defer_rb(s, s->defer_rb_req) : auto_defer_rb(s);
     }
     HIP_TRY(hipMemsetAsync(s->prow_send, 0, sizeof(int64_t) * s->ld, s->stream));
+    clk.mark("create: side arrays");
 
     // tableau
     if (prob->kind == dlp::PROB_RANDOM) {
@@ -548,6 +570,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     HIP_TRY(dlp::launch_price_init(g, s->pp, opt->tol_dj, opt->update_variant, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     s->Tb[0] = s->T;
+    clk.mark("create: fill + state");
 
     // lookahead: deferred, a pass form with an out-of-place instance, the exchange (if
     // any) driven by the session, no per-phase timing, and room for a second tableau
@@ -601,6 +624,12 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
             s->la = true;
         }
         s->opt.lookahead = s->la ? 1 : 0;
+        // a K = 64 streaming pass with nothing beside it (no lookahead: a multi-rank session,
+        // or lookahead off) streams its rows through the LDS ring (form 23: C3 7.9 vs 8.2 ms
+        // per pass in situ, 7.3 in the lab).  Under lookahead form 21 stays: the ring's
+        // deeper memory queue slows the selection chain beside it more than it speeds the pass
+        // (C3 6,578 vs 7,685 pivots/s, profiles/r03d/)
+        if (s->d.form == 21 && s->d.K == 64 && s->streaming && !s->la) s->d.form = 23;
     }
 
     if (comm_in) {
@@ -619,6 +648,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         for (auto& e : s->ev) HIP_TRY(hipEventCreate(&e));
         s->ev_flush.assign(opt->check_interval, 0);
     }
+    clk.mark("create: lookahead + comm");
     return DLP_OK;
 }
 
@@ -2043,7 +2073,7 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
 }
 
 int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
-    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 22) return DLP_ERR_ARG;
+    if (!s || occupancy < 0 || occupancy > 32 || form < -1 || form > 23) return DLP_ERR_ARG;
     if ((form == 0 || form == 4 || form == 6 || form == 7 || form == 10 || form == 11 || form == 14 ||
          form == 15 || form == 16 || form == 17 || form == 20) &&
         s->d.K > 32) {

@@ -1,7 +1,7 @@
 """GPU, BASELINE.json C3 (32768 x 32768, N = 65536) as the multi-GPU row
 partition runs it, on ONE MI355X: 8 rank sessions of the same LP (4,096 local
 rows x 65,537 columns each, 2.2 GB per rank), the geometry a rank of the
-8-GPU split picks by itself (K = 64 deferred blocks through the form-21 pass,
+8-GPU split picks by itself (K = 64 deferred blocks through the form-23 pass,
 256-row bands, no lookahead), the exchange done by the host (all-gather of the
 32-B candidates, int64 MAX all-reduce of the pivot row: the device code the RCCL
 path runs, SURVEY.md §8(e), replacing the reference's per-impression
@@ -53,7 +53,7 @@ def test_c3_row_partition_one_gpu(P):
     try:
         for r, s in enumerate(sess):
             occ, form, K = s.get_defer_tuning()
-            assert (K, form) == (64, 21), (r, K, form)   # the auto multi-rank geometry
+            assert (K, form) == (64, 23), (r, K, form)   # the auto multi-rank geometry (no lookahead)
             assert s.get_tuning()[1] == 256               # 256-row bands below 16k local rows
             assert not s.lookahead()
             assert s.rows in (m // P, m // P + 1)

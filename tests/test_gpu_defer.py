@@ -181,7 +181,8 @@ def test_defer_update_stats():
 
 
 @pytest.mark.parametrize("P,K,form", [(1, 8, -1), (2, 4, -1), (2, 16, -1), (3, 32, -1), (2, 64, 21), (3, 64, 21),
-                                      (2, 64, 22), (4, 16, -1), (4, 64, 21), (8, 16, -1), (8, 64, 21)])
+                                      (2, 64, 22), (4, 16, -1), (4, 64, 21), (8, 16, -1), (8, 64, 21),
+                                      (2, 64, 23), (8, 64, 23)])
 def test_defer_step_api_multi_rank_one_gpu(P, K, form):
     """The deferred exchange path (ratio -> candidate all-gather -> select ->
     pivot-row MAX all-reduce -> commit, pass every K pivots) with P row-block
@@ -235,12 +236,13 @@ def test_auto_block_size_policy():
         assert s.update_stats()[2] == 16
 
 
-@pytest.mark.parametrize("form", [21, 22])
+@pytest.mark.parametrize("form", [21, 22, 23])
 @pytest.mark.parametrize("m,n,seed,rb,nt,occ", [(300, 520, 5, 64, 1, 0), (300, 520, 5, 256, 0, 0),
                                                 (700, 1337, 7, 1000, 1, 0), (129, 4000, 2, 37, 1, 2),
                                                 (1200, 700, 9, 128, 1, 3)])
 def test_pass_form21_dpp_full_blocks(m, n, seed, rb, nt, occ, form):
-    """Forms 21 (DPP-broadcast coefficients) and 22 (MFMA), K = 64: two full blocks and a partial one
+    """Forms 21 (DPP-broadcast coefficients), 22 (MFMA) and 23 (DPP from an LDS ring), K = 64: two full
+    blocks and a partial one
     (17 steps: the unused steps' coefficients and pivot rows zeroed at block start), widths that are not a
     multiple of the 256-column tile, bands from 37 to 1000 rows (the last one short),
     pivot rows inside the bands; whole tableau byte-equal to the eager session's."""
@@ -262,7 +264,7 @@ def test_pass_form21_dpp_full_blocks(m, n, seed, rb, nt, occ, form):
     assert Td.tobytes() == Te.tobytes()
 
 
-@pytest.mark.parametrize("form", [21, 22])
+@pytest.mark.parametrize("form", [21, 22, 23])
 @pytest.mark.parametrize("K", [64, 40])
 def test_pass_form21_sparse_and_degenerate(K, form):
     """Form 21 on a sparse tableau (ad-allocation LP: untouched / sparse rows through
@@ -304,7 +306,7 @@ def test_lds_forms_on_streaming_k64_geometry(form):
     k = 2 * 64 + 9
     prob = dlp.Problem.random(m, n, 21)
     with dlp.Session(prob, defer=64, check_interval=64) as s:
-        assert s.get_tuning()[1] == 768 and s.defer_form() == 21
+        assert s.get_tuning()[1] == 768 and s.defer_form() == (21 if s.lookahead() else 23)
         s.set_defer_tuning(0, form)
         rb = s.get_tuning()[1]
         assert 64 * rb * 8 + rb * 4 + 64 * 4 <= 160 * 1024 and rb >= 256

@@ -71,24 +71,29 @@ def test_c3_full_size():
     assert np.ascontiguousarray(obj_row[:w]).tobytes() == ref_rows[-1].tobytes()
 
 
+AUTO_K64_FORM = 21   # the streaming K = 64 default (dlp_session.cpp auto_form)
+
+
 def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0, tableau_digest=None):
+def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0, tableau_digest=None, form=None):
     """k pivots in windows of ci (whole K-blocks, then a tail) through the auto
     geometry of the bench (deferred K, pass form, band rows, ld alignment);
     the whole pivot log, every pivot row, random rows and the objective row
     against the oracle on the same generated LP, byte for byte."""
     rng = np.random.default_rng(seed)
     with dlp.Session(dlp.Problem.random(m, n, seed), check_interval=ci, defer=defer) as s:
-        occ, form, K = s.get_defer_tuning()
+        if form is not None:
+            s.set_defer_tuning(0, form)
+        occ, f, K = s.get_defer_tuning()
         assert K == want_K
         if K == 64:
-            assert form == 21 and s.get_tuning()[1] == 768   # the bench's pass
+            assert f == (form or AUTO_K64_FORM) and s.get_tuning()[1] == 768   # the bench's pass
             assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
         if K == 32:
-            assert form == 4 and s.get_tuning()[1] == 256   # round 2's first default
+            assert f == 4 and s.get_tuning()[1] == 256   # round 2's first default
             assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
         done = 0
         while done < k:
@@ -117,13 +122,15 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0, tableau_digest=No
     return launches
 
 
-def test_c3_full_blocks_bit_exact():
-    """C3 at the bench geometry: 2 full K = 64 blocks through the form-21 pass
-    (DPP coefficients, 768-row bands, ld 66048, nt), then an 8-pivot tail (a
-    partial block: coefficients of the unused steps zeroed in memory)."""
+@pytest.mark.parametrize("form", [None, 21, 23])
+def test_c3_full_blocks_bit_exact(form):
+    """C3 at the bench geometry: 2 full K = 64 blocks through the auto pass (and forms 21
+    and 23 explicitly: DPP coefficients, registers / LDS ring; 768-row bands, ld 66048,
+    nt), then an 8-pivot tail (a partial block: coefficients of the unused steps zeroed in
+    memory); the whole tableau against the oracle's digest."""
     tab = load_golden("digests.json")["c3_tableau"]
     _full_blocks_vs_oracle(32768, 32768, 3, 136, 128, 64,
-                           tableau_digest=dict(tab["stops"]["136"], width=tab["width"]))
+                           tableau_digest=dict(tab["stops"]["136"], width=tab["width"]), form=form)
 
 
 def test_c3_k32_lookahead_full_blocks_bit_exact():

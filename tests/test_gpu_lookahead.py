@@ -85,7 +85,8 @@ def test_lookahead_tableau(K, rb, nt, form, ci):
 
 
 @pytest.mark.parametrize("form,rb,nt,ci", [(21, 256, 1, 64), (21, 37, 0, 100), (3, 64, 1, 64), (21, 1000, 1, 30),
-                                            (22, 256, 1, 64), (22, 37, 0, 100)])
+                                            (22, 256, 1, 64), (22, 37, 0, 100), (23, 256, 1, 64), (23, 37, 0, 100),
+                                            (23, 1000, 1, 30), (23, 768, 1, 64)])
 def test_lookahead_k64_tableau(form, rb, nt, ci):
     """K = 64 under lookahead: selections replay up to 127 steps (the sealed block in
     flight + their own), the 128-step ratio kernel; two full blocks and a partial one,
@@ -173,7 +174,7 @@ def test_lookahead_off_for_streamed_form():
     _check(res, ref)
 
 
-@pytest.mark.parametrize("defer,form", [(8, -1), (32, -1), (64, 21), (64, 3), (64, 22)])
+@pytest.mark.parametrize("defer,form", [(8, -1), (32, -1), (64, 21), (64, 3), (64, 22), (64, 23)])
 def test_lookahead_rccl_exchange_single_rank(defer, form):
     """The RCCL path (candidate all-gather, select, MAX all-reduce, commit) with the
     pass on the second stream, as bench.py --gpus N runs it (K = 64: the LEAN

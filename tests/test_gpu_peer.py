@@ -54,7 +54,8 @@ def _peer_ranks(prob, P, **opts):
 
 
 @pytest.mark.parametrize("P,K,form", [(2, 1, -1), (3, 1, -1), (8, 1, -1), (2, 16, -1), (3, 32, -1),
-                                      (4, 16, -1), (8, 16, -1), (2, 64, 21), (4, 64, 21), (8, 64, 21)])
+                                      (4, 16, -1), (8, 16, -1), (2, 64, 21), (4, 64, 21), (8, 64, 21),
+                                      (4, 64, 23), (8, 64, -1)])
 def test_peer_exchange_dense(P, K, form):
     m, n, seed = 150, 170, 4
     A, b, c = O.gen_dense(m, n, seed)
@@ -182,7 +183,7 @@ def test_peer_wait_is_bounded():
 
 def test_c3_row_partition_peer_exchange_one_gpu():
     """BASELINE.json C3 (32768 x 32768) as the 8-GPU split runs it, on ONE MI355X:
-    8 rank sessions (4,096 local rows each; K = 64, form 21, 256-row bands), the
+    8 rank sessions (4,096 local rows each; K = 64, form 23, 256-row bands), the
     exchange through the peer blocks, 160 pivots (two full blocks + a 32-pivot tail),
     against the oracle's committed digests: pivot log, basis, objective and the
     whole tableau."""
@@ -194,7 +195,7 @@ def test_c3_row_partition_peer_exchange_one_gpu():
     sess = [dlp.Session(prob, rank=r, nranks=P, defer=64, check_interval=64) for r in range(P)]
     try:
         for s in sess:
-            assert s.get_defer_tuning()[1:] == (21, 64) and s.get_tuning()[1] == 256
+            assert s.get_defer_tuning()[1:] == (23, 64) and s.get_tuning()[1] == 256
         dlp.Session.connect_peers(sess)
         st, done = dlp.Session.run_ranks(sess, k)
         assert done == k

@@ -1359,38 +1359,53 @@ __device__ __forceinline__ void glds16(const void* g, uint32_t m0) {
 }
 template <int N>
 __device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-template <int D>
+// newer than group g's U DMAs: U per prologue group still to come, 2 U (U stores + U DMAs)
+// per finished group: U (D - 1) + U g while g < D - 1, then 2 U (D - 1)
+template <int D, int U>
 __device__ __forceinline__ void vmwait_group(int g) {
-    // newer than group g's two DMAs: 2 (D - 1 - g) prologue DMAs + 4 per finished group,
-    // 4 (D - 1) in the steady state (2 stores + 2 DMAs per group)
-    if (g >= D - 1) { vmwait<4 * (D - 1)>(); return; }
+    if (g >= D - 1) { vmwait<2 * U * (D - 1)>(); return; }
     switch (g) {
-        case 0: vmwait<2 * (D - 1)>(); break;
-        case 1: vmwait<2 * (D - 1) + 2>(); break;
-        case 2: vmwait<2 * (D - 1) + 4>(); break;
-        case 3: vmwait<2 * (D - 1) + 6>(); break;
-        case 4: vmwait<2 * (D - 1) + 8>(); break;
-        case 5: vmwait<2 * (D - 1) + 10>(); break;
-        default: vmwait<2 * (D - 1) + 12>(); break;
+        case 0: vmwait<U * (D - 1)>(); break;
+        case 1: vmwait<U * (D - 1) + U>(); break;
+        case 2: vmwait<U * (D - 1) + 2 * U>(); break;
+        case 3: vmwait<U * (D - 1) + 3 * U>(); break;
+        case 4: vmwait<U * (D - 1) + 4 * U>(); break;
+        case 5: vmwait<U * (D - 1) + 5 * U>(); break;
+        default: vmwait<U * (D - 1) + 6 * U>(); break;
     }
 }
-template <int L>
-__device__ __forceinline__ void rstep(double (&t)[2], const double (&c)[2][2][2], const double (&pr)[64]) {
-    constexpr int h = L / 32, e = L & 1, n = (L & 31) >> 1;
-    fmac_bc<n>(t[0], c[0][h][e], pr[L]);
-    fmac_bc<n>(t[1], c[1][h][e], pr[L]);
+// step L of a half (coefficients of that half in c[u][even/odd]) for the U rows
+template <int U, int L>
+__device__ __forceinline__ void rstep(double (&t)[U], const double (&c)[U][2], const double (&pr)[64]) {
+    constexpr int e = L & 1, n = (L & 31) >> 1;
+#pragma unroll
+    for (int u = 0; u < U; ++u) fmac_bc<n>(t[u], c[u][e], pr[L]);
 }
-template <int L0, int... I>
-__device__ __forceinline__ void rhalf(double (&t)[2], const double (&c)[2][2][2], const double (&pr)[64],
+template <int U, int L0, int... I>
+__device__ __forceinline__ void rhalf(double (&t)[U], const double (&c)[U][2], const double (&pr)[64],
                                       std::integer_sequence<int, I...>) {
-    (rstep<L0 + I>(t, c, pr), ...);
+    (rstep<U, L0 + I>(t, c, pr), ...);
 }
-template <bool NT, int D, int W>
+// ---- f4r: form 21's compute (P[0..64) of one column per lane in VGPRs, coefficients
+// broadcast by v_fmac_f64_dpp) with the U rows AND their coefficient rows of each group
+// staged per wave in an LDS ring of D groups by LDS-DMA (global_load_lds_dwordx4 from
+// inline asm: the compiler does not count it; the kernel waits with its own counted vmcnt),
+// so D groups of loads are in flight per wave instead of one group in registers.  Ring
+// slot (1 KB per row): U rows x the wave's 64 columns (DMA k: rows 2k, 2k+1; lane l's 16 B
+// = row 2k + l / 32, columns 2 (l % 32) .. +1), then the U rows' 64 coefficients (same
+// layout).  The coefficients of one 32-step half at a time are in registers.
+// MODE 0: the pass; 1: no fmas (the ring's streaming structure alone); 2: no memory in the
+// loop (the first group's slot reused, no stores: the chain's compute alone; wrong values)
+// IL: interleaved row groups instead of bands: workgroup (tile, gi), gi < G = gridDim.y, takes
+// the U-row groups gi, gi + G, gi + 2G, ... of the whole height (P loaded once per
+// workgroup; the resident workgroups' row fronts stay within ~G U rows of each other, as
+// short bands' do)
+template <bool NT, int U, int D, int W, int MODE = 0, bool IL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void f4r_kernel(
     const double* __restrict__ T, double* __restrict__ To, int64_t ld, int64_t rows, int64_t width,
     const double* __restrict__ Cr, const double* __restrict__ P, int rb) {
-    constexpr int K = 64;
-    extern __shared__ double ring[];   // [4 waves][D slots][256 doubles]
+    constexpr int K = 64, SLOT = 128 * U;   // doubles per ring slot
+    extern __shared__ double ring[];   // [4 waves][D slots][SLOT]
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1399,60 +1414,84 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void f
     double pr[K];
 #pragma unroll
     for (int l = 0; l < K; ++l) pr[l] = P[(int64_t)l * ld + jc];
-    const int64_t i0 = (int64_t)blockIdx.y * rb;
-    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    const int G = IL ? (int)gridDim.y : 1, gi = IL ? (int)blockIdx.y : 0;
+    const int64_t i0 = IL ? 0 : (int64_t)blockIdx.y * rb;
+    const int64_t iend = IL ? rows : ((i0 + rb < rows) ? i0 + rb : rows);
     const int nr = (int)(iend - i0);
-    const int ng = nr / 2;   // (the lab's bands have even row counts)
+    // groups of this workgroup (the lab's heights are multiples of U rows)
+    const int ng = IL ? (int)((rows / U - gi + G - 1) / G) : nr / U;
+    auto grow = [&](int g) -> int64_t { return IL ? ((int64_t)gi + (int64_t)G * g) * U : (int64_t)g * U; };
     const int64_t wc = (int64_t)blockIdx.x * 256 + w * 64 + 2 * (lane & 31);
     const int64_t wcc = wc < ld - 1 ? wc : ld - 2;
     const double* tsrc = T + (i0 + (lane >> 5)) * ld + wcc;
     const double* csrc = Cr + (i0 + (lane >> 5)) * K + 2 * (lane & 31);
-    double* wbase = ring + (size_t)w * D * 256;
+    double* wbase = ring + (size_t)w * D * SLOT;
     const uint32_t lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)wbase;
-    // a uniform descriptor (a per-lane one becomes a waterfall loop of stores, which would
-    // break the counted waits); lanes past the width aim out of range and are dropped
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(To + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
     const int voff = colok ? jc * 8 : 0x7fffff00;
     const int rowb = (int)(ld * 8);
     auto dma = [&](int g, int s) {
-        const int gg = g < ng ? g : ng - 1;
-        glds16(tsrc + (int64_t)gg * 2 * ld, __builtin_amdgcn_readfirstlane(lbase + s * 2048));
-        glds16(csrc + (int64_t)gg * 2 * K, __builtin_amdgcn_readfirstlane(lbase + s * 2048 + 1024));
+        const int64_t r = grow(g < ng ? g : ng - 1);
+#pragma unroll
+        for (int k = 0; k < U / 2; ++k)
+            glds16(tsrc + (r + 2 * k) * ld, __builtin_amdgcn_readfirstlane(lbase + s * SLOT * 8 + k * 1024));
+#pragma unroll
+        for (int k = 0; k < U / 2; ++k)
+            glds16(csrc + (r + 2 * k) * K,
+                   __builtin_amdgcn_readfirstlane(lbase + s * SLOT * 8 + U * 512 + k * 1024));
     };
 #pragma unroll
     for (int s = 0; s < D; ++s) dma(s, s);
     int s = 0;
+    if (MODE == 2) vmwait<0>();
     for (int g = 0; g < ng; ++g) {
-        vmwait_group<D>(g);
-        const double* sl = wbase + s * 256;
-        double t[2];
-        t[0] = sl[lane];
-        t[1] = sl[64 + lane];
-        double c[2][2][2];
+        if (MODE != 2) vmwait_group<D, U>(g);   // U DMA instructions per group (U / 2 row pairs, rows + coefficients)
+        const double* sl = wbase + (MODE == 2 ? 0 : s) * SLOT;
+        double t[U];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < U; ++u) t[u] = sl[u * 64 + lane];
+        double c[U][2];
+        auto loadc = [&](int h) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const d2 v = *(const d2*)(sl + 128 + u * 64 + h * 32 + 2 * (lane & 15));
-                c[u][h][0] = v.x;
-                c[u][h][1] = v.y;
+            for (int u = 0; u < U; ++u) {
+                const d2 v = *(const d2*)(sl + U * 64 + u * 64 + h * 32 + 2 * (lane & 15));
+                c[u][0] = v.x;
+                c[u][1] = v.y;
             }
-        rhalf<0>(t, c, pr, std::make_integer_sequence<int, 32>{});
-        rhalf<32>(t, c, pr, std::make_integer_sequence<int, 32>{});
+        };
+        if constexpr (MODE != 1) {
+            loadc(0);
+            rhalf<U, 0>(t, c, pr, std::make_integer_sequence<int, 32>{});
+            loadc(1);
+            rhalf<U, 32>(t, c, pr, std::make_integer_sequence<int, 32>{});
+        }
+        if constexpr (MODE == 2) {
+            if (t[0] == 12345.678) To[0] = t[1];   // keep the chains
+            continue;
+        }
+        // a uniform descriptor per group (a per-lane one becomes a waterfall loop of stores,
+        // which would break the counted waits); lanes past the width aim out of range
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(To + (i0 + grow(g)) * ld), (short)0, (int)((int64_t)U * ld * 8), 0x00020000);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < U; ++u) {
             const double v = t[u];
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), ro, voff, (2 * g + u) * rowb, NT ? 2 : 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), ro, voff, u * rowb, NT ? 2 : 0);
         }
         dma(g + D, s);
         s = s + 1 == D ? 0 : s + 1;
     }
 }
-template <int D, int W>
+template <int U, int D, int W, int MODE = 0, int G = 0, bool NT = true>
 void launch_f4r(const Lab& L, int, int rb, hipStream_t s) {
+    if (G > 0) {   // interleaved: G workgroups per 256-column tile
+        dim3 grid((unsigned)((L.width + 255) / 256), (unsigned)G);
+        f4r_kernel<NT, U, D, W, MODE, true><<<grid, 256, (size_t)4 * D * 1024 * U, s>>>(
+            L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+        return;
+    }
     dim3 grid((unsigned)((L.width + 255) / 256), (unsigned)((L.rows + rb - 1) / rb));
-    f4r_kernel<true, D, W><<<grid, 256, (size_t)4 * D * 2048, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+    f4r_kernel<NT, U, D, W, MODE><<<grid, 256, (size_t)4 * D * 1024 * U, s>>>(L.T, L.To, L.ld, L.rows, L.width,
+                                                                               L.Cr, L.P, rb);
 }
 
 struct Variant {
@@ -1511,13 +1550,12 @@ int main(int argc, char** argv) {
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
     const char* only = argc > 4 ? argv[4] : nullptr;
     std::vector<Variant> vs = {
-        {"f4r K64 D2 w3", 64, 768, launch_f4r<2, 3>, true},
-        {"f4r K64 D3 w3", 64, 768, launch_f4r<3, 3>, true},
-        {"f4r K64 D4 w3", 64, 768, launch_f4r<4, 3>, true},
-        {"f4r K64 D5 w3", 64, 768, launch_f4r<5, 3>, true},
-        {"f4r K64 D6 w3", 64, 768, launch_f4r<6, 3>, true},
-        {"f4r K64 D4 w3 rb256", 64, 256, launch_f4r<4, 3>, true},
-        {"f4r K64 D6 w2", 64, 768, launch_f4r<6, 2>, true},
+        {"f4r K64 U4 D3 w3", 64, 768, launch_f4r<4, 3, 3>, true},
+        {"f4r K64 U4 D3 w3 copy", 64, 768, launch_f4r<4, 3, 3, 1>, false},
+        {"f4r K64 U4 D3 w3 nnt", 64, 768, launch_f4r<4, 3, 3, 0, 0, false>, true},
+        {"f4r K64 U4 D3 w3 rb1536", 64, 1536, launch_f4r<4, 3, 3>, true},
+        {"f4r K64 U2 D4 w3", 64, 768, launch_f4r<2, 4, 3>, true},
+        {"f4q K64 V1U2 w3 rb768", 64, 768, launch_f4q<2, 3>, true},
         {"f4d K32 V2U2 mov", 32, 256, launch_f4d<32, 2, 2, false>, true},
         {"f4d K32 V2U2 asm", 32, 256, launch_f4d<32, 2, 2, true>, true},
         {"f4d K32 V2U4 asm", 32, 256, launch_f4d<32, 2, 4, true>, true},
@@ -1596,7 +1634,12 @@ int main(int argc, char** argv) {
     printf("tableau %ld x %ld (width %ld, ld %ld): %.2f GB\n", (long)rows, (long)ncols, (long)L.width, (long)L.ld,
            rows * L.ld * 8 / 1e9);
     CK(hipMalloc(&L.T, rows * L.ld * 8));
-    L.To = L.T;   // in place, as the product's pass
+    L.To = L.T;   // in place, as the product's pass without lookahead
+    if (getenv("LAB_OOP")) {   // out of place, as the product's pass under lookahead
+        CK(hipMalloc(&L.To, rows * L.ld * 8));
+        CK(hipMemset(L.To, 0, rows * L.ld * 8));
+        printf("out of place\n");
+    }
     CK(hipMalloc(&L.Cr, rows * 128 * 8));
     CK(hipMalloc(&L.P, (int64_t)128 * L.ld * 8));
     fill_kernel<<<4096, 256>>>(L.T, rows * L.ld, 1);
