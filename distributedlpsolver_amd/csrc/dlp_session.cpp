@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -157,6 +158,7 @@ struct dlp_session {
     dlp::Defer dslot[2];
     hipStream_t pstream = nullptr;
     hipEvent_t ev_seal = nullptr, ev_pass = nullptr;
+    int prio_chain = 0, prio_pass = 0;   // the two streams' priorities (stream pool key)
 };
 
 extern "C" int flush_pending(dlp_session* s);   // defined with the C entry points
@@ -164,6 +166,46 @@ extern "C" int flush_pending(dlp_session* s);   // defined with the C entry poin
 namespace {
 
 int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
+
+// Streams are reused across sessions: creating a HIP stream costs ~1.7-2.3 ms and
+// destroying one ~1.6-1.9 ms on MI355X (ROCm 7.2, DLP_TRACE_CREATE), against ~0.05 ms for all
+// of a small session's allocations: C1 (200 x 400, 353 pivots) spent 4 of its 10 ms end to
+// end there (profiles/r03f/).  A freed session's streams (drained without error) go back to a
+// per-(device, priority) pool of at most kStreamPoolMax; a new session takes one from it.
+constexpr size_t kStreamPoolMax = 16;
+struct PooledStream {
+    int device, prio;
+    hipStream_t s;
+};
+std::mutex g_stream_mu;
+std::vector<PooledStream> g_stream_pool;
+
+hipError_t acquire_stream(int device, int prio, hipStream_t* out) {
+    {
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        for (size_t k = g_stream_pool.size(); k-- > 0;)
+            if (g_stream_pool[k].device == device && g_stream_pool[k].prio == prio) {
+                *out = g_stream_pool[k].s;
+                g_stream_pool.erase(g_stream_pool.begin() + (ptrdiff_t)k);
+                return hipSuccess;
+            }
+    }
+    return hipStreamCreateWithPriority(out, hipStreamNonBlocking, prio);
+}
+
+// the caller has set the device; a stream whose work failed is destroyed, not pooled
+void release_stream(int device, int prio, hipStream_t s) {
+    if (!s) return;
+    if (hipStreamSynchronize(s) == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        if (g_stream_pool.size() < kStreamPoolMax) {
+            g_stream_pool.push_back({device, prio, s});
+            return;
+        }
+    }
+    (void)hipGetLastError();
+    (void)hipStreamDestroy(s);
+}
 
 // DLP_TRACE_CREATE=1: milliseconds of each stage of session creation / free on stderr
 // (tools/c1_overhead.py; diagnostics only)
@@ -300,7 +342,7 @@ void free_session(dlp_session* s) {
     }
     if (s->ev_seal) (void)hipEventDestroy(s->ev_seal);
     if (s->ev_pass) (void)hipEventDestroy(s->ev_pass);
-    if (s->pstream) (void)hipStreamDestroy(s->pstream);
+    if (s->pstream) release_stream(s->device, s->prio_pass, s->pstream);
     if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
     for (void* p : s->ipc_open) (void)hipIpcCloseMemHandle(p);
     if (s->xblk) (void)hipFree(s->xblk);
@@ -308,7 +350,7 @@ void free_session(dlp_session* s) {
     if (s->xabort) (void)hipHostFree(s->xabort);
     if (s->host_st) (void)hipHostFree(s->host_st);
     clk.mark("free: buffers");
-    if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->stream) release_stream(s->device, s->prio_chain, s->stream);
     clk.mark("free: stream");
     delete s;
 }
@@ -367,9 +409,13 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     //    row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt stores;
     //  - smaller ones stay partly cache-resident: uncapped, 4-row bands,
     //    default cache policy;
-    //  - rows of >= 4096 doubles are aligned to 4 KiB (whole-tile alignment).
+    //  - rows of >= 4096 doubles are aligned to 4 KiB (whole-tile alignment) for the eager
+    //    update, to 1 KiB for the deferred pass of a streaming tableau (C3 ld 65,664 vs
+    //    66,048: 7,716-7,737 vs 7,620-7,632 pivots/s, alternating runs on one box; the
+    //    LDS-ring copy probe 6.2 vs 7.0 ms: profiles/r03g/)
     const bool streaming = (double)(s->rows + 1) * (double)s->width * 8.0 > (double)(1ll << 30);
-    if (s->opt.ld_align <= 0) s->opt.ld_align = s->width >= 4096 ? 512 : 16;
+    if (s->opt.ld_align <= 0)
+        s->opt.ld_align = s->width >= 4096 ? ((streaming && s->opt.defer != 1) ? 128 : 512) : 16;
     if (s->opt.update_variant < 0) s->opt.update_variant = streaming ? 22 : 26;
     if (s->opt.nontemporal < 0) s->opt.nontemporal = streaming ? 1 : 0;
     s->streaming = streaming;
@@ -401,7 +447,9 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     // launches share the device with the pass (pstream, lowest priority)
     int prio_least = 0, prio_greatest = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
-    HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_greatest));
+    s->prio_chain = prio_greatest;
+    s->prio_pass = prio_least;
+    HIP_TRY(acquire_stream(s->device, prio_greatest, &s->stream));
     clk.mark("create: stream");
 
     const int64_t rows_total = s->rows + 1;
@@ -617,7 +665,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
             HIP_TRY(hipMemsetAsync(d1.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
             HIP_TRY(hipMemsetAsync(d1.Cc, 0, sizeof(double) * s->d.K * s->d.ldcc, s->stream));
             HIP_TRY(hipMemsetAsync(d1.P, 0, sizeof(double) * kt * s->ld, s->stream));
-            HIP_TRY(hipStreamCreateWithPriority(&s->pstream, hipStreamNonBlocking, prio_least));
+            HIP_TRY(acquire_stream(s->device, prio_least, &s->pstream));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_seal, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_pass, hipEventDisableTiming));
             HIP_TRY(hipStreamSynchronize(s->stream));

@@ -131,7 +131,8 @@ typedef struct dlp_options {
     int32_t use_graph;       /* replay each poll window as a hipGraph (default 1) */
     int32_t update_variant;  /* rank-1 kernel variant 0..dlp_update_variants()-1, -1 = auto (default) */
     int32_t ld_align;        /* tableau row stride alignment in doubles, multiple of 16, 0 = auto
-                                (default: 512 when a row has >= 4096 columns, else 16); the
+                                (default: when a row has >= 4096 columns, 128 for a deferred
+                                session on a tableau > 1 GiB and 512 otherwise; else 16); the
                                 kernels only touch the first roundup(N+1,16) columns */
     int32_t small_lp;        /* one-launch LDS solve for small LPs (dlp_cluster.hip): 0 = auto
                                 (default: single-rank dense / random / ad-allocation problems

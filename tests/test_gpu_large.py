@@ -125,7 +125,7 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0, tableau_digest=No
 @pytest.mark.parametrize("form", [None, 21, 23])
 def test_c3_full_blocks_bit_exact(form):
     """C3 at the bench geometry: 2 full K = 64 blocks through the auto pass (and forms 21
-    and 23 explicitly: DPP coefficients, registers / LDS ring; 768-row bands, ld 66048,
+    and 23 explicitly: DPP coefficients, registers / LDS ring; 768-row bands, ld 65664,
     nt), then an 8-pivot tail (a partial block: coefficients of the unused steps zeroed in
     memory); the whole tableau against the oracle's digest."""
     tab = load_golden("digests.json")["c3_tableau"]
