@@ -64,6 +64,22 @@ __device__ inline void stv(double* p, d2 v) {
         *(d2*)p = v;
 }
 
+// 16-B LDS-DMA (global_load_lds_dwordx4: lane x's 16 bytes land at the wave-uniform LDS
+// address m0 + 16 x) issued from inline asm, so that hipcc does not count it: with the
+// builtin it waits vmcnt(0) before the next LDS read or ordinary-load use, draining every
+// DMA in flight (cdna_hip_programming.md, glds).  The callers retire their DMAs with counted
+// waits of their own (vmwait), which hold because between two of them they issue no other
+// vector-memory instruction, or a fixed number of them.  The lgkmcnt(0) orders the DMA's
+// LDS write after this wave's earlier LDS reads of the slot it refills.
+__device__ __forceinline__ void glds16(const void* g, uint32_t m0) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p);
+}
+
 // a1 + a2 (+ a4 single rank) on the replayed column q.  Pricing as in the
 // eager ratio_kernel.  Lane i: a = T_j[i][q] by replaying steps 0..j-1 on
 // T0[i][q]; C[j][i] = a; the RHS cache advances by step j-1 (or is read from
@@ -90,6 +106,18 @@ __device__ inline void release_go(DevState* st) {
     __hip_atomic_store(&st->go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Diagnostics (DLP_CHAIN_STAMPS=<file>, never set in a timed run): wall-clock stamps (100 MHz)
+// of the phases of the lookahead chain kernels, one row per pivot (mod 64): ratio kernel
+// workgroup 0 at start / q known / T0 and P[l][q] in / replay done / block reduce done /
+// ticket taken, the last workgroup at its end; the pivot-row kernel's workgroup 0 at start /
+// step table in / replay done / end.  Written by one lane; dumped by the session at free.
+__device__ uint64_t g_chain_stamps[64][16];
+__device__ int g_chain_stamps_on;
+#define CHAIN_STAMP(slot, k)                                                                  \
+    do {                                                                                      \
+        if (g_chain_stamps_on && threadIdx.x == 0) g_chain_stamps[(slot) & 63][k] = wall_clock64(); \
+    } while (0)
+
 // Block reductions through an LDS tree (LEAN kernels: fewer VGPRs than the wave shuffles of
 // block_cand / block_price).  Both orders are total, so the winner is the same.
 template <typename T, typename Better>
@@ -113,6 +141,11 @@ __device__ inline T block_tree(T v, T* s, Better better) {
 // the 32 VGPRs per SIMD that three pass waves (3 x 160) leave free.  Same operations in
 // the same order.  (Staging the chain in LDS by LDS-DMA, 32 steps per round trip, measured
 // no faster beside the pass: 96 vs 95 us per selection, profiles/r02j/.)
+// LEAN, LCH = 0: the coefficient chain streams through a per-wave LDS ring by LDS-DMA, two
+// steps per DMA, kRatioRingPairs DMAs in flight (launch-time LDS, kRatioRing bytes: see
+// kProwRing).
+constexpr int kRatioRingPairs = 8;
+constexpr size_t kRatioRing = (kRatioDeferThreads / 64) * kRatioRingPairs * 128 * sizeof(double);
 template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4>
 __device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
@@ -137,6 +170,8 @@ __device__ __forceinline__ void ratio_defer_body(
             return block_cand(v, lds_c);
     };
     if (st->status != DLP_RUNNING) return;
+    const int64_t slot = st->npivots;
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 0);
 
     // replayed steps: the sealed previous block (lookahead: not yet applied to T, its kp
     // steps first), then this block's j steps; C / Cc / nzc are written at index j
@@ -148,6 +183,28 @@ __device__ __forceinline__ void ratio_defer_body(
         s_pn[l] = l < kp ? Pp[(int64_t)l * ld + ncols] : P[(int64_t)(l - kp) * ld + ncols];
         s_pl[l] = l < kp ? st->seal[prev_seal].pl[l] : st->pl[l - kp];
     }
+    // ring: lanes 0-31 of a DMA bring step 2p, lanes 32-63 step 2p+1, 16 B = two rows each,
+    // so the ring slot holds the wave's 64 rows of both steps; Cc does not depend on q, so the
+    // first DMAs are issued here and land during the pricing reduce.  Steps past J-1 re-read
+    // step J-1 (harmless), so every pair issues exactly one DMA.
+    constexpr bool RING = LEAN && LCH == 0;
+    extern __shared__ double s_dyn[];
+    const int wl = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + wv * 64;
+    const bool wave_rows = i0 < rows;   // (i0 + 63 < ldcc = round64(rows + 1))
+    auto ring_at = [&](int p) { return s_dyn + (wv * kRatioRingPairs + p % kRatioRingPairs) * 128; };
+    auto sbase = [&](int l) -> const double* {   // wave-uniform: step l's row i0 (l clamped)
+        l = l < J ? l : J - 1;
+        return (l < kp ? Ccp + (int64_t)l * ldcc : Cc + (int64_t)(l - kp) * ldcc) + i0;
+    };
+    auto csrc = [&](int p) -> const double* {
+        return ((wl >> 5) ? sbase(2 * p + 1) : sbase(2 * p)) + 2 * (wl & 31);
+    };
+    if constexpr (RING)
+        if (wave_rows && J > 0)
+#pragma unroll
+            for (int p = 0; p < kRatioRingPairs; ++p) glds16(csrc(p), lds_addr(ring_at(p)));
     const int64_t ic = i < rows ? i : rows;   // clamped: loads need no guard
     double f[LEAN ? 1 : KMAX];
     if constexpr (!LEAN) {
@@ -189,6 +246,7 @@ __device__ __forceinline__ void ratio_defer_body(
     else
         q = (acc.jmin != kNoIndex && acc.zmin < -tol_dj) ? acc.jmin : kNoIndex;
     if (q == kNoIndex) {
+        if constexpr (RING) vmwait<0>();   // no DMA into LDS outlives the wave
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->q = -1;
             st->status = DLP_OK;
@@ -197,15 +255,40 @@ __device__ __forceinline__ void ratio_defer_body(
         return;
     }
 
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 1);
     // T0[i][q] is requested before the P[l][q] loads and their barrier: both wait only for q
     double a = i <= rows ? T[i * ld + q] : 0.0;
     for (int l = threadIdx.x; l < J; l += blockDim.x)
         s_pq[l] = l < kp ? Pp[(int64_t)l * ld + q] : P[(int64_t)(l - kp) * ld + q];
     __syncthreads();
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 2);
 
     Cand c = cand_empty();
     double flast = 0.0;   // LEAN: C of step J-1 (the RHS cache's step)
-    if constexpr (LEAN) {
+    if constexpr (RING) {
+        auto step = [&](int l, double fv) {
+            if (i < rows) {
+                if (i == s_pl[l])
+                    a = s_pq[l];
+                else if (fv != 0.0)
+                    a = __builtin_fma(-fv, s_pq[l], a);
+            }
+            flast = fv;
+        };
+        if (wave_rows) {
+            const int npairs = (J + 1) >> 1;
+            for (int p = 0; p < npairs; ++p) {
+                vmwait<kRatioRingPairs - 1>();   // pair p landed: only ring DMAs issue in this loop
+                double* rs = ring_at(p);
+                const double f0 = rs[wl], f1 = rs[64 + wl];
+                step(2 * p, f0);
+                if (2 * p + 1 < J) step(2 * p + 1, f1);
+                glds16(csrc(p + kRatioRingPairs), lds_addr(rs));
+            }
+            vmwait<0>();
+        }
+        if (blockIdx.x == 0) CHAIN_STAMP(slot, 3);
+    } else if constexpr (LEAN) {
         // LCH coefficient loads per round trip (the register budget of this kernel)
         if (i < rows)
             for (int l0 = 0; l0 < J; l0 += LCH) {
@@ -225,6 +308,7 @@ __device__ __forceinline__ void ratio_defer_body(
                     }
                 }
             }
+        if (blockIdx.x == 0) CHAIN_STAMP(slot, 3);
     }
     if (i <= rows) {
         if (i < rows) {
@@ -277,6 +361,7 @@ __device__ __forceinline__ void ratio_defer_body(
         }
     }
     c = cand_red(c);
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 4);
 
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)partials, (short)0, (int)(nblocks * sizeof(Cand)), 0x00020000);
@@ -291,6 +376,7 @@ __device__ __forceinline__ void ratio_defer_body(
         s_last = (prev == (unsigned)nblocks - 1);
     }
     __syncthreads();
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 5);
     if (!s_last) return;
     Cand best = cand_empty();
     for (int k = threadIdx.x; k < nblocks; k += blockDim.x) {
@@ -315,6 +401,7 @@ __device__ __forceinline__ void ratio_defer_body(
             release_go(st);
         }
     }
+    if constexpr (LEAN) CHAIN_STAMP(slot, 6);
 }
 
 template <int KMAX>
@@ -388,8 +475,10 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
 // T0[p], divided by the pivot element (IEEE division).  fused (single rank):
 // commit_row as well.  Otherwise the owner writes the fp64 bits and every
 // other rank INT64_MIN for the int64 MAX exchange.
-template <bool LEAN = false>
-__global__ __launch_bounds__(256) void prow_defer_kernel(
+constexpr int kProwRingSteps = 16;
+constexpr size_t kProwRing = 4 * kProwRingSteps * 128 * sizeof(double);
+template <bool LEAN>
+__device__ __forceinline__ void prow_defer_body(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
     int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
@@ -398,13 +487,36 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     __shared__ PricePart lds_pp[4];
     __shared__ double s_cp[kMaxReplay];
     __shared__ int32_t s_pl[kMaxReplay];
+    // LEAN: the replayed pivot rows stream through a per-wave LDS ring by LDS-DMA, RING steps
+    // in flight (each lane's own 16 B of a row land at ring + 16 lane), instead of 4 rows per
+    // round trip in the 32 VGPRs this kernel has beside the pass
+    // (launch-time LDS, kProwRing bytes: static LDS of that size makes hipcc's descriptor ask for
+    // the VGPRs its LDS-bound occupancy would leave, 176, and the kernel no longer fits beside
+    // the pass)
+    constexpr int RING = kProwRingSteps;
+    extern __shared__ double s_dyn[];
+    auto s_ring = reinterpret_cast<double(*)[RING][128]>(s_dyn);
     if (st->status != DLP_RUNNING) return;
+    const int64_t slot = st->npivots - 1;
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 8);
     const int s = st->blk - 1;
     // replayed steps: the sealed previous block first (lookahead), then this block's s
     const int kp = prev_seal >= 0 ? st->seal[prev_seal].blk : 0;
     const int S = kp + s;
     const int32_t pl = st->p_local;
     const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    const bool owner_lane = pl >= 0 && j < ld;
+    // the ring's first RING rows are requested first (they depend on nothing but the step
+    // counts); rows past the last step re-read it (harmless), so every step issues one DMA
+    auto psrc = [&](int l) -> const double* {
+        l = l < S ? l : S - 1;
+        return (l < kp ? Pp + (int64_t)l * ld : P + (int64_t)(l - kp) * ld) + j;
+    };
+    const int wv = threadIdx.x >> 6, wl = threadIdx.x & 63;
+    if constexpr (LEAN)
+        if (owner_lane && S > 0)
+#pragma unroll
+            for (int r = 0; r < RING; ++r) glds16(psrc(r), lds_addr(&s_ring[wv][r][0]));
     // everything that depends only on (p, s) is requested before the step-table barrier:
     // T0[p][j..j+1] and, for the fused commit, the objective row and z_q
     d2 t0 = d2{0.0, 0.0}, zpre = d2{0.0, 0.0};
@@ -420,14 +532,33 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
             s_pl[l] = l < kp ? st->seal[prev_seal].pl[l] : st->pl[l - kp];
         }
     __syncthreads();
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 9);
     d2 pr;
     pr.x = 0.0;
     pr.y = 0.0;
-    if (pl >= 0 && j < ld) {
+    if (owner_lane && LEAN) {
+        d2 t = t0;
+        asm volatile("" ::"v"(t.x), "v"(t.y));   // T0[p] in here (hipcc's own wait), not in the loop
+        for (int l = 0; l < S; ++l) {
+            vmwait<RING - 1>();   // step l's DMA retired: only ring DMAs issue in this loop
+            const d2 pv = *(const d2*)&s_ring[wv][l % RING][2 * wl];
+            if (pl == s_pl[l]) {
+                t = pv;
+            } else if (s_cp[l] != 0.0) {
+                t.x = __builtin_fma(-s_cp[l], pv.x, t.x);
+                t.y = __builtin_fma(-s_cp[l], pv.y, t.y);
+            }
+            glds16(psrc(l + RING), lds_addr(&s_ring[wv][l % RING][0]));
+        }
+        vmwait<0>();   // the ring drained (the clamped tail DMAs) before the block exits
+        const double piv = st->piv;
+        pr.x = t.x / piv;
+        pr.y = t.y / piv;
+    } else if (owner_lane) {
         d2 t = t0;
         // chunks of CH pivot rows: loads issued back to back (row index clamped), then applied
-        // in order (LEAN, lookahead beside the form-21 pass: 2 rows, 21 VGPRs)
-        constexpr int CH = LEAN ? 4 : 8;
+        // in order
+        constexpr int CH = 8;
         for (int l0 = 0; l0 < S; l0 += CH) {
             d2 pv[CH];
 #pragma unroll
@@ -452,6 +583,7 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
         pr.x = t.x / piv;
         pr.y = t.y / piv;
     }
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 10);
     if (!fused && xp) {   // peer exchange: the owner's row into every rank's row region
         // (scalars first: hipcc of ROCm 7.2 compiles __builtin_bit_cast(T, v.y) of an
         // ext_vector element as a cast of element 0; tests/test_isa.py guards this site)
@@ -474,7 +606,30 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(
     }
     commit_row<!LEAN>(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
                       lds_pp, zpre, zqpre);
+    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 11);
 }
+#define DLP_PROW_ARGS                                                                              \
+    double *__restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice, const DevState *st, \
+        const double *__restrict__ C, int64_t ldc, double *__restrict__ P, int64_t *__restrict__ bits,  \
+        PricePart *pp, double tol_dj, dlp_pivot *log, int64_t log_cap, int fused,                    \
+        const double *__restrict__ Cp, const double *__restrict__ Pp, int prev_seal, const XPeers *xp, \
+        uint32_t xseq
+#define DLP_PROW_PASS T, ld, rows, ncols, nprice, st, C, ldc, P, bits, pp, tol_dj, log, log_cap, fused, Cp, Pp, \
+                      prev_seal, xp, xseq
+// The LEAN instance (lookahead at K = 64, beside the form-21 pass) is held to 32 VGPRs in its
+// kernel descriptor: the pass leaves 32 per SIMD (with the LDS-DMA asm, hipcc's descriptor
+// otherwise requested 176 for a body that uses 30, and the kernel could not share a CU).
+template <bool LEAN = false>
+__global__ __launch_bounds__(256) void prow_defer_kernel(DLP_PROW_ARGS) {
+    prow_defer_body<false>(DLP_PROW_PASS);
+}
+template <>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void prow_defer_kernel<true>(
+    DLP_PROW_ARGS) {
+    prow_defer_body<true>(DLP_PROW_PASS);
+}
+#undef DLP_PROW_ARGS
+#undef DLP_PROW_PASS
 
 // Multi-rank: P[s] from the exchanged bits, then the objective row + pricing.
 __global__ __launch_bounds__(256) void commit_defer_kernel(
@@ -1569,11 +1724,6 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
 // U rows are all dense run the chains from LDS; any other group replays row by row
 // (replay_row: T and the coefficients from the slot, P from the registers).  Lab:
 // 7.3-7.5 ms per C3 pass against form 21's 8.2-8.5 (tools/passlab.hip f4r, bit-exact).
-__device__ __forceinline__ void glds16(const void* g, uint32_t m0) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 // newer than group g's U DMAs: U per prologue group still to come and 2 U (U stores + U
 // DMAs) per finished group: U (D - 1) + U g while g < D - 1, then 2 U (D - 1)
 template <int D, int U>
@@ -1929,15 +2079,17 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     else   // lookahead at K = 64, beside the form-21 pass
     {
         static const int lch = std::getenv("DLP_LEAN_LCH") ? std::atoi(std::getenv("DLP_LEAN_LCH")) : 4;
-#define DLP_RATIO_LEAN(L)                                                                                  \
-    ratio_lean_kernel<128, L><<<nblocks, kRatioDeferThreads, 0, s>>>(                                       \
+#define DLP_RATIO_LEAN(L, DYN)                                                                             \
+    ratio_lean_kernel<128, L><<<nblocks, kRatioDeferThreads, DYN, s>>>(                                       \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
         d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
         xp, xseq)
         if (lch == 8)   // tuning only (DLP_LEAN_LCH)
-            DLP_RATIO_LEAN(8);
+            DLP_RATIO_LEAN(8, 0);
+        else if (lch == 0)
+            DLP_RATIO_LEAN(0, kRatioRing);
         else
-            DLP_RATIO_LEAN(4);
+            DLP_RATIO_LEAN(4, 0);
 #undef DLP_RATIO_LEAN
     }
 #undef DLP_RATIO_DEFER
@@ -1981,7 +2133,7 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     if (prev_seal >= 0 && d.K > 32)   // lookahead at K = 64: beside the form-21 pass
-        prow_defer_kernel<true><<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
+        prow_defer_kernel<true><<<blocks, 256, kProwRing, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
                                                      d.P, prow_bits, pp, tol_dj, log, log_cap,
                                                      nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal,
                                                      nranks == 1 ? nullptr : xp, xseq);
@@ -2211,6 +2363,14 @@ hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, b
         return hipErrorInvalidValue;
     return nontemporal ? pass_k<true>(g, d, st, rows_per_block, occupancy, s, Tout, seal)
                        : pass_k<false>(g, d, st, rows_per_block, occupancy, s, Tout, seal);
+}
+
+hipError_t chain_stamps_enable() {
+    const int on = 1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_chain_stamps_on), &on, sizeof(on));
+}
+hipError_t chain_stamps_dump(uint64_t* host64x16) {
+    return hipMemcpyFromSymbol(host64x16, HIP_SYMBOL(g_chain_stamps), sizeof(uint64_t) * 64 * 16);
 }
 
 hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s) {

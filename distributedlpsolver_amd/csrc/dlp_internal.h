@@ -234,6 +234,9 @@ hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, b
                               int rows_per_block, int occupancy, hipStream_t s,
                               double* Tout = nullptr, int seal = -1);
 bool lookahead_form(int form);
+// Diagnostics (DLP_CHAIN_STAMPS): phase stamps of the LEAN chain kernels (dlp_defer.hip).
+hipError_t chain_stamps_enable();
+hipError_t chain_stamps_dump(uint64_t* host64x16);
 // End of a lookahead block: st->seal[slot] := (blk, pl), blk := 0.
 hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s);
 hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits, int nranks,

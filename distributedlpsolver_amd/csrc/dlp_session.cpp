@@ -325,6 +325,15 @@ void free_session(dlp_session* s) {
     if (s->device >= 0) (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     clk.mark("free: sync");
+    // diagnostics: DLP_CHAIN_STAMPS=<file> dumps the chain kernels' phase stamps (tools only)
+    if (const char* path = std::getenv("DLP_CHAIN_STAMPS")) {
+        std::vector<uint64_t> h(64 * 16, 0);
+        if (dlp::chain_stamps_dump(h.data()) == hipSuccess)
+            if (FILE* f = std::fopen(path, "wb")) {
+                std::fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+                std::fclose(f);
+            }
+    }
     if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
     if (s->graph) (void)hipGraphDestroy(s->graph);
     for (auto e : s->ev) (void)hipEventDestroy(e);
@@ -443,6 +452,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     if (s->device < 0 || s->device >= ndev) { set_error("device ordinal out of range"); return DLP_ERR_ARG; }
     StageClock clk;
     HIP_TRY(hipSetDevice(s->device));
+    if (std::getenv("DLP_CHAIN_STAMPS")) HIP_TRY(dlp::chain_stamps_enable());   // diagnostics
     // the pivot chain runs at the highest stream priority: under lookahead its small
     // launches share the device with the pass (pstream, lowest priority)
     int prio_least = 0, prio_greatest = 0;

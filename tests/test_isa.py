@@ -84,8 +84,18 @@ def test_fused_dpp_fma_has_no_valu_write_hazard():
     assert n_dpp >= 512, n_dpp
 
 
+def _readelf(d, f, *args):
+    return subprocess.run([os.path.join(LLVM, "llvm-readelf"), *args, f], cwd=d, check=True,
+                          capture_output=True, text=True).stdout
+
+
 def _vgpr_counts():
-    """{kernel symbol: .vgpr_count} from the AMDGPU metadata notes of the bundled code objects."""
+    """{kernel symbol: VGPRs per lane} of the bundled code objects, as the hardware allocates them.
+
+    Both the metadata note (.vgpr_count) and the kernel descriptor (<kernel>.kd: 64 bytes, the
+    granulated count in compute_pgm_rsrc1 bits 5:0, granules of 8 VGPRs on gfx950) are read and
+    the larger kept: hipcc can write a descriptor far above the note (a kernel with 64 KB of
+    static LDS got 176 for a body of 30 VGPRs), and the descriptor is what the CU allocates."""
     if not os.path.exists(SO) or not os.path.exists(os.path.join(LLVM, "llvm-readelf")):
         pytest.skip("libdlp.so or llvm-readelf missing")
     d = tempfile.mkdtemp()
@@ -96,14 +106,26 @@ def _vgpr_counts():
         counts, name = {}, None
         for f in sorted(os.listdir(d)):
             if "amdgcn" in f and "gfx950" in f:
-                r = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", f], cwd=d, check=True,
-                                   capture_output=True, text=True)
-                for line in r.stdout.splitlines():
+                for line in _readelf(d, f, "--notes").splitlines():
                     line = line.strip()
                     if line.startswith(".name:"):
                         name = line.split(":", 1)[1].strip()
                     elif line.startswith(".vgpr_count:") and name:
                         counts[name] = int(line.split(":", 1)[1])
+                secs = []   # (addr, offset, size) of every section
+                for line in _readelf(d, f, "-S", "--wide").splitlines():
+                    m = re.match(r"\s*\[\s*\d+\]\s+\S+\s+\S+\s+([0-9a-f]+)\s+([0-9a-f]+)\s+([0-9a-f]+)", line)
+                    if m:
+                        secs.append(tuple(int(x, 16) for x in m.groups()))
+                blob = open(os.path.join(d, f), "rb").read()
+                for line in _readelf(d, f, "-s", "--wide").splitlines():
+                    p = line.split()
+                    if len(p) >= 8 and p[7].endswith(".kd"):
+                        addr = int(p[1], 16)
+                        off = next(o + addr - a for a, o, n in secs if a <= addr < a + n)
+                        rsrc1 = int.from_bytes(blob[off + 48:off + 52], "little")
+                        k = p[7][:-3]
+                        counts[k] = max(counts.get(k, 0), ((rsrc1 & 63) + 1) * 8)
         return counts
     finally:
         shutil.rmtree(d, ignore_errors=True)

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Phase times of the lookahead selection chain beside the pass.
+
+    python tools/chain_stamps.py [bench args...]
+
+Runs bench.py (C3 default, short) with DLP_CHAIN_STAMPS set, then reads the 64 x 16 stamps
+(100 MHz wall clock) the LEAN kernels wrote for the last 64 pivots: ratio kernel workgroup 0
+at start / q known / T0 and P[l][q] in / replay done / block reduce done / ticket taken, the
+last workgroup at its end; the pivot-row kernel at start / step table in / replay done / end."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+path = os.path.join(ROOT, "gpurun_out", "chain_stamps.bin")
+env = dict(os.environ, DLP_CHAIN_STAMPS=path)
+cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-eager-window",
+       "--no-pivot-window", "--steps", "3", "--warmup", "2"] + sys.argv[1:]
+out = subprocess.run(cmd, env=env, check=True, capture_output=True, text=True).stdout
+line = json.loads(out.strip().splitlines()[-1])
+st = np.fromfile(path, dtype=np.uint64).reshape(64, 16).astype(np.float64) / 100.0   # µs
+ok = (st[:, [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11]] > 0).all(axis=1)
+st = st[ok]
+names = ["ratio: pricing reduce (start -> q)", "ratio: T0[i][q] + P[l][q] in", "ratio: replay (lane 0)",
+         "ratio: block reduce", "ratio: partials + ticket", "ratio: last workgroup select (ticket -> end)",
+         "gap ratio end -> prow start", "prow: step table + T0[p] in", "prow: replay + divide",
+         "prow: commit (P, objective row, pricing)"]
+pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 8), (8, 9), (9, 10), (10, 11)]
+res = {n: float(np.median(st[:, b] - st[:, a])) for n, (a, b) in zip(names, pairs)}
+res["ratio total (start -> end)"] = float(np.median(st[:, 6] - st[:, 0]))
+res["prow total"] = float(np.median(st[:, 11] - st[:, 8]))
+print(json.dumps({"pivots_sampled": int(ok.sum()), "bench_value": line["value"],
+                  "pass_ms": line["roofline"]["launch_ms"], "median_us": res}, indent=1))
