@@ -155,7 +155,7 @@ __device__ __forceinline__ void ratio_defer_body(
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, int nblocks, const double* __restrict__ Ccp = nullptr,
     const double* __restrict__ Pp = nullptr, int prev_seal = -1, const XPeers* xp = nullptr,
-    uint32_t xseq = 0) {
+    uint32_t xseq = 0, uint32_t* bcnt = nullptr, int brb = 1, int bnt = 0, const double* Tn = nullptr) {
     __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
     __shared__ Cand lds_c[kRatioDeferThreads / 64];
     __shared__ int s_last;
@@ -193,16 +193,27 @@ __device__ __forceinline__ void ratio_defer_body(
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + wv * 64;
     const bool wave_rows = i0 < rows;   // (i0 + 63 < ldcc = round64(rows + 1))
+    // band publication (RING): the wave's 64 rows final in Tn (their bands of the sealed
+    // block's pass are done): start there and replay this block's steps only
+    bool wdone = false;
+    if constexpr (RING)
+        if (bcnt && kp > 0 && i0 + 63 < rows) {
+            const int64_t b0 = i0 / brb, b1 = (i0 + 63) / brb;
+            const uint32_t c0 = __hip_atomic_load(&bcnt[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t c1 = b1 == b0 ? c0 : __hip_atomic_load(&bcnt[b1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wdone = __builtin_amdgcn_readfirstlane(c0 == (uint32_t)bnt && c1 == (uint32_t)bnt ? 1 : 0) != 0;
+        }
+    const int L0 = wdone ? kp : 0;
     auto ring_at = [&](int p) { return s_dyn + (wv * kRatioRingPairs + p % kRatioRingPairs) * 128; };
     auto sbase = [&](int l) -> const double* {   // wave-uniform: step l's row i0 (l clamped)
         l = l < J ? l : J - 1;
         return (l < kp ? Ccp + (int64_t)l * ldcc : Cc + (int64_t)(l - kp) * ldcc) + i0;
     };
     auto csrc = [&](int p) -> const double* {
-        return ((wl >> 5) ? sbase(2 * p + 1) : sbase(2 * p)) + 2 * (wl & 31);
+        return ((wl >> 5) ? sbase(L0 + 2 * p + 1) : sbase(L0 + 2 * p)) + 2 * (wl & 31);
     };
     if constexpr (RING)
-        if (wave_rows && J > 0)
+        if (wave_rows && J > L0)
 #pragma unroll
             for (int p = 0; p < kRatioRingPairs; ++p) glds16(csrc(p), lds_addr(ring_at(p)));
     const int64_t ic = i < rows ? i : rows;   // clamped: loads need no guard
@@ -257,7 +268,12 @@ __device__ __forceinline__ void ratio_defer_body(
 
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 1);
     // T0[i][q] is requested before the P[l][q] loads and their barrier: both wait only for q
-    double a = i <= rows ? T[i * ld + q] : 0.0;
+    double a = 0.0;
+    if (wdone)   // sc1 load (the pass stored Tn write-through)
+        a = __builtin_bit_cast(double, __hip_atomic_load((const uint64_t*)(Tn + i * ld + q), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT));
+    else if (i <= rows)
+        a = T[i * ld + q];
     for (int l = threadIdx.x; l < J; l += blockDim.x)
         s_pq[l] = l < kp ? Pp[(int64_t)l * ld + q] : P[(int64_t)(l - kp) * ld + q];
     __syncthreads();
@@ -276,16 +292,19 @@ __device__ __forceinline__ void ratio_defer_body(
             flast = fv;
         };
         if (wave_rows) {
-            const int npairs = (J + 1) >> 1;
+            const int npairs = (J - L0 + 1) >> 1;
             for (int p = 0; p < npairs; ++p) {
                 vmwait<kRatioRingPairs - 1>();   // pair p landed: only ring DMAs issue in this loop
                 double* rs = ring_at(p);
                 const double f0 = rs[wl], f1 = rs[64 + wl];
-                step(2 * p, f0);
-                if (2 * p + 1 < J) step(2 * p + 1, f1);
+                step(L0 + 2 * p, f0);
+                if (L0 + 2 * p + 1 < J) step(L0 + 2 * p + 1, f1);
                 glds16(csrc(p + kRatioRingPairs), lds_addr(rs));
             }
             vmwait<0>();
+            // no step replayed (first selection of a block on a finished band): the RHS cache
+            // still advances by the sealed block's last step
+            if (npairs == 0 && J > 0) flast = Ccp[(int64_t)(kp - 1) * ldcc + i];
         }
         if (blockIdx.x == 0) CHAIN_STAMP(slot, 3);
     } else if constexpr (LEAN) {
@@ -428,11 +447,11 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
-    int prev_seal, const XPeers* xp, uint32_t xseq) {
+    int prev_seal, const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn) {
     ratio_defer_body<KMAX, false, true, LCH>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                         ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                         tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
-                                        xp, xseq);
+                                        xp, xseq, bcnt, brb, bnt, Tn);
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
@@ -475,7 +494,7 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
 // T0[p], divided by the pivot element (IEEE division).  fused (single rank):
 // commit_row as well.  Otherwise the owner writes the fp64 bits and every
 // other rank INT64_MIN for the int64 MAX exchange.
-constexpr int kProwRingSteps = 16;
+constexpr int kProwRingSteps = 8;
 constexpr size_t kProwRing = 4 * kProwRingSteps * 128 * sizeof(double);
 template <bool LEAN>
 __device__ __forceinline__ void prow_defer_body(
@@ -483,7 +502,7 @@ __device__ __forceinline__ void prow_defer_body(
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
     int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
     int fused, const double* __restrict__ Cp, const double* __restrict__ Pp, int prev_seal,
-    const XPeers* xp, uint32_t xseq) {
+    const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn) {
     __shared__ PricePart lds_pp[4];
     __shared__ double s_cp[kMaxReplay];
     __shared__ int32_t s_pl[kMaxReplay];
@@ -506,6 +525,14 @@ __device__ __forceinline__ void prow_defer_body(
     const int32_t pl = st->p_local;
     const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
     const bool owner_lane = pl >= 0 && j < ld;
+    // LEAN, band publication: row p final in Tn (its band of the sealed block's pass is done):
+    // start there and replay this block's steps only
+    bool pdone = false;
+    if constexpr (LEAN)
+        if (bcnt && kp > 0 && pl >= 0)
+            pdone = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(&bcnt[pl / brb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == (uint32_t)bnt;
+    const int L0 = pdone ? kp : 0;
     // the ring's first RING rows are requested first (they depend on nothing but the step
     // counts); rows past the last step re-read it (harmless), so every step issues one DMA
     auto psrc = [&](int l) -> const double* {
@@ -514,14 +541,22 @@ __device__ __forceinline__ void prow_defer_body(
     };
     const int wv = threadIdx.x >> 6, wl = threadIdx.x & 63;
     if constexpr (LEAN)
-        if (owner_lane && S > 0)
+        if (owner_lane && S > L0)
 #pragma unroll
-            for (int r = 0; r < RING; ++r) glds16(psrc(r), lds_addr(&s_ring[wv][r][0]));
+            for (int r = 0; r < RING; ++r) glds16(psrc(L0 + r), lds_addr(&s_ring[wv][(L0 + r) % RING][0]));
     // everything that depends only on (p, s) is requested before the step-table barrier:
     // T0[p][j..j+1] and, for the fused commit, the objective row and z_q
     d2 t0 = d2{0.0, 0.0}, zpre = d2{0.0, 0.0};
     double zqpre = 0.0;
-    if (pl >= 0 && j < ld) t0 = *(const d2*)(T + (int64_t)pl * ld + j);
+    if (pdone && j < ld) {   // sc1 loads (the pass stored Tn write-through)
+        const uint64_t* tn = (const uint64_t*)(Tn + (int64_t)pl * ld + j);
+        const double x0 = __builtin_bit_cast(double, __hip_atomic_load(tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const double x1 = __builtin_bit_cast(double, __hip_atomic_load(tn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        t0.x = x0;
+        t0.y = x1;
+    } else if (pl >= 0 && j < ld) {
+        t0 = *(const d2*)(T + (int64_t)pl * ld + j);
+    }
     if (fused && !LEAN) {   // (LEAN: within the 32 VGPRs that let it run beside the pass)
         zqpre = C[rows * ldc + s];
         if (j < ((ncols + 16) & ~(int64_t)15)) zpre = *(const d2*)(T + rows * ld + j);
@@ -539,7 +574,7 @@ __device__ __forceinline__ void prow_defer_body(
     if (owner_lane && LEAN) {
         d2 t = t0;
         asm volatile("" ::"v"(t.x), "v"(t.y));   // T0[p] in here (hipcc's own wait), not in the loop
-        for (int l = 0; l < S; ++l) {
+        for (int l = L0; l < S; ++l) {
             vmwait<RING - 1>();   // step l's DMA retired: only ring DMAs issue in this loop
             const d2 pv = *(const d2*)&s_ring[wv][l % RING][2 * wl];
             if (pl == s_pl[l]) {
@@ -613,9 +648,9 @@ __device__ __forceinline__ void prow_defer_body(
         const double *__restrict__ C, int64_t ldc, double *__restrict__ P, int64_t *__restrict__ bits,  \
         PricePart *pp, double tol_dj, dlp_pivot *log, int64_t log_cap, int fused,                    \
         const double *__restrict__ Cp, const double *__restrict__ Pp, int prev_seal, const XPeers *xp, \
-        uint32_t xseq
+        uint32_t xseq, uint32_t *bcnt, int brb, int bnt, const double *Tn
 #define DLP_PROW_PASS T, ld, rows, ncols, nprice, st, C, ldc, P, bits, pp, tol_dj, log, log_cap, fused, Cp, Pp, \
-                      prev_seal, xp, xseq
+                      prev_seal, xp, xseq, bcnt, brb, bnt, Tn
 // The LEAN instance (lookahead at K = 64, beside the form-21 pass) is held to 32 VGPRs in its
 // kernel descriptor: the pass leaves 32 per SIMD (with the LDS-DMA asm, hipcc's descriptor
 // otherwise requested 176 for a body that uses 30, and the kernel could not share a CU).
@@ -1596,14 +1631,20 @@ __device__ __forceinline__ double replay_row(double t, int cl, const double (&pr
     return t;
 }
 
-template <bool NT>
+// PUB (lookahead): the output rows are stored write-through (sc1) and every workgroup, once
+// all its waves have drained their stores, adds 1 to its band's count, so the next block's
+// selections can read a finished band from Tout instead of replaying this block on it
+// (band_done; MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table).
+template <bool NT, bool PUB = false>
 __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ T, double* __restrict__ Tout,
                                                      int64_t ld, int64_t rows, int64_t width,
                                                      const BlockDesc* __restrict__ bd,
                                                      const double* __restrict__ C, int64_t ldc,
                                                      const double* __restrict__ P,
-                                                     const int32_t* __restrict__ nzc, int rb) {
+                                                     const int32_t* __restrict__ nzc, int rb,
+                                                     uint32_t* bcnt = nullptr) {
     constexpr int K = 64, U = 2;
+    constexpr int kSt = (NT ? 2 : 0) | (PUB ? kAuxSc1 : 0);   // store policy
     __shared__ int32_t cls[1024];
     const int kb = bd->blk;
     const bool outplace = Tout != T;
@@ -1670,7 +1711,7 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
 #pragma unroll
         for (int u = 0; u < U; ++u)
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t[u]), ro, voff_st, (r0 + u) * ld8,
-                                                  NT ? 2 : 0);
+                                                  kSt);
     };
     double ta[U], tb[U];
     int r = 0;
@@ -1697,16 +1738,21 @@ __global__ __launch_bounds__(256) void pass_d_kernel(const double* __restrict__ 
         const int cl = cls[r];
         if (cl == kUntouched && outplace) {
             const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rt, voff, r * ld8, NT ? 2 : 0);
-            __builtin_amdgcn_raw_buffer_store_b64(x, ro, voff_st, r * ld8, NT ? 2 : 0);
+            __builtin_amdgcn_raw_buffer_store_b64(x, ro, voff_st, r * ld8, kSt);
         } else if (cl != kUntouched) {
             const double* cr = C + (i0 + r) * ldc;
             double t = 0.0;
             if (cl < 0)
                 t = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rt, voff, r * ld8, NT ? 2 : 0));
             t = replay_row(t, cl, pr, [&](int l) { return cr[l]; });
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t), ro, voff_st, r * ld8, NT ? 2 : 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t), ro, voff_st, r * ld8, kSt);
         }
         r += 1;
+    }
+    if constexpr (PUB) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 stores are through
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(&bcnt[blockIdx.y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2035,9 +2081,13 @@ __global__ void blk_reset_kernel(DevState* st) {
 
 // Lookahead: the block just selected becomes st->seal[slot] (read by its pass and
 // replayed by the next block's selections); the next block starts empty.
-__global__ __launch_bounds__(64) void seal_kernel(DevState* st, int slot) {
+// (bcnt: the slot's band counts restart at 0 for the pass about to be launched, whose
+// output the next block's selections poll; the slot's previous pass has finished.)
+__global__ __launch_bounds__(64) void seal_kernel(DevState* st, int slot, uint32_t* bcnt, int64_t nb) {
     const int kb = st->blk;
     for (int l = threadIdx.x; l < kMaxDefer; l += 64) st->seal[slot].pl[l] = l < kb ? st->pl[l] : -1;
+    if (bcnt)
+        for (int64_t b = threadIdx.x; b < nb; b += 64) bcnt[b] = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
         st->seal[slot].blk = kb;
@@ -2055,8 +2105,10 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               const PricePart* pp, DevState* st, Cand* partials, int nblocks,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
-                              const Defer* prev, int prev_seal, const XPeers* xp, uint32_t xseq) {
+                              const Defer* prev, int prev_seal, const XPeers* xp, uint32_t xseq,
+                              const BandPub* bp) {
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
+    const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
     if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
     nblocks = ratio_defer_blocks(g);
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
@@ -2078,18 +2130,20 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
         DLP_RATIO_DEFER(64);
     else   // lookahead at K = 64, beside the form-21 pass
     {
-        static const int lch = std::getenv("DLP_LEAN_LCH") ? std::atoi(std::getenv("DLP_LEAN_LCH")) : 4;
+        static const int lch = std::getenv("DLP_LEAN_LCH") ? std::atoi(std::getenv("DLP_LEAN_LCH")) : 0;
 #define DLP_RATIO_LEAN(L, DYN)                                                                             \
     ratio_lean_kernel<128, L><<<nblocks, kRatioDeferThreads, DYN, s>>>(                                       \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
         d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
-        xp, xseq)
-        if (lch == 8)   // tuning only (DLP_LEAN_LCH)
+        xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,   \
+        pub ? bp->Tn : nullptr)
+        // the LDS ring (0); 4 or 8 coefficient loads per round trip for tuning only (DLP_LEAN_LCH)
+        if (lch == 8)
             DLP_RATIO_LEAN(8, 0);
-        else if (lch == 0)
-            DLP_RATIO_LEAN(0, kRatioRing);
-        else
+        else if (lch == 4)
             DLP_RATIO_LEAN(4, 0);
+        else
+            DLP_RATIO_LEAN(0, kRatioRing);
 #undef DLP_RATIO_LEAN
     }
 #undef DLP_RATIO_DEFER
@@ -2129,20 +2183,22 @@ int fused_pivot_blocks(const Geometry& g) {
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
                              int64_t log_cap, int nranks, hipStream_t s, const Defer* prev,
-                             int prev_seal, const XPeers* xp, uint32_t xseq) {
+                             int prev_seal, const XPeers* xp, uint32_t xseq, const BandPub* bp) {
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
+    const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
     if (prev_seal >= 0 && d.K > 32)   // lookahead at K = 64: beside the form-21 pass
-        prow_defer_kernel<true><<<blocks, 256, kProwRing, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
-                                                     d.P, prow_bits, pp, tol_dj, log, log_cap,
-                                                     nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal,
-                                                     nranks == 1 ? nullptr : xp, xseq);
+        prow_defer_kernel<true><<<blocks, 256, kProwRing, s>>>(
+            g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap,
+            nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal, nranks == 1 ? nullptr : xp, xseq,
+            pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,
+            pub ? bp->Tn : nullptr);
     else
         prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
                                                  d.P, prow_bits, pp, tol_dj, log, log_cap,
                                                  nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
                                                  prev_seal >= 0 ? prev->P : nullptr, prev_seal,
-                                                 nranks == 1 ? nullptr : xp, xseq);
+                                                 nranks == 1 ? nullptr : xp, xseq, nullptr, 1, 0, nullptr);
     return hipGetLastError();
 }
 
@@ -2173,7 +2229,7 @@ static void launch_pass_r(const Geometry& g, const Defer& d, DevState* st, int r
 
 template <bool NT, int K>
 static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
-                       hipStream_t s, double* Tout, int seal) {
+                       hipStream_t s, double* Tout, int seal, uint32_t* bcnt) {
     // lookahead: out of place, the sealed block; pass_s forms only (lookahead_form)
     if (seal >= 0 && !lookahead_form(d.form)) return hipErrorInvalidValue;
     const BlockDesc* bd = seal >= 0 ? &st->seal[seal] : (const BlockDesc*)&st->blk;
@@ -2234,8 +2290,12 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             if (occ > 0) dyn = (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t);
             const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
             if (g.rows > 0) {
-                pass_d_kernel<NT><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P,
-                                                         d.nzc, rb);
+                if (bcnt)
+                    pass_d_kernel<NT, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
+                                                                   d.P, d.nzc, rb, bcnt);
+                else
+                    pass_d_kernel<NT><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P,
+                                                             d.nzc, rb);
             }
             if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
             return hipGetLastError();
@@ -2344,25 +2404,34 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
 
 template <bool NT>
 static hipError_t pass_k(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
-                         hipStream_t s, double* Tout, int seal) {
-    if (d.K <= 4) return pass<NT, 4>(g, d, st, rb, occ, s, Tout, seal);
-    if (d.K <= 8) return pass<NT, 8>(g, d, st, rb, occ, s, Tout, seal);
-    if (d.K <= 16) return pass<NT, 16>(g, d, st, rb, occ, s, Tout, seal);
-    if (d.K <= 32) return pass<NT, 32>(g, d, st, rb, occ, s, Tout, seal);
-    return pass<NT, 64>(g, d, st, rb, occ, s, Tout, seal);
+                         hipStream_t s, double* Tout, int seal, uint32_t* bcnt) {
+    if (d.K <= 4) return pass<NT, 4>(g, d, st, rb, occ, s, Tout, seal, nullptr);
+    if (d.K <= 8) return pass<NT, 8>(g, d, st, rb, occ, s, Tout, seal, nullptr);
+    if (d.K <= 16) return pass<NT, 16>(g, d, st, rb, occ, s, Tout, seal, nullptr);
+    if (d.K <= 32) return pass<NT, 32>(g, d, st, rb, occ, s, Tout, seal, nullptr);
+    return pass<NT, 64>(g, d, st, rb, occ, s, Tout, seal, bcnt);
 }
 
 bool lookahead_form(int form) {
     return form == 3 || form == 4 || form == 5 || form == 20 || form == 21 || form == 22 || form == 23;
 }
 
+bool band_pub_ok(const BandPub& bp, const Geometry& g, const Defer& d, int rb) {
+    return d.form == 21 && d.K == 64 && d.ldc == 64 && rb == bp.rb && (g.rows + rb - 1) / rb <= bp.stride &&
+           (int)((g.width + 255) / 256) == bp.ntiles;
+}
+
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
                               int rows_per_block, int occupancy, hipStream_t s, double* Tout,
-                              int seal) {
+                              int seal, const BandPub* bp) {
     if (d.K < 1 || d.K > kMaxDefer || rows_per_block < 1 || rows_per_block > 1024 || seal > 1)
         return hipErrorInvalidValue;
-    return nontemporal ? pass_k<true>(g, d, st, rows_per_block, occupancy, s, Tout, seal)
-                       : pass_k<false>(g, d, st, rows_per_block, occupancy, s, Tout, seal);
+    // band publication: lookahead passes of form 21 (band_pub_ok), counted per seal slot
+    uint32_t* bcnt = nullptr;
+    if (bp && bp->cnt && seal >= 0 && Tout && Tout != g.T && band_pub_ok(*bp, g, d, rows_per_block))
+        bcnt = bp->cnt + seal * bp->stride;
+    return nontemporal ? pass_k<true>(g, d, st, rows_per_block, occupancy, s, Tout, seal, bcnt)
+                       : pass_k<false>(g, d, st, rows_per_block, occupancy, s, Tout, seal, bcnt);
 }
 
 hipError_t chain_stamps_enable() {
@@ -2373,9 +2442,10 @@ hipError_t chain_stamps_dump(uint64_t* host64x16) {
     return hipMemcpyFromSymbol(host64x16, HIP_SYMBOL(g_chain_stamps), sizeof(uint64_t) * 64 * 16);
 }
 
-hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s) {
+hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s, const BandPub* bp) {
     if (slot < 0 || slot > 1) return hipErrorInvalidValue;
-    seal_kernel<<<1, 64, 0, s>>>(st, slot);
+    seal_kernel<<<1, 64, 0, s>>>(st, slot, bp && bp->cnt ? bp->cnt + slot * bp->stride : nullptr,
+                                 bp ? bp->stride : 0);
     return hipGetLastError();
 }
 

@@ -132,6 +132,20 @@ struct Defer {
                            // 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows
 };
 
+// Lookahead band publication: the form-21 pass of seal slot s counts its
+// finished workgroups per band in cnt[s * stride + band]; a band whose count reached ntiles
+// is final in Tn, so the next block's selections read its rows there and replay only their
+// own block (bit-identical: the pass computes the same operations in the same order).
+struct BandPub {
+    uint32_t* cnt = nullptr;    // [2][stride]
+    int64_t stride = 0;         // >= the pass's bands
+    int rb = 0;                 // pass rows per band
+    int ntiles = 0;             // pass workgroups per band (256-column tiles)
+    const double* Tn = nullptr; // the pass's output buffer (set per pass by the session)
+};
+struct Geometry;
+bool band_pub_ok(const BandPub& bp, const Geometry& g, const struct Defer& d, int rb);
+
 static_assert(offsetof(DevState, pl) - offsetof(DevState, blk) == offsetof(BlockDesc, pl),
               "BlockDesc must alias DevState::blk / pl");
 
@@ -196,12 +210,13 @@ hipError_t launch_set_status(DevState* st, int status, hipStream_t s);
 // Deferred launchers (dlp_defer.hip).  Pricing tiles are kDeferTile columns.
 // prev / prev_seal (lookahead): the sealed block st->seal[prev_seal] whose arrays are
 // `prev` is not yet applied to g.T; its steps are replayed before the current block's.
+// bp (lookahead at K = 64): the pass in flight publishes its finished bands (BandPub).
 hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               const PricePart* pp, DevState* st, Cand* partials, int nblocks,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
                               const Defer* prev = nullptr, int prev_seal = -1,
-                              const XPeers* xp = nullptr, uint32_t seq = 0);
+                              const XPeers* xp = nullptr, uint32_t seq = 0, const BandPub* bp = nullptr);
 // nranks == 1: ratio test + selection + pivot row + objective row + pricing in ONE launch
 // (K <= 32; grid of fused_pivot_blocks(g), all of which must be resident at once).
 int fused_pivot_blocks(const Geometry& g);
@@ -217,7 +232,7 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
                              int64_t log_cap, int nranks, hipStream_t s,
                              const Defer* prev = nullptr, int prev_seal = -1,
-                             const XPeers* xp = nullptr, uint32_t seq = 0);
+                             const XPeers* xp = nullptr, uint32_t seq = 0, const BandPub* bp = nullptr);
 // nranks > 1, after the MAX all-reduce: P[s] from the exchanged bits + objective row + pricing.
 // xp: each workgroup first waits for its chunk's flag (seq), then reads the row region
 // with system-scope loads (prow_bits = this rank's row region).
@@ -232,13 +247,13 @@ hipError_t launch_commit_defer(const Geometry& g, const Defer& d, DevState* st,
 // 22, 23).
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,
                               int rows_per_block, int occupancy, hipStream_t s,
-                              double* Tout = nullptr, int seal = -1);
+                              double* Tout = nullptr, int seal = -1, const BandPub* bp = nullptr);
 bool lookahead_form(int form);
 // Diagnostics (DLP_CHAIN_STAMPS): phase stamps of the LEAN chain kernels (dlp_defer.hip).
 hipError_t chain_stamps_enable();
 hipError_t chain_stamps_dump(uint64_t* host64x16);
 // End of a lookahead block: st->seal[slot] := (blk, pl), blk := 0.
-hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s);
+hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s, const BandPub* bp = nullptr);
 hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits, int nranks,
                        hipStream_t s);
 hipError_t launch_update(const Geometry& g, const double* colq, const double* prow,

@@ -153,6 +153,9 @@ struct dlp_session {
     // row is current.
     bool la = false;
     double* Tb[2] = {nullptr, nullptr};
+    // band publication of the lookahead pass (dlp::BandPub): [2][band_stride] counts
+    uint32_t* band_cnt = nullptr;
+    int64_t band_stride = 0;
     int tread = 0, tcur = 0, zbuf = 0, cur = 0;
     bool la_pending = false;   // a pass is in flight: Tb[tread] lacks block (1 - cur)
     dlp::Defer dslot[2];
@@ -341,7 +344,7 @@ void free_session(dlp_session* s) {
     if (s->pstream) (void)hipStreamSynchronize(s->pstream);
     void* dev[] = {s->Tb[0] ? s->Tb[0] : s->T, s->Tb[1], s->colq, s->prow_send, s->partials,
                    s->cand_send, s->cand_recv, s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc,
-                   s->d.P, s->d.rhs, s->d.nzc, s->cl_gran};
+                   s->d.P, s->d.rhs, s->d.nzc, s->cl_gran, s->band_cnt};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     if (s->la || s->dslot[1].C) {   // slot 0 aliases s->d
@@ -675,6 +678,9 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
             HIP_TRY(hipMemsetAsync(d1.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
             HIP_TRY(hipMemsetAsync(d1.Cc, 0, sizeof(double) * s->d.K * s->d.ldcc, s->stream));
             HIP_TRY(hipMemsetAsync(d1.P, 0, sizeof(double) * kt * s->ld, s->stream));
+            s->band_stride = (s->rows + 63) / 64 + 1;   // bands of >= 64 rows
+            HIP_TRY(hipMalloc(&s->band_cnt, sizeof(uint32_t) * 2 * s->band_stride));
+            HIP_TRY(hipMemsetAsync(s->band_cnt, 0, sizeof(uint32_t) * 2 * s->band_stride, s->stream));
             HIP_TRY(acquire_stream(s->device, prio_least, &s->pstream));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_seal, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_pass, hipEventDisableTiming));
@@ -770,19 +776,35 @@ int la_drain(dlp_session* s) {
     return DLP_OK;
 }
 
+// The lookahead pass's band publication: the form-21 pass counts its
+// finished workgroups per band; the next block's selections read a finished band's rows
+// from the pass's output (Tn) and replay their own block only.  DLP_BAND_PUB=0: off (A/B).
+dlp::BandPub band_pub(const dlp_session* s) {
+    static const bool off = std::getenv("DLP_BAND_PUB") && std::atoi(std::getenv("DLP_BAND_PUB")) == 0;
+    dlp::BandPub b;
+    if (!s->band_cnt || off) return b;
+    b.cnt = s->band_cnt;
+    b.stride = s->band_stride;
+    b.rb = s->defer_rb;
+    b.ntiles = (int)((s->g.width + 255) / 256);
+    b.Tn = s->la_pending ? s->Tb[s->tcur] : nullptr;   // the pass in flight writes Tb[tcur]
+    return b;
+}
+
 // End of a block: seal it, start its pass (Tb[tcur] -> the other buffer) on pstream
 // behind the seal, and move the selections to the pass's source, which the previous
 // pass (if one is in flight) must have finished writing.  drain: also wait for
 // this pass (a window's end).
 int la_block_end(dlp_session* s, bool drain, hipEvent_t* evp) {
-    HIP_TRY(dlp::launch_seal_defer(s->st, s->cur, s->stream));
+    const dlp::BandPub bp = band_pub(s);
+    HIP_TRY(dlp::launch_seal_defer(s->st, s->cur, s->stream, &bp));
     HIP_TRY(hipEventRecord(s->ev_seal, s->stream));
     HIP_TRY(hipStreamWaitEvent(s->pstream, s->ev_seal, 0));
     if (evp) HIP_TRY(hipEventRecord(evp[0], s->pstream));
     dlp::Geometry gp = s->g;
     gp.T = s->Tb[s->tcur];
     HIP_TRY(dlp::launch_flush_defer(gp, s->dslot[s->cur], s->st, s->opt.nontemporal != 0, s->defer_rb,
-                                    s->defer_occ, s->pstream, s->Tb[1 - s->tcur], s->cur));
+                                    s->defer_occ, s->pstream, s->Tb[1 - s->tcur], s->cur, &bp));
     if (evp) HIP_TRY(hipEventRecord(evp[1], s->pstream));
     if (s->la_pending) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_pass, 0));   // previous pass
     HIP_TRY(hipEventRecord(s->ev_pass, s->pstream));                            // this pass
@@ -835,6 +857,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     const dlp::Defer* dcur = &s->d;
     const dlp::Defer* dprev = nullptr;
     int pseal = -1;
+    const dlp::BandPub bp = band_pub(s);
     if (s->la) {
         gsel.T = s->Tb[s->tread];
         dcur = &s->dslot[s->cur];
@@ -856,7 +879,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         HIP_TRY(dlp::launch_ratio_defer(gsel, *dcur, s->basis, s->pp, s->st, s->partials,
                                         s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
                                         o.tol_piv, o.pricing, s->log, s->log_cap, s->stream, dprev,
-                                        pseal, xp, s->xseq_c));
+                                        pseal, xp, s->xseq_c, &bp));
         if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
         if (s->xmode == dlp_session::X_RCCL)
             NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
@@ -872,7 +895,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         if (xp) s->xseq_r += 1;
         HIP_TRY(dlp::launch_prow_defer(gsel, *dcur, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
                                        s->log_cap, s->exchange ? 2 : 1, s->stream, dprev, pseal, xp,
-                                       s->xseq_r));
+                                       s->xseq_r, &bp));
         if (s->xmode == dlp_session::X_RCCL)
             NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
                                    s->comm, s->stream));
