@@ -1801,14 +1801,17 @@ __device__ __forceinline__ void ring_half(double (&t)[U], const double (&c)[U][2
     (ring_step<U, L0 + I>(t, c, pr), ...);
 }
 
-template <bool NT, int U, int D>
+// PUB: band publication as form 21's (pass_d_kernel)
+template <bool NT, int U, int D, bool PUB = false>
 __global__ __launch_bounds__(256) void pass_q_kernel(const double* __restrict__ T, double* __restrict__ Tout,
                                                      int64_t ld, int64_t rows, int64_t width,
                                                      const BlockDesc* __restrict__ bd,
                                                      const double* __restrict__ C, int64_t ldc,
                                                      const double* __restrict__ P,
-                                                     const int32_t* __restrict__ nzc, int rb) {
+                                                     const int32_t* __restrict__ nzc, int rb,
+                                                     uint32_t* bcnt = nullptr) {
     constexpr int K = 64, SLOT = 128 * U;   // doubles per ring slot
+    constexpr int kSt = (NT ? 2 : 0) | (PUB ? kAuxSc1 : 0);   // store policy
     static_assert(U % 2 == 0, "one DMA carries two rows");
     __shared__ int32_t cls[1024];
     extern __shared__ double ring[];   // [4 waves][D slots][SLOT]
@@ -1866,7 +1869,7 @@ __global__ __launch_bounds__(256) void pass_q_kernel(const double* __restrict__ 
     const int voff_st = colok ? jc * 8 : 0x7fffff00;
     auto store = [&](double v, int r, bool keep) {
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), ro, keep ? voff_st : 0x7fffff00,
-                                              (r < nr ? r : 0) * ld8, NT ? 2 : 0);
+                                              (r < nr ? r : 0) * ld8, kSt);
     };
 #pragma unroll
     for (int s = 0; s < D; ++s) dma(s, s);
@@ -1914,6 +1917,11 @@ __global__ __launch_bounds__(256) void pass_q_kernel(const double* __restrict__ 
         }
         dma(g + D, s);
         s = s + 1 == D ? 0 : s + 1;
+    }
+    if constexpr (PUB) {
+        vmwait<0>();   // every wave: its sc1 stores are through (and the clamped tail DMAs landed)
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(&bcnt[blockIdx.y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2312,8 +2320,12 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             if (occ > 0) dyn = std::max(dyn, (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t));
             const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
             if (g.rows > 0) {
-                pass_q_kernel<NT, U, D><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
-                                                              d.P, d.nzc, rb);
+                if (bcnt)
+                    pass_q_kernel<NT, U, D, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C,
+                                                                         d.ldc, d.P, d.nzc, rb, bcnt);
+                else
+                    pass_q_kernel<NT, U, D><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
+                                                                  d.P, d.nzc, rb);
             }
             if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
             return hipGetLastError();
@@ -2417,7 +2429,7 @@ bool lookahead_form(int form) {
 }
 
 bool band_pub_ok(const BandPub& bp, const Geometry& g, const Defer& d, int rb) {
-    return d.form == 21 && d.K == 64 && d.ldc == 64 && rb == bp.rb && (g.rows + rb - 1) / rb <= bp.stride &&
+    return (d.form == 21 || d.form == 23) && d.K == 64 && d.ldc == 64 && rb == bp.rb && (g.rows + rb - 1) / rb <= bp.stride &&
            (int)((g.width + 255) / 256) == bp.ntiles;
 }
 
