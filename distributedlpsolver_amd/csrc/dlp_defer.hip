@@ -282,14 +282,16 @@ __device__ __forceinline__ void ratio_defer_body(
     Cand c = cand_empty();
     double flast = 0.0;   // LEAN: C of step J-1 (the RHS cache's step)
     if constexpr (RING) {
-        auto step = [&](int l, double fv) {
-            if (i < rows) {
-                if (i == s_pl[l])
-                    a = s_pq[l];
-                else if (fv != 0.0)
-                    a = __builtin_fma(-fv, s_pq[l], a);
-            }
-            flast = fv;
+        // branch-free (the fma is computed and dropped where the eager rule skips it), so
+        // the LDS reads of a pair's two steps issue together instead of one per branch
+        // (ok = false: a pair's second step past J-1, read from the tables' spare entries and
+        // dropped: l <= J <= KMAX - 1)
+        auto step = [&](int l, double fv, bool ok) {
+            const double pq = s_pq[l];
+            const bool piv = i == s_pl[l];
+            const double u = __builtin_fma(-fv, pq, a);
+            a = ok && i < rows ? (piv ? pq : (fv != 0.0 ? u : a)) : a;
+            flast = ok ? fv : flast;
         };
         if (wave_rows) {
             const int npairs = (J - L0 + 1) >> 1;
@@ -297,8 +299,8 @@ __device__ __forceinline__ void ratio_defer_body(
                 vmwait<kRatioRingPairs - 1>();   // pair p landed: only ring DMAs issue in this loop
                 double* rs = ring_at(p);
                 const double f0 = rs[wl], f1 = rs[64 + wl];
-                step(L0 + 2 * p, f0);
-                if (L0 + 2 * p + 1 < J) step(L0 + 2 * p + 1, f1);
+                step(L0 + 2 * p, f0, true);
+                step(L0 + 2 * p + 1, f1, L0 + 2 * p + 1 < J);
                 glds16(csrc(p + kRatioRingPairs), lds_addr(rs));
             }
             vmwait<0>();
@@ -577,12 +579,11 @@ __device__ __forceinline__ void prow_defer_body(
         for (int l = L0; l < S; ++l) {
             vmwait<RING - 1>();   // step l's DMA retired: only ring DMAs issue in this loop
             const d2 pv = *(const d2*)&s_ring[wv][l % RING][2 * wl];
-            if (pl == s_pl[l]) {
-                t = pv;
-            } else if (s_cp[l] != 0.0) {
-                t.x = __builtin_fma(-s_cp[l], pv.x, t.x);
-                t.y = __builtin_fma(-s_cp[l], pv.y, t.y);
-            }
+            const double cp = s_cp[l];
+            const bool piv = pl == s_pl[l];
+            const double ux = __builtin_fma(-cp, pv.x, t.x), uy = __builtin_fma(-cp, pv.y, t.y);
+            t.x = piv ? pv.x : (cp != 0.0 ? ux : t.x);   // (branch-free, as the ratio ring's step)
+            t.y = piv ? pv.y : (cp != 0.0 ? uy : t.y);
             glds16(psrc(l + RING), lds_addr(&s_ring[wv][l % RING][0]));
         }
         vmwait<0>();   // the ring drained (the clamped tail DMAs) before the block exits
