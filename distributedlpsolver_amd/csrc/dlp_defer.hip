@@ -2316,18 +2316,31 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
         // flight per wave: 32 KiB of ring + 4 KiB of row classes per workgroup, so three pass
         // workgroups leave the lookahead chain's LDS free on a CU
         if constexpr (K == 64) {
-            constexpr int U = 2, D = 4;
+            // ring depth D: 4 groups in flight (DLP_Q_DEPTH = 2 or 3: tuning only)
+            static const int qd = std::getenv("DLP_Q_DEPTH") ? std::atoi(std::getenv("DLP_Q_DEPTH")) : 4;
+            constexpr int U = 2;
+            const int D = qd == 2 || qd == 3 ? qd : 4;
             size_t dyn = (size_t)4 * D * 128 * U * sizeof(double);
             if (occ > 0) dyn = std::max(dyn, (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t));
             const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
+#define DLP_PASS_Q(DD)                                                                                     \
+    do {                                                                                                   \
+        if (bcnt)                                                                                          \
+            pass_q_kernel<NT, U, DD, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, \
+                                                                  d.ldc, d.P, d.nzc, rb, bcnt);           \
+        else                                                                                               \
+            pass_q_kernel<NT, U, DD><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, \
+                                                           d.P, d.nzc, rb);                                \
+    } while (0)
             if (g.rows > 0) {
-                if (bcnt)
-                    pass_q_kernel<NT, U, D, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C,
-                                                                         d.ldc, d.P, d.nzc, rb, bcnt);
+                if (D == 2)
+                    DLP_PASS_Q(2);
+                else if (D == 3)
+                    DLP_PASS_Q(3);
                 else
-                    pass_q_kernel<NT, U, D><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
-                                                                  d.P, d.nzc, rb);
+                    DLP_PASS_Q(4);
             }
+#undef DLP_PASS_Q
             if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
             return hipGetLastError();
         }
