@@ -113,6 +113,34 @@ def test_peer_exchange_lookahead_and_windows():
             s.close()
 
 
+@pytest.mark.parametrize("P,form", [(2, 21), (4, 21), (3, 23)])
+def test_peer_exchange_lookahead_k64(P, form):
+    """Lookahead forced on at K = 64 with the peer exchange: the LEAN selection kernels
+    (LDS-DMA rings) push candidates and pivot rows to the peers while the pass of the
+    sealed block runs, and read rows of finished bands from the pass's output (band
+    publication, form 21; form 23 replays every row).  Windows end inside blocks."""
+    m, n, seed = 400, 600, 11
+    A, b, c = O.gen_dense(m, n, seed)
+    ref = O.solve_dense(A, b, c)
+    assert ref.num_pivots > 3 * 64
+    sess = _peer_ranks(dlp.Problem.random(m, n, seed), P, defer=64, lookahead=1, check_interval=64)
+    try:
+        for s in sess:
+            s.set_defer_tuning(0, form)
+        assert all(s.lookahead() for s in sess)
+        total = 0
+        while True:
+            st, done = dlp.Session.run_ranks(sess, 101)
+            total += done
+            if st != L.PIVOT_LIMIT and st != L.RUNNING:
+                break
+        assert st == L.OK and total == ref.num_pivots
+        _check(dlp.Session.merged_result(sess), ref)
+    finally:
+        for s in sess:
+            s.close()
+
+
 @pytest.mark.parametrize("P", [2, 3])
 @pytest.mark.parametrize("name", ["lpgen_2d_20x20_eq", "enzo_c_infeasible", "basic_artificial_vars"])
 def test_peer_exchange_general(P, name):
