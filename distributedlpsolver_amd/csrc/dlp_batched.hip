@@ -13,7 +13,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dlp_host.h"
@@ -268,6 +270,229 @@ __global__ __launch_bounds__(512) void batched_solve_kernel(const double* __rest
         for (int i = tid; i < m; i += blockDim.x) out.basis[lp * m + i] = basis[i];
 }
 
+// C5, register-resident (round 3): at m = 64 one LANE owns one slot (column) of the
+// nonbasic tableau, all 65 of its rows in 130 VGPRs (rows unrolled: no dynamic register
+// index), so the elimination is 65 fmas per lane from registers with the column q read
+// from LDS as a broadcast, and the pivot row is computed in place (each lane divides its
+// own T[p][s]).  A workgroup of NW = ceil((n + 1) / 64) waves is one LP (192 lanes at
+// 64 x 128, 129 of them owning a slot); no LDS holds the tableau, so 3 waves per SIMD fit:
+// 4 LPs per CU at 64 x 128 (the LDS kernel: 2), 6 at 64 x 64 (4).  Per pivot: pricing
+// (wave shuffles + one LDS partial per wave), the entering column and the RHS written to
+// LDS by their two owner lanes, the ratio test by wave 0 (one row per lane), 3 barriers.
+// Same operations on the same values as batched_solve_kernel (same bits).
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): a register array indexed
+// by I stays in registers (a #pragma unroll of 65 iterations may be left rolled, and the
+// array then lives in scratch)
+template <typename F, int... I>
+__device__ __forceinline__ void each_(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void each(F&& f) {
+    each_(f, std::make_integer_sequence<int, N>{});
+}
+
+// One row of the register-resident elimination, in inline asm with uniform (scalar)
+// branches: the entering column's entry f and the pivot row index are the same for every
+// lane of the LP, so the eager rule's two tests (row p takes the pivot row; f == 0 leaves the
+// row untouched) are SALU compares and branches, and each row costs one VALU fma.  (hipcc,
+// left to itself, turned the 2 x 65 tests into live vector masks and spilled them, or the
+// register rows into scratch.)  f == +-0 is tested on the bits without the sign.
+// tp := t where row == p
+template <int ROW>
+__device__ __forceinline__ void pick_row(double& tp, double t, int p) {
+    asm volatile(
+        "s_cmp_eq_u32 %[p], %[row]\n\t"
+        "s_cbranch_scc0 1f\n\t"
+        "v_mov_b64 %[tp], %[t]\n"
+        "1:"
+        : [tp] "+v"(tp)
+        : [t] "v"(t), [p] "s"(p), [row] "n"(ROW)
+        : "scc");
+}
+// t := pj (row p) | t (f == 0) | fma(-f, pj, t)
+template <int ROW>
+__device__ __forceinline__ void elim_row(double& t, double f, double pj, int p) {
+    uint64_t tmp;
+    asm volatile(
+        "s_cmp_eq_u32 %[p], %[row]\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "s_lshl_b64 %[tmp], %[f], 1\n\t"
+        "s_cmp_lg_u64 %[tmp], 0\n\t"
+        "s_cbranch_scc0 3f\n\t"
+        "v_fma_f64 %[t], -%[f], %[pj], %[t]\n\t"
+        "s_branch 3f\n"
+        "2:\n\t"
+        "v_mov_b64 %[t], %[pj]\n"
+        "3:"
+        : [t] "+v"(t), [tmp] "=&s"(tmp)
+        : [f] "s"(f), [pj] "v"(pj), [p] "s"(p), [row] "n"(ROW)
+        : "scc");
+}
+__device__ __forceinline__ double uniform_d(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+template <int M, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void batched_reg_kernel(const double* __restrict__ Tg, int64_t ldg, int n,
+                                                           int64_t max_pivots, int pricing, double tol_dj,
+                                                           double tol_piv, BatchOut out) {
+    static_assert(M == 64, "one ratio-test row per lane of wave 0");
+    constexpr int R = M + 1;   // rows, the objective row last
+    __shared__ double s_colq[R], s_rhs[M];
+    __shared__ double s_zv[NW];
+    __shared__ int32_t s_zvar[NW], s_zslot[NW], s_bvar[NW], s_bslot[NW];
+    __shared__ int32_t s_basis[M];
+    __shared__ int32_t s_p, s_leave, s_bland;
+    __shared__ double s_piv;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W = n + 1, N = n + M;
+    const int sl = tid;              // this lane's slot: < n a variable's column, n the RHS
+    const bool own = sl < W;
+    int var = sl < n ? sl : kNoIndex;   // the variable in the slot
+    const int64_t lp = blockIdx.x;
+    // buffer loads, one lane offset and the row in the scalar offset (a flat load per row
+    // would hold 65 64-bit addresses in VGPRs next to the 65 values); lanes past the slots
+    // read out of range, which returns +0
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Tg + lp * (int64_t)R * ldg), (short)0, (int)((int64_t)R * ldg * 8), 0x00020000);
+    const int voff = own ? (sl < n ? sl : N) * 8 : 0x7fffff00;
+    double t[R];
+    each<R>([&](auto I) {
+        t[I] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (int)(I * ldg * 8), 0));
+    });
+    for (int i = tid; i < M; i += blockDim.x) s_basis[i] = n + i;
+    if (tid == 0) s_bland = pricing == DLP_PRICING_BLAND ? 1 : 0;
+    __syncthreads();
+    int status = DLP_RUNNING;
+    int64_t k = 0;
+    for (; k < max_pivots; ++k) {
+        // ---- a1 pricing: lexicographic (z, variable) min; Bland: first variable with z < -tol
+        {
+            double zmin = __builtin_inf();
+            int vmin = kNoIndex, smin = -1, vb = kNoIndex, sb = -1;
+            if (sl < n) {
+                const double z = t[M];
+                if (z < zmin) { zmin = z; vmin = var; smin = sl; }
+                if (z < -tol_dj) { vb = var; sb = sl; }
+            }
+#pragma unroll
+            for (int sh = 32; sh >= 1; sh >>= 1) {
+                const double oz = __shfl_xor(zmin, sh);
+                const int ov = __shfl_xor(vmin, sh), os = __shfl_xor(smin, sh);
+                const int ob = __shfl_xor(vb, sh), osb = __shfl_xor(sb, sh);
+                if (oz < zmin || (oz == zmin && ov < vmin)) { zmin = oz; vmin = ov; smin = os; }
+                if (ob < vb) { vb = ob; sb = osb; }
+            }
+            if (lane == 0) {
+                s_zv[wid] = zmin; s_zvar[wid] = vmin; s_zslot[wid] = smin;
+                s_bvar[wid] = vb; s_bslot[wid] = sb;
+            }
+        }
+        __syncthreads();
+        int q = kNoIndex, sq = -1;
+        {
+            double zmin = s_zv[0];
+            int vmin = s_zvar[0], smin = s_zslot[0], vb = s_bvar[0], sb = s_bslot[0];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) {
+                if (s_zv[w] < zmin || (s_zv[w] == zmin && s_zvar[w] < vmin)) {
+                    zmin = s_zv[w]; vmin = s_zvar[w]; smin = s_zslot[w];
+                }
+                if (s_bvar[w] < vb) { vb = s_bvar[w]; sb = s_bslot[w]; }
+            }
+            if (s_bland) {
+                q = vb; sq = sb;
+            } else if (vmin != kNoIndex && zmin < -tol_dj) {
+                q = vmin; sq = smin;
+            }
+        }
+        if (q == kNoIndex) {
+            status = DLP_OK;
+            break;
+        }
+        // ---- the entering column and the RHS to LDS (their owner lanes)
+        if (sl == sq) each<R>([&](auto I) { s_colq[I] = t[I]; });
+        if (sl == n) each<M>([&](auto I) { s_rhs[I] = t[I]; });
+        __syncthreads();
+        // ---- a2 ratio test (wave 0, row = lane) + a4 select and log
+        if (wid == 0) {
+            Cand best;
+            best.valid = 0; best.ratio = 0.0; best.basis_var = kNoIndex; best.row = -1;
+            best.pad0 = 0; best.pivot = 0.0;
+            const double a = s_colq[lane];
+            if (a > tol_piv) {
+                double rhs = s_rhs[lane];
+                if (!(rhs > 0.0)) rhs = 0.0;
+                best.ratio = rhs / a; best.basis_var = s_basis[lane]; best.row = lane; best.valid = 1;
+                best.pivot = a;
+            }
+#pragma unroll
+            for (int sh = 32; sh >= 1; sh >>= 1) {
+                Cand o;
+                o.ratio = __shfl_xor(best.ratio, sh);
+                o.basis_var = __shfl_xor(best.basis_var, sh);
+                o.row = __shfl_xor(best.row, sh);
+                o.valid = __shfl_xor(best.valid, sh);
+                o.pad0 = 0;
+                o.pivot = __shfl_xor(best.pivot, sh);
+                if (cand_better(o, best)) best = o;
+            }
+            if (lane == 0) {
+                if (!best.valid) {
+                    s_p = -1;
+                } else {
+                    const int p = best.row;
+                    const int leaving = s_basis[p];
+                    s_basis[p] = q;
+                    s_leave = leaving;
+                    s_p = p;
+                    s_bland = (pricing == DLP_PRICING_BLAND) ? 1 : (best.ratio == 0.0 ? 1 : 0);
+                    s_piv = best.pivot;
+                    if (out.logs && k < out.log_cap) {
+                        dlp_pivot e;
+                        e.q = q; e.p = p; e.leaving = leaving; e.pad = 0;
+                        e.ratio = best.ratio; e.objective = 0.0;
+                        out.logs[lp * out.log_cap + k] = e;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const int p = __builtin_amdgcn_readfirstlane(s_p);   // (uniform: an SGPR operand below)
+        if (p < 0) {
+            status = DLP_UNBOUNDED;
+            break;
+        }
+        // ---- a3 pivot row (IEEE division, in place) and the elimination; the entering slot
+        // takes the leaving variable's column (e_p before the pivot)
+        const bool ent = sl == sq;
+        if (ent) var = s_leave;
+        double tp = 0.0;
+        each<R>([&](auto I) { pick_row<I>(tp, t[I], p); });   // tp = t[p]
+        const double pj = (ent ? 1.0 : tp) / s_piv;
+        if (ent) each<R>([&](auto I) { t[I] = 0.0; });   // e_p before the pivot (see the LDS kernel)
+        double fq[8];   // a group's column entries, read together
+        each<R>([&](auto I) {
+            if constexpr ((I & 7) == 0) each<(R - I < 8 ? R - I : 8)>([&](auto J) { fq[J] = s_colq[I + J]; });
+            elim_row<I>(t[I], uniform_d(fq[I & 7]), pj, p);
+        });
+        if (sl == n && out.logs && k < out.log_cap) out.logs[lp * out.log_cap + k].objective = t[M];
+    }
+    if (sl == n) {
+        int stt = status;
+        if (stt == DLP_RUNNING) stt = DLP_PIVOT_LIMIT;
+        if (out.status) out.status[lp] = stt;
+        if (out.npivots) out.npivots[lp] = k;
+        if (out.objective) out.objective[lp] = t[M];
+    }
+    if (out.basis)
+        for (int i = tid; i < M; i += blockDim.x) out.basis[lp * M + i] = s_basis[i];
+}
+
 }  // namespace
 }  // namespace dlp
 
@@ -334,13 +559,31 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
         bo.basis = dBasis;
         bo.logs = dLog;
         bo.log_cap = dLog ? log_cap : 0;
-        HIP_BTRY(hipFuncSetAttribute((const void*)dlp::batched_solve_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        // m = 64 with n + 1 <= 192 slots: the register-resident kernel (DLP_BATCH_LDS=1: the
+        // LDS kernel, for A/B); otherwise the LDS-resident one
+        static const bool force_lds = std::getenv("DLP_BATCH_LDS") && std::atoi(std::getenv("DLP_BATCH_LDS")) == 1;
+        const int nw = (int)((n + 1 + 63) / 64);
+        const bool reg = !force_lds && m == 64 && nw >= 1 && nw <= 3;
+        if (!reg)
+            HIP_BTRY(hipFuncSetAttribute((const void*)dlp::batched_solve_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         HIP_BTRY(hipEventRecord(e0, s));
-        // 512 lanes per LP when few LPs share a CU (LDS > 40 KB each), else 256
-        const unsigned threads = lds > 40 * 1024 ? 512 : 256;
-        dlp::batched_solve_kernel<<<(unsigned)nlp, threads, lds, s>>>(
-            dT, ldg, (int)m, (int)n, o.max_pivots, o.pricing, o.tol_dj, o.tol_piv, bo);
+        if (reg) {
+            if (nw == 1)
+                dlp::batched_reg_kernel<64, 1><<<(unsigned)nlp, 64, 0, s>>>(dT, ldg, (int)n, o.max_pivots, o.pricing,
+                                                                          o.tol_dj, o.tol_piv, bo);
+            else if (nw == 2)
+                dlp::batched_reg_kernel<64, 2><<<(unsigned)nlp, 128, 0, s>>>(dT, ldg, (int)n, o.max_pivots, o.pricing,
+                                                                           o.tol_dj, o.tol_piv, bo);
+            else
+                dlp::batched_reg_kernel<64, 3><<<(unsigned)nlp, 192, 0, s>>>(dT, ldg, (int)n, o.max_pivots, o.pricing,
+                                                                           o.tol_dj, o.tol_piv, bo);
+        } else {
+            // 512 lanes per LP when few LPs share a CU (LDS > 40 KB each), else 256
+            const unsigned threads = lds > 40 * 1024 ? 512 : 256;
+            dlp::batched_solve_kernel<<<(unsigned)nlp, threads, lds, s>>>(
+                dT, ldg, (int)m, (int)n, o.max_pivots, o.pricing, o.tol_dj, o.tol_piv, bo);
+        }
         HIP_BTRY(hipGetLastError());
         HIP_BTRY(hipEventRecord(e1, s));
         HIP_BTRY(hipStreamSynchronize(s));

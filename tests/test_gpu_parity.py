@@ -242,6 +242,24 @@ def test_batched_c5_small():
             _same_log(br.logs[k][:ref.num_pivots], ref.pivot_log)
 
 
+@pytest.mark.parametrize("n", [32, 100, 128, 191])
+def test_batched_register_kernel_shapes(n):
+    """m = 64: the register-resident batched kernel (one lane per slot; 1, 2, 2, 3 waves
+    per LP, the last wave partly idle except at n = 191), dense and degenerate LPs (Bland,
+    exact ratio ties), every LP against the oracle."""
+    nlp, m, seed = 16, 64, 300 + n
+    for degen in (False, True):
+        br = dlp.batched_solve(nlp, m, n, seed, degenerate=degen, want_basis=True, log_cap=4096)
+        for k in range(nlp):
+            A, b, c = O.gen_dense(m, n, seed + k, degen)
+            ref = O.solve_dense(A, b, c, nthreads=1)
+            assert br.status[k] == ref.status
+            assert br.num_pivots[k] == ref.num_pivots
+            assert np.float64(br.objective[k]).tobytes() == np.float64(ref.objective).tobytes()
+            np.testing.assert_array_equal(br.basis[k], ref.basis)
+            _same_log(br.logs[k][:ref.num_pivots], ref.pivot_log)
+
+
 def test_batched_matches_single_gpu_path():
     br = dlp.batched_solve(4, 32, 96, 7, log_cap=2048)
     for k in range(4):
