@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <utility>
@@ -80,6 +81,7 @@ struct BatchOut {
     int32_t* basis;
     dlp_pivot* logs;
     int64_t log_cap;
+    uint64_t* stamps;   // diagnostics (DLP_BATCH_STAMPS): LP 0's phase clocks, [64 pivots][8]
 };
 
 // One workgroup = one LP.  The LDS holds only the NONBASIC columns of the
@@ -292,50 +294,37 @@ __device__ __forceinline__ void each(F&& f) {
     each_(f, std::make_integer_sequence<int, N>{});
 }
 
-// One row of the register-resident elimination, in inline asm with uniform (scalar)
-// branches: the entering column's entry f and the pivot row index are the same for every
-// lane of the LP, so the eager rule's two tests (row p takes the pivot row; f == 0 leaves the
-// row untouched) are SALU compares and branches, and each row costs one VALU fma.  (hipcc,
-// left to itself, turned the 2 x 65 tests into live vector masks and spilled them, or the
-// register rows into scratch.)  f == +-0 is tested on the bits without the sign.
-// tp := t where row == p
-template <int ROW>
-__device__ __forceinline__ void pick_row(double& tp, double t, int p) {
+// Rows of the register-resident elimination in inline asm.  The entering column's entry f
+// and the pivot row index are the same for every lane of the LP, so each test is a uniform
+// exec mask (all lanes or none) set by SALU, with no branch: a row costs one compare and one
+// fma on the VALU.  (hipcc, left to itself, turned the 2 x 65 tests into live vector masks
+// and spilled them, or moved the register rows to scratch.)
+// t := fma(-f, pj, t) unless f == +-0 (the eager rule leaves the row untouched)
+__device__ __forceinline__ void elim_row(double& t, double f, double pj) {
+    uint64_t sv;
     asm volatile(
-        "s_cmp_eq_u32 %[p], %[row]\n\t"
-        "s_cbranch_scc0 1f\n\t"
-        "v_mov_b64 %[tp], %[t]\n"
-        "1:"
-        : [tp] "+v"(tp)
-        : [t] "v"(t), [p] "s"(p), [row] "n"(ROW)
-        : "scc");
-}
-// t := pj (row p) | t (f == 0) | fma(-f, pj, t)
-template <int ROW>
-__device__ __forceinline__ void elim_row(double& t, double f, double pj, int p) {
-    uint64_t tmp;
-    asm volatile(
-        "s_cmp_eq_u32 %[p], %[row]\n\t"
-        "s_cbranch_scc1 2f\n\t"
-        "s_lshl_b64 %[tmp], %[f], 1\n\t"
-        "s_cmp_lg_u64 %[tmp], 0\n\t"
-        "s_cbranch_scc0 3f\n\t"
+        "v_cmp_neq_f64_e32 vcc, 0, %[f]\n\t"
+        "s_and_saveexec_b64 %[sv], vcc\n\t"
         "v_fma_f64 %[t], -%[f], %[pj], %[t]\n\t"
-        "s_branch 3f\n"
-        "2:\n\t"
-        "v_mov_b64 %[t], %[pj]\n"
-        "3:"
-        : [t] "+v"(t), [tmp] "=&s"(tmp)
-        : [f] "s"(f), [pj] "v"(pj), [p] "s"(p), [row] "n"(ROW)
+        "s_mov_b64 exec, %[sv]"
+        : [t] "+v"(t), [sv] "=&s"(sv)
+        : [f] "v"(f), [pj] "v"(pj)
+        : "vcc");
+}
+// dst := src where ROW == p (p uniform)
+template <int ROW>
+__device__ __forceinline__ void move_if_row(double& dst, double src, int p) {
+    uint64_t m, sv;
+    asm volatile(
+        "s_cmp_eq_u32 %[p], %[row]\n\t"
+        "s_cselect_b64 %[m], -1, 0\n\t"
+        "s_and_saveexec_b64 %[sv], %[m]\n\t"
+        "v_mov_b64 %[d], %[s]\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [d] "+v"(dst), [m] "=&s"(m), [sv] "=&s"(sv)
+        : [s] "v"(src), [p] "s"(p), [row] "n"(ROW)
         : "scc");
 }
-__device__ __forceinline__ double uniform_d(double v) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-
 template <int M, int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void batched_reg_kernel(const double* __restrict__ Tg, int64_t ldg, int n,
                                                            int64_t max_pivots, int pricing, double tol_dj,
@@ -369,7 +358,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     __syncthreads();
     int status = DLP_RUNNING;
     int64_t k = 0;
+    auto stamp = [&](int ph) {
+        if (out.stamps && lp == 0 && tid == 0 && k < 64) out.stamps[k * 8 + ph] = wall_clock64();
+    };
     for (; k < max_pivots; ++k) {
+        stamp(0);
         // ---- a1 pricing: lexicographic (z, variable) min; Bland: first variable with z < -tol
         {
             double zmin = __builtin_inf();
@@ -393,6 +386,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             }
         }
         __syncthreads();
+        stamp(1);
         int q = kNoIndex, sq = -1;
         {
             double zmin = s_zv[0];
@@ -418,6 +412,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         if (sl == sq) each<R>([&](auto I) { s_colq[I] = t[I]; });
         if (sl == n) each<M>([&](auto I) { s_rhs[I] = t[I]; });
         __syncthreads();
+        stamp(2);
         // ---- a2 ratio test (wave 0, row = lane) + a4 select and log
         if (wid == 0) {
             Cand best;
@@ -462,6 +457,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             }
         }
         __syncthreads();
+        stamp(3);
         const int p = __builtin_amdgcn_readfirstlane(s_p);   // (uniform: an SGPR operand below)
         if (p < 0) {
             status = DLP_UNBOUNDED;
@@ -472,14 +468,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         const bool ent = sl == sq;
         if (ent) var = s_leave;
         double tp = 0.0;
-        each<R>([&](auto I) { pick_row<I>(tp, t[I], p); });   // tp = t[p]
+        each<R>([&](auto I) { move_if_row<I>(tp, t[I], p); });   // tp = t[p]
         const double pj = (ent ? 1.0 : tp) / s_piv;
+        stamp(4);
         if (ent) each<R>([&](auto I) { t[I] = 0.0; });   // e_p before the pivot (see the LDS kernel)
         double fq[8];   // a group's column entries, read together
         each<R>([&](auto I) {
             if constexpr ((I & 7) == 0) each<(R - I < 8 ? R - I : 8)>([&](auto J) { fq[J] = s_colq[I + J]; });
-            elim_row<I>(t[I], uniform_d(fq[I & 7]), pj, p);
+            elim_row(t[I], fq[I & 7], pj);
         });
+        each<R>([&](auto I) { move_if_row<I>(t[I], pj, p); });   // row p := the pivot row
+        stamp(5);
         if (sl == n && out.logs && k < out.log_cap) out.logs[lp * out.log_cap + k].objective = t[M];
     }
     if (sl == n) {
@@ -536,6 +535,7 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
     int64_t* dNp = nullptr;
     int32_t* dBasis = nullptr;
     dlp_pivot* dLog = nullptr;
+    uint64_t* dStamps = nullptr;
     hipStream_t s = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     dlp::BatchOut bo{};
@@ -559,6 +559,12 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
         bo.basis = dBasis;
         bo.logs = dLog;
         bo.log_cap = dLog ? log_cap : 0;
+        static const char* stamp_file = std::getenv("DLP_BATCH_STAMPS");
+        if (stamp_file) {
+            HIP_BTRY(hipMalloc(&dStamps, sizeof(uint64_t) * 64 * 8));
+            HIP_BTRY(hipMemsetAsync(dStamps, 0, sizeof(uint64_t) * 64 * 8, s));
+            bo.stamps = dStamps;
+        }
         // m = 64 with n + 1 <= 192 slots: the register-resident kernel (DLP_BATCH_LDS=1: the
         // LDS kernel, for A/B); otherwise the LDS-resident one
         static const bool force_lds = std::getenv("DLP_BATCH_LDS") && std::atoi(std::getenv("DLP_BATCH_LDS")) == 1;
@@ -598,11 +604,19 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
         if (basis) HIP_BTRY(hipMemcpy(basis, dBasis, sizeof(int32_t) * nlp * m, hipMemcpyDeviceToHost));
         if (dLog)
             HIP_BTRY(hipMemcpy(logs, dLog, sizeof(dlp_pivot) * nlp * log_cap, hipMemcpyDeviceToHost));
+        if (dStamps) {   // diagnostics only
+            std::vector<uint64_t> h(64 * 8);
+            HIP_BTRY(hipMemcpy(h.data(), dStamps, sizeof(uint64_t) * 64 * 8, hipMemcpyDeviceToHost));
+            if (FILE* f = std::fopen(stamp_file, "wb")) {
+                std::fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+                std::fclose(f);
+            }
+        }
     }
 done:
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
-    for (void* p : {(void*)dT, (void*)dObj, (void*)dSt, (void*)dNp, (void*)dBasis, (void*)dLog})
+    for (void* p : {(void*)dT, (void*)dObj, (void*)dSt, (void*)dNp, (void*)dBasis, (void*)dLog, (void*)dStamps})
         if (p) (void)hipFree(p);
     if (s) (void)hipStreamDestroy(s);
     return rc;
