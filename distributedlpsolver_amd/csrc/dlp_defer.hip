@@ -2189,6 +2189,18 @@ int fused_pivot_blocks(const Geometry& g) {
     return ratio_defer_blocks(g) + (int)((g.ld + kDeferTile - 1) / kDeferTile);
 }
 
+// How many workgroups of the fused pivot kernel (the instance launch_pivot_defer picks for K)
+// the device holds at once, from the compiled kernel's real occupancy (0 when unknown): its
+// pivot-row blocks spin on the ratio blocks' selection, so the whole grid must be resident.
+int fused_pivot_capacity(int K, int cus) {
+    int per = 0;
+    const hipError_t e =
+        K <= 8    ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pivot_defer_kernel<8>, 256, 0)
+        : K <= 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pivot_defer_kernel<16>, 256, 0)
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pivot_defer_kernel<32>, 256, 0);
+    return e == hipSuccess ? per * cus : 0;
+}
+
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
                              int64_t log_cap, int nranks, hipStream_t s, const Defer* prev,

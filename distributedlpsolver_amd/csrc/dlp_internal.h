@@ -220,6 +220,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
 // nranks == 1: ratio test + selection + pivot row + objective row + pricing in ONE launch
 // (K <= 32; grid of fused_pivot_blocks(g), all of which must be resident at once).
 int fused_pivot_blocks(const Geometry& g);
+int fused_pivot_capacity(int K, int cus);   // resident workgroups of the fused kernel (0: unknown)
 hipError_t launch_pivot_defer(const Geometry& g, const Defer& d, int32_t* basis, PricePart* pp,
                               DevState* st, Cand* partials, int nblocks, double tol_dj,
                               double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,

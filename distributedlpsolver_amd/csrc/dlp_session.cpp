@@ -104,7 +104,7 @@ struct dlp_session {
     // deferred, single rank: one launch for ratio + selection + pivot row (opt-in: measured
     // equal to two launches, C2 24.7 vs 25.0 us/pivot, profiles/r02c/tune_*_fused.txt)
     bool fuse_pivot = false;
-    bool fuse_fits = false;   // ... when K <= 32 and the grid fits 2 blocks per CU
+    bool fuse_fits = false;   // ... when K <= 32 and the whole grid is resident at once
     // small LPs: the whole window in one launch, tableau in the LDS of cl_wg workgroups
     bool cluster = false;
     int cl_wg = 0, cl_cw = 0;
@@ -563,7 +563,9 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess)
             cus = 0;
-        s->fuse_fits = s->d.K > 1 && s->d.K <= 32 && dlp::fused_pivot_blocks(g) <= 2 * cus;
+        // (the kernel's real occupancy, not an assumed 2 per CU: ADVICE r02)
+        s->fuse_fits = s->d.K > 1 && s->d.K <= 32 &&
+                       dlp::fused_pivot_blocks(g) <= std::min(2 * cus, dlp::fused_pivot_capacity(s->d.K, cus));
     }
     s->ratio_blocks_max = std::max(s->ratio_blocks, dlp::ratio_defer_blocks(g));
     HIP_TRY(hipMalloc(&s->colq, sizeof(double) * (rows_total + dlp::kColqPad)));
