@@ -279,8 +279,9 @@ __global__ __launch_bounds__(512) void batched_solve_kernel(const double* __rest
 // own T[p][s]).  A workgroup of NW = ceil((n + 1) / 64) waves is one LP (192 lanes at
 // 64 x 128, 129 of them owning a slot); no LDS holds the tableau, so 3 waves per SIMD fit:
 // 4 LPs per CU at 64 x 128 (the LDS kernel: 2), 6 at 64 x 64 (4).  Per pivot: pricing
-// (wave shuffles + one LDS partial per wave), the entering column and the RHS written to
-// LDS by their two owner lanes, the ratio test by wave 0 (one row per lane), 3 barriers.
+// (wave shuffles + one LDS partial per wave), the entering column written to LDS by its
+// owner lane, the ratio test by wave 0 (one row per lane, which also keeps that row's RHS),
+// 3 barriers.
 // Same operations on the same values as batched_solve_kernel (same bits).
 // f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): a register array indexed
 // by I stays in registers (a #pragma unroll of 65 iterations may be left rolled, and the
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
                                                            double tol_piv, BatchOut out) {
     static_assert(M == 64, "one ratio-test row per lane of wave 0");
     constexpr int R = M + 1;   // rows, the objective row last
-    __shared__ double s_colq[R], s_rhs[M];
+    __shared__ double s_colq[R];
     __shared__ double s_zv[NW];
     __shared__ int32_t s_zvar[NW], s_zslot[NW], s_bvar[NW], s_bslot[NW];
     __shared__ int32_t s_basis[M];
@@ -353,6 +354,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     each<R>([&](auto I) {
         t[I] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (int)(I * ldg * 8), 0));
     });
+    // wave 0, lane i also keeps row i's RHS (the ratio test's), updated with the RHS slot's own
+    // operations below (same bits), so the RHS column is never copied to LDS
+    double rr = 0.0;
+    if (wid == 0)
+        rr = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(((int64_t)lane * ldg + N) * 8), 0, 0));
     for (int i = tid; i < M; i += blockDim.x) s_basis[i] = n + i;
     if (tid == 0) s_bland = pricing == DLP_PRICING_BLAND ? 1 : 0;
     __syncthreads();
@@ -363,26 +369,35 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     };
     for (; k < max_pivots; ++k) {
         stamp(0);
-        // ---- a1 pricing: lexicographic (z, variable) min; Bland: first variable with z < -tol
+        // ---- a1 pricing: lexicographic (z, variable) min; Bland: first variable with z < -tol.
+        // Reduced field by field (min z, then the smallest variable among the lanes holding it;
+        // the Bland variable apart): fewer cross-lane moves than shuffling the whole tuple.
         {
-            double zmin = __builtin_inf();
-            int vmin = kNoIndex, smin = -1, vb = kNoIndex, sb = -1;
-            if (sl < n) {
-                const double z = t[M];
-                if (z < zmin) { zmin = z; vmin = var; smin = sl; }
-                if (z < -tol_dj) { vb = var; sb = sl; }
-            }
+            const bool cand = sl < n;
+            const double z = cand && t[M] < __builtin_inf() ? t[M] : __builtin_inf();   // (as z < zmin: NaN skipped)
+            double zmin = z;
 #pragma unroll
             for (int sh = 32; sh >= 1; sh >>= 1) {
-                const double oz = __shfl_xor(zmin, sh);
-                const int ov = __shfl_xor(vmin, sh), os = __shfl_xor(smin, sh);
-                const int ob = __shfl_xor(vb, sh), osb = __shfl_xor(sb, sh);
-                if (oz < zmin || (oz == zmin && ov < vmin)) { zmin = oz; vmin = ov; smin = os; }
-                if (ob < vb) { vb = ob; sb = osb; }
+                const double o = __shfl_xor(zmin, sh);
+                zmin = o < zmin ? o : zmin;
             }
+            const int vz = cand && z == zmin ? var : kNoIndex;
+            const int vbl = cand && z < -tol_dj ? var : kNoIndex;
+            int vmin = vz, vb = vbl;
+#pragma unroll
+            for (int sh = 32; sh >= 1; sh >>= 1) {
+                vmin = min(vmin, __shfl_xor(vmin, sh));
+                vb = min(vb, __shfl_xor(vb, sh));
+            }
+            // the slots of the two winners (variables are distinct: one lane each)
+            const uint64_t wz = __ballot(vz == vmin && vmin != kNoIndex);
+            const uint64_t wb = __ballot(vbl == vb && vb != kNoIndex);
             if (lane == 0) {
-                s_zv[wid] = zmin; s_zvar[wid] = vmin; s_zslot[wid] = smin;
-                s_bvar[wid] = vb; s_bslot[wid] = sb;
+                s_zv[wid] = zmin;
+                s_zvar[wid] = vmin;
+                s_zslot[wid] = wz ? wid * 64 + __ffsll((unsigned long long)wz) - 1 : -1;
+                s_bvar[wid] = vb;
+                s_bslot[wid] = wb ? wid * 64 + __ffsll((unsigned long long)wb) - 1 : -1;
             }
         }
         __syncthreads();
@@ -408,34 +423,46 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             status = DLP_OK;
             break;
         }
-        // ---- the entering column and the RHS to LDS (their owner lanes)
+        // ---- the entering column to LDS (its owner lane)
         if (sl == sq) each<R>([&](auto I) { s_colq[I] = t[I]; });
-        if (sl == n) each<M>([&](auto I) { s_rhs[I] = t[I]; });
         __syncthreads();
         stamp(2);
         // ---- a2 ratio test (wave 0, row = lane) + a4 select and log
         if (wid == 0) {
-            Cand best;
-            best.valid = 0; best.ratio = 0.0; best.basis_var = kNoIndex; best.row = -1;
-            best.pad0 = 0; best.pivot = 0.0;
+            // min ratio over the valid rows, then the smallest basis variable among the rows
+            // holding it (cand_better's order), field by field
             const double a = s_colq[lane];
-            if (a > tol_piv) {
-                double rhs = s_rhs[lane];
+            const bool valid = a > tol_piv;
+            double ratio = __builtin_inf();
+            if (valid) {
+                double rhs = rr;
                 if (!(rhs > 0.0)) rhs = 0.0;
-                best.ratio = rhs / a; best.basis_var = s_basis[lane]; best.row = lane; best.valid = 1;
-                best.pivot = a;
+                ratio = rhs / a;
             }
+            const uint64_t anyv = __ballot(valid);
+            double rmin = ratio;
 #pragma unroll
             for (int sh = 32; sh >= 1; sh >>= 1) {
-                Cand o;
-                o.ratio = __shfl_xor(best.ratio, sh);
-                o.basis_var = __shfl_xor(best.basis_var, sh);
-                o.row = __shfl_xor(best.row, sh);
-                o.valid = __shfl_xor(best.valid, sh);
-                o.pad0 = 0;
-                o.pivot = __shfl_xor(best.pivot, sh);
-                if (cand_better(o, best)) best = o;
+                const double o = __shfl_xor(rmin, sh);
+                rmin = o < rmin ? o : rmin;
             }
+            const bool tie = valid && ratio == rmin;
+            const int bv = s_basis[lane];
+            const uint64_t ties = __ballot(tie);
+            int wl = __ffsll((unsigned long long)ties) - 1;
+            if (__popcll(ties) > 1) {   // exact ties: the smallest basis variable
+                int bmin = tie ? bv : kNoIndex;
+#pragma unroll
+                for (int sh = 32; sh >= 1; sh >>= 1) bmin = min(bmin, __shfl_xor(bmin, sh));
+                wl = __ffsll((unsigned long long)__ballot(tie && bv == bmin)) - 1;
+            }
+            Cand best;
+            best.valid = anyv != 0 ? 1 : 0;
+            best.row = wl;
+            best.basis_var = anyv != 0 ? __shfl(bv, wl) : kNoIndex;
+            best.ratio = anyv != 0 ? __shfl(ratio, wl) : 0.0;
+            best.pivot = anyv != 0 ? __shfl(a, wl) : 0.0;
+            best.pad0 = 0;
             if (lane == 0) {
                 if (!best.valid) {
                     s_p = -1;
@@ -478,6 +505,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             elim_row(t[I], fq[I & 7], pj);
         });
         each<R>([&](auto I) { move_if_row<I>(t[I], pj, p); });   // row p := the pivot row
+        if (wid == 0) {   // the RHS of row `lane`, as the RHS slot updates it
+            const double fr = s_colq[lane];
+            const double pjr = __shfl(rr, p) / s_piv;
+            const double v = __builtin_fma(-fr, pjr, rr);
+            rr = lane == p ? pjr : (fr != 0.0 ? v : rr);
+        }
         stamp(5);
         if (sl == n && out.logs && k < out.log_cap) out.logs[lp * out.log_cap + k].objective = t[M];
     }
