@@ -300,7 +300,32 @@ __device__ __forceinline__ void each(F&& f) {
 // exec mask (all lanes or none) set by SALU, with no branch: a row costs one compare and one
 // fma on the VALU.  (hipcc, left to itself, turned the 2 x 65 tests into live vector masks
 // and spilled them, or moved the register rows to scratch.)
-// t := fma(-f, pj, t) unless f == +-0 (the eager rule leaves the row untouched)
+// t := fma(-f, pj, t) unless f == +-0 (the eager rule leaves the row untouched); four rows per
+// block, their four tests issued first so that no exec write waits on the compare before it
+__device__ __forceinline__ void elim_row4(double& t0, double& t1, double& t2, double& t3, double f0, double f1,
+                                          double f2, double f3, double pj) {
+    uint64_t m0, m1, m2, m3, sv;
+    asm volatile(
+        "v_cmp_neq_f64_e64 %[m0], 0, %[f0]\n\t"
+        "v_cmp_neq_f64_e64 %[m1], 0, %[f1]\n\t"
+        "v_cmp_neq_f64_e64 %[m2], 0, %[f2]\n\t"
+        "v_cmp_neq_f64_e64 %[m3], 0, %[f3]\n\t"
+        "s_and_saveexec_b64 %[sv], %[m0]\n\t"
+        "v_fma_f64 %[t0], -%[f0], %[pj], %[t0]\n\t"
+        "s_mov_b64 exec, %[sv]\n\t"
+        "s_and_saveexec_b64 %[sv], %[m1]\n\t"
+        "v_fma_f64 %[t1], -%[f1], %[pj], %[t1]\n\t"
+        "s_mov_b64 exec, %[sv]\n\t"
+        "s_and_saveexec_b64 %[sv], %[m2]\n\t"
+        "v_fma_f64 %[t2], -%[f2], %[pj], %[t2]\n\t"
+        "s_mov_b64 exec, %[sv]\n\t"
+        "s_and_saveexec_b64 %[sv], %[m3]\n\t"
+        "v_fma_f64 %[t3], -%[f3], %[pj], %[t3]\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [t0] "+v"(t0), [t1] "+v"(t1), [t2] "+v"(t2), [t3] "+v"(t3), [m0] "=&s"(m0), [m1] "=&s"(m1),
+          [m2] "=&s"(m2), [m3] "=&s"(m3), [sv] "=&s"(sv)
+        : [f0] "v"(f0), [f1] "v"(f1), [f2] "v"(f2), [f3] "v"(f3), [pj] "v"(pj));
+}
 __device__ __forceinline__ void elim_row(double& t, double f, double pj) {
     uint64_t sv;
     asm volatile(
@@ -502,7 +527,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         double fq[8];   // a group's column entries, read together
         each<R>([&](auto I) {
             if constexpr ((I & 7) == 0) each<(R - I < 8 ? R - I : 8)>([&](auto J) { fq[J] = s_colq[I + J]; });
-            elim_row(t[I], fq[I & 7], pj);
+            if constexpr (I + 3 < R && (I & 3) == 0)   // rows I..I+3 (I & 7 is 0 or 4: one fq group)
+                elim_row4(t[I], t[I + 1], t[I + 2], t[I + 3], fq[I & 7], fq[(I & 7) + 1], fq[(I & 7) + 2],
+                          fq[(I & 7) + 3], pj);
+            else if constexpr (I + 3 >= R && (I & 3) == 0)
+                elim_row(t[I], fq[I & 7], pj);   // (the objective row, R = 65)
         });
         each<R>([&](auto I) { move_if_row<I>(t[I], pj, p); });   // row p := the pivot row
         if (wid == 0) {   // the RHS of row `lane`, as the RHS slot updates it
