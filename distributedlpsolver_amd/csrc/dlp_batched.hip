@@ -337,6 +337,48 @@ __device__ __forceinline__ void elim_row(double& t, double f, double pj) {
         : [f] "v"(f), [pj] "v"(pj)
         : "vcc");
 }
+// 8 rows at a time, one exec save/restore per block (exec is all lanes or none per row: p is
+// uniform), so a row costs a compare, an exec select and one move.  tp := t[p]
+template <int R0>
+__device__ __forceinline__ void pick8(double& tp, const double* t, int p) {
+    uint64_t sv;
+    asm volatile("s_mov_b64 %[sv], exec\n\t"
+                 "s_cmp_eq_u32 %[p], %[r0]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[d], %[t0]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r1]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[d], %[t1]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r2]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[d], %[t2]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r3]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[d], %[t3]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r4]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[d], %[t4]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r5]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[d], %[t5]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r6]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[d], %[t6]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r7]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[d], %[t7]\n\t"
+                 "s_mov_b64 exec, %[sv]"
+                 : [d] "+v"(tp), [sv] "=&s"(sv)
+                 : [t0] "v"(t[0]), [t1] "v"(t[1]), [t2] "v"(t[2]), [t3] "v"(t[3]), [t4] "v"(t[4]),
+                   [t5] "v"(t[5]), [t6] "v"(t[6]), [t7] "v"(t[7]), [p] "s"(p), [r0] "n"(R0), [r1] "n"(R0 + 1),
+                   [r2] "n"(R0 + 2), [r3] "n"(R0 + 3), [r4] "n"(R0 + 4), [r5] "n"(R0 + 5), [r6] "n"(R0 + 6),
+                   [r7] "n"(R0 + 7)
+                 : "scc");
+}
+// t[R0 + k] := v where R0 + k == p
+template <int R0>
+__device__ __forceinline__ void set8(double* t, double v, int p) {
+    uint64_t sv;
+    asm volatile("s_mov_b64 %[sv], exec\n\t"
+                 "s_cmp_eq_u32 %[p], %[r0]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[t0], %[v]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r1]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[t1], %[v]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r2]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[t2], %[v]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r3]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[t3], %[v]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r4]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[t4], %[v]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r5]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[t5], %[v]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r6]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[t6], %[v]\n\t"
+                 "s_cmp_eq_u32 %[p], %[r7]\n\ts_cselect_b64 exec, %[sv], 0\n\tv_mov_b64 %[t7], %[v]\n\t"
+                 "s_mov_b64 exec, %[sv]"
+                 : [t0] "+v"(t[0]), [t1] "+v"(t[1]), [t2] "+v"(t[2]), [t3] "+v"(t[3]), [t4] "+v"(t[4]),
+                   [t5] "+v"(t[5]), [t6] "+v"(t[6]), [t7] "+v"(t[7]), [sv] "=&s"(sv)
+                 : [v] "v"(v), [p] "s"(p), [r0] "n"(R0), [r1] "n"(R0 + 1), [r2] "n"(R0 + 2), [r3] "n"(R0 + 3),
+                   [r4] "n"(R0 + 4), [r5] "n"(R0 + 5), [r6] "n"(R0 + 6), [r7] "n"(R0 + 7)
+                 : "scc");
+}
 // dst := src where ROW == p (p uniform)
 template <int ROW>
 __device__ __forceinline__ void move_if_row(double& dst, double src, int p) {
@@ -520,7 +562,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         const bool ent = sl == sq;
         if (ent) var = s_leave;
         double tp = 0.0;
-        each<R>([&](auto I) { move_if_row<I>(tp, t[I], p); });   // tp = t[p]
+        each<M / 8>([&](auto G) { pick8<8 * G>(tp, &t[8 * G], p); });   // tp = t[p]
+        move_if_row<M>(tp, t[M], p);
         const double pj = (ent ? 1.0 : tp) / s_piv;
         stamp(4);
         if (ent) each<R>([&](auto I) { t[I] = 0.0; });   // e_p before the pivot (see the LDS kernel)
@@ -533,7 +576,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             else if constexpr (I + 3 >= R && (I & 3) == 0)
                 elim_row(t[I], fq[I & 7], pj);   // (the objective row, R = 65)
         });
-        each<R>([&](auto I) { move_if_row<I>(t[I], pj, p); });   // row p := the pivot row
+        each<M / 8>([&](auto G) { set8<8 * G>(&t[8 * G], pj, p); });   // row p := the pivot row
+        move_if_row<M>(t[M], pj, p);
         if (wid == 0) {   // the RHS of row `lane`, as the RHS slot updates it
             const double fr = s_colq[lane];
             const double pjr = __shfl(rr, p) / s_piv;
