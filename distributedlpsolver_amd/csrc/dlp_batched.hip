@@ -300,31 +300,31 @@ __device__ __forceinline__ void each(F&& f) {
 // exec mask (all lanes or none) set by SALU, with no branch: a row costs one compare and one
 // fma on the VALU.  (hipcc, left to itself, turned the 2 x 65 tests into live vector masks
 // and spilled them, or moved the register rows to scratch.)
-// t := fma(-f, pj, t) unless f == +-0 (the eager rule leaves the row untouched); four rows per
-// block, their four tests issued first so that no exec write waits on the compare before it
-__device__ __forceinline__ void elim_row4(double& t0, double& t1, double& t2, double& t3, double f0, double f1,
-                                          double f2, double f3, double pj) {
-    uint64_t m0, m1, m2, m3, sv;
+// t := fma(-f, pj, t) unless f == +-0 (the eager rule leaves the row untouched).
+// 8 rows: the 8 tests first, then per row one exec select (from the saved exec) and the fma
+__device__ __forceinline__ void elim8(double* t, const double* f, double pj) {
+    uint64_t m0, m1, m2, m3, m4, m5, m6, m7, sv;
     asm volatile(
-        "v_cmp_neq_f64_e64 %[m0], 0, %[f0]\n\t"
-        "v_cmp_neq_f64_e64 %[m1], 0, %[f1]\n\t"
-        "v_cmp_neq_f64_e64 %[m2], 0, %[f2]\n\t"
-        "v_cmp_neq_f64_e64 %[m3], 0, %[f3]\n\t"
-        "s_and_saveexec_b64 %[sv], %[m0]\n\t"
-        "v_fma_f64 %[t0], -%[f0], %[pj], %[t0]\n\t"
-        "s_mov_b64 exec, %[sv]\n\t"
-        "s_and_saveexec_b64 %[sv], %[m1]\n\t"
-        "v_fma_f64 %[t1], -%[f1], %[pj], %[t1]\n\t"
-        "s_mov_b64 exec, %[sv]\n\t"
-        "s_and_saveexec_b64 %[sv], %[m2]\n\t"
-        "v_fma_f64 %[t2], -%[f2], %[pj], %[t2]\n\t"
-        "s_mov_b64 exec, %[sv]\n\t"
-        "s_and_saveexec_b64 %[sv], %[m3]\n\t"
-        "v_fma_f64 %[t3], -%[f3], %[pj], %[t3]\n\t"
+        "v_cmp_neq_f64_e64 %[m0], 0, %[f0]\n\tv_cmp_neq_f64_e64 %[m1], 0, %[f1]\n\t"
+        "v_cmp_neq_f64_e64 %[m2], 0, %[f2]\n\tv_cmp_neq_f64_e64 %[m3], 0, %[f3]\n\t"
+        "v_cmp_neq_f64_e64 %[m4], 0, %[f4]\n\tv_cmp_neq_f64_e64 %[m5], 0, %[f5]\n\t"
+        "v_cmp_neq_f64_e64 %[m6], 0, %[f6]\n\tv_cmp_neq_f64_e64 %[m7], 0, %[f7]\n\t"
+        "s_mov_b64 %[sv], exec\n\t"
+        "s_and_b64 exec, %[sv], %[m0]\n\tv_fma_f64 %[t0], -%[f0], %[pj], %[t0]\n\t"
+        "s_and_b64 exec, %[sv], %[m1]\n\tv_fma_f64 %[t1], -%[f1], %[pj], %[t1]\n\t"
+        "s_and_b64 exec, %[sv], %[m2]\n\tv_fma_f64 %[t2], -%[f2], %[pj], %[t2]\n\t"
+        "s_and_b64 exec, %[sv], %[m3]\n\tv_fma_f64 %[t3], -%[f3], %[pj], %[t3]\n\t"
+        "s_and_b64 exec, %[sv], %[m4]\n\tv_fma_f64 %[t4], -%[f4], %[pj], %[t4]\n\t"
+        "s_and_b64 exec, %[sv], %[m5]\n\tv_fma_f64 %[t5], -%[f5], %[pj], %[t5]\n\t"
+        "s_and_b64 exec, %[sv], %[m6]\n\tv_fma_f64 %[t6], -%[f6], %[pj], %[t6]\n\t"
+        "s_and_b64 exec, %[sv], %[m7]\n\tv_fma_f64 %[t7], -%[f7], %[pj], %[t7]\n\t"
         "s_mov_b64 exec, %[sv]"
-        : [t0] "+v"(t0), [t1] "+v"(t1), [t2] "+v"(t2), [t3] "+v"(t3), [m0] "=&s"(m0), [m1] "=&s"(m1),
-          [m2] "=&s"(m2), [m3] "=&s"(m3), [sv] "=&s"(sv)
-        : [f0] "v"(f0), [f1] "v"(f1), [f2] "v"(f2), [f3] "v"(f3), [pj] "v"(pj));
+        : [t0] "+v"(t[0]), [t1] "+v"(t[1]), [t2] "+v"(t[2]), [t3] "+v"(t[3]), [t4] "+v"(t[4]), [t5] "+v"(t[5]),
+          [t6] "+v"(t[6]), [t7] "+v"(t[7]), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3),
+          [m4] "=&s"(m4), [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7), [sv] "=&s"(sv)
+        : [f0] "v"(f[0]), [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [f4] "v"(f[4]), [f5] "v"(f[5]),
+          [f6] "v"(f[6]), [f7] "v"(f[7]), [pj] "v"(pj)
+        : "scc");
 }
 __device__ __forceinline__ void elim_row(double& t, double f, double pj) {
     uint64_t sv;
@@ -568,14 +568,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         stamp(4);
         if (ent) each<R>([&](auto I) { t[I] = 0.0; });   // e_p before the pivot (see the LDS kernel)
         double fq[8];   // a group's column entries, read together
-        each<R>([&](auto I) {
-            if constexpr ((I & 7) == 0) each<(R - I < 8 ? R - I : 8)>([&](auto J) { fq[J] = s_colq[I + J]; });
-            if constexpr (I + 3 < R && (I & 3) == 0)   // rows I..I+3 (I & 7 is 0 or 4: one fq group)
-                elim_row4(t[I], t[I + 1], t[I + 2], t[I + 3], fq[I & 7], fq[(I & 7) + 1], fq[(I & 7) + 2],
-                          fq[(I & 7) + 3], pj);
-            else if constexpr (I + 3 >= R && (I & 3) == 0)
-                elim_row(t[I], fq[I & 7], pj);   // (the objective row, R = 65)
+        each<M / 8>([&](auto G) {
+            each<8>([&](auto J) { fq[J] = s_colq[8 * G + J]; });
+            elim8(&t[8 * G], fq, pj);
         });
+        elim_row(t[M], s_colq[M], pj);   // the objective row
         each<M / 8>([&](auto G) { set8<8 * G>(&t[8 * G], pj, p); });   // row p := the pivot row
         move_if_row<M>(t[M], pj, p);
         if (wid == 0) {   // the RHS of row `lane`, as the RHS slot updates it
