@@ -169,6 +169,9 @@ __device__ __forceinline__ void ratio_defer_body(
         else
             return block_cand(v, lds_c);
     };
+    // this lane's pricing partial is requested first: it depends on nothing, and the reduce
+    // below then waits for it alongside the step-table loads instead of after them
+    const PricePart pp0 = (int)threadIdx.x < ntiles ? pp[threadIdx.x] : pp_empty();
     if (st->status != DLP_RUNNING) return;
     const int64_t slot = st->npivots;
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 0);
@@ -233,7 +236,8 @@ __device__ __forceinline__ void ratio_defer_body(
     }
 
     PricePart acc = pp_empty();
-    for (int k = threadIdx.x; k < ntiles; k += blockDim.x) pp_combine(acc, pp[k]);
+    pp_combine(acc, pp0);
+    for (int k = threadIdx.x + blockDim.x; k < ntiles; k += blockDim.x) pp_combine(acc, pp[k]);
     if constexpr (LEAN) {
         // the tree keeps one side per pair: pp_combine's outcome, as a "better" test
         s_pt[threadIdx.x] = acc;
