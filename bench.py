@@ -47,6 +47,12 @@ WORKLOADS = {
     "c3": (32768, 32768, 3, "C3 dense LP 32768 x 32768 (+32768 slack): fp64 tableau 32769 x 65537, "
                             "row-block over the GPUs"),
     "c2": (4096, 4096, 2, "C2 dense LP 4096 x 4096 (+4096 slack): fp64 tableau 4097 x 8193"),
+    # the per-rank floor of the 8-GPU C3 split, on ONE GPU: a rank of C3 at P = 8 holds 4,096 rows
+    # x 65,537 columns; a 4096 x 61440 LP has exactly that tableau.  Run as a 1-rank exchange
+    # session (RCCL id, nranks = 1), so the chain carries the select / commit kernels and the
+    # exchange stores a rank of the split runs; only the xGMI latency is missing
+    "c3r8": (4096, 61440, 38, "C3 rank geometry at P = 8: dense LP 4096 x 61440 (+4096 slack), fp64 "
+                              "tableau 4097 x 65537 = one rank of the 8-GPU C3 split, 1-rank exchange"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP64_PEAK_TFS = 77.3   # measured v_fma_f64 peak on MI355X (tools/passlab.hip valu probe)
@@ -68,9 +74,10 @@ def parse():
     ap.add_argument("--eager-pivots", type=int, default=3)
     ap.add_argument("--no-pivot-window", action="store_true",
                     help="skip the extra --step-unit pivot window reported beside the main figure")
-    ap.add_argument("--exchange", default="rccl", choices=("rccl", "peer"),
-                    help="N > 1: the main window's row-block exchange (RCCL collectives, or owner-rooted "
-                         "peer stores into the ranks' exchange blocks)")
+    ap.add_argument("--exchange", default="auto", choices=("auto", "rccl", "peer"),
+                    help="N > 1 (and c3r8): the main window's row-block exchange: owner-rooted peer stores "
+                         "into the ranks' exchange blocks, or RCCL collectives; auto = peer where every "
+                         "rank pair connects, else RCCL (the reason is reported)")
     ap.add_argument("--alt-pivots", type=int, default=256,
                     help="N > 1: pivots of the second window, run with the other exchange (0 = none)")
     ap.add_argument("--rows-per-block", type=int, default=0)
@@ -228,7 +235,7 @@ def alt_exchange_window(sess, dist, barrier_sync, args, L, torch):
     to PEER all-gathers the exchange blocks' IPC handles over the session's communicator;
     every rank's outcome is agreed (MIN all-reduce) before anything is timed, and the window
     runs with a 60 s stall limit, so a broken path ends as an error field, never a hang."""
-    mode, name = (L.XCHG_PEER, "peer") if args.exchange == "rccl" else (L.XCHG_RCCL, "rccl")
+    mode, name = (L.XCHG_PEER, "peer") if sess.get_exchange() == L.XCHG_RCCL else (L.XCHG_RCCL, "rccl")
     out = {"exchange": name, "pivots": args.alt_pivots}
     ok = 1
     try:
@@ -279,7 +286,10 @@ def main():
         rccl_id = obj[0]
     else:
         dist = None
-        rccl_id = None
+        # c3r8: a 1-rank communicator, so the rank's exchange kernels run (select / commit waits)
+        rccl_id = dlp.comm_unique_id() if args.workload == "c3r8" else None
+    xsess = world > 1 or rccl_id is not None
+    xopt = {"auto": getattr(L, "XCHG_DEFAULT", 0), "rccl": L.XCHG_RCCL, "peer": L.XCHG_PEER}[args.exchange]
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -296,12 +306,18 @@ def main():
                        ld_align=args.ld_align, rows_per_block=args.rows_per_block,
                        max_pivots=64 * (args.warmup + args.steps) + args.steps + args.alt_pivots + 2,
                        log_pivots=1, defer=args.defer, lookahead=args.lookahead,
-                       exchange=(L.XCHG_PEER if args.exchange == "peer" else L.XCHG_RCCL) if world > 1 else 0)
+                       exchange=xopt if xsess else 0)
     if args.occupancy >= 0 or args.form >= 0:
         if sess.update_stats()[2] > 1:
             sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 0, args.form)
     K = sess.update_stats()[2]
     lookahead_on = sess.lookahead()
+    XNAMES = {L.XCHG_RCCL: "rccl", L.XCHG_PEER: "peer"}
+    xmode = XNAMES.get(sess.get_exchange(), "none") if xsess else None
+    xreason = sess.exchange_reason() if xsess and hasattr(sess, "exchange_reason") else None
+    if xsess:
+        # a dead rank ends the run in bounded time (its peers' waits abort), never a hang
+        sess.set_exchange_timeout(60.0)
     per_step = K if args.step_unit == "block" else 1
     warm, timed = args.warmup * per_step, args.steps * per_step
 
@@ -361,7 +377,7 @@ def main():
     # (RCCL collectives <-> owner-rooted peer stores), timed the same way, so that one
     # scaling run measures both; a failure to switch or to run is reported, not fatal
     alt = None
-    if dist is not None and args.alt_pivots > 0:
+    if dist is not None and args.alt_pivots > 0 and K > 1:
         alt = alt_exchange_window(sess, dist, barrier_sync, args, L, torch)
         if alt.get("pivots_per_s") and rank == 0:
             alt["pivot_log_vs_oracle"] = log_parity(args.workload, sess.result().pivot_log)
@@ -437,7 +453,16 @@ def main():
                                     if args.timing >= 2 else None),
             "update_launches": launches,
             "pivot_step_window": pw,
-            "exchange": args.exchange if world > 1 else None,
+            "exchange": xmode,
+            "exchange_requested": args.exchange if xsess else None,
+            "exchange_fallback_reason": xreason or None,
+            # the rank's block, split (c3r8: the per-rank floor of the 8-GPU split): without
+            # lookahead a block is its selection chain, then its pass, so the chain per pivot is
+            # (block - pass) / K; under lookahead they overlap and only the block is measured
+            "block": {"ms": 1e3 * elapsed / args.steps * (K / per_step), "pass_ms": upd_ms,
+                      "chain_us_per_pivot": ((1e3 * elapsed / args.steps * (K / per_step) - upd_ms) / K * 1e3
+                                             if (K > 1 and not lookahead_on and upd_ms > 0) else None),
+                      "lookahead": lookahead_on, "rows_local": rows_local},
             "alt_exchange_window": alt,
             "objective_after_run": obj_after,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -20,7 +20,7 @@ GEN_DENSE, GEN_DEGENERATE = 0, 1
 MINIMIZE, MAXIMIZE = 1, -1
 BUF_CAND_SEND, BUF_CAND_RECV, BUF_PROW_SEND, BUF_PROW_RECV = 0, 1, 2, 3
 PHASE_RATIO, PHASE_EXCHANGE, PHASE_PROW, PHASE_UPDATE = 0, 1, 2, 3
-XCHG_HOST, XCHG_RCCL, XCHG_PEER = 0, 1, 2
+XCHG_DEFAULT, XCHG_RCCL, XCHG_PEER, XCHG_HOST = 0, 1, 2, 3
 NUM_PHASES = 4
 
 
@@ -155,6 +155,7 @@ SIGNATURES = [
     ("dlp_session_connect_ipc", C.c_int, [_P, C.c_void_p]),
     ("dlp_session_set_exchange", C.c_int, [_P, C.c_int]),
     ("dlp_session_get_exchange", C.c_int, [_P, C.POINTER(C.c_int)]),
+    ("dlp_session_exchange_reason", C.c_int, [_P, C.c_char_p, C.c_size_t]),
     ("dlp_sessions_run", C.c_int, [C.POINTER(_P), C.c_int, _I64, C.POINTER(_I64)]),
     ("dlp_session_get_defer_tuning", C.c_int,
      [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),

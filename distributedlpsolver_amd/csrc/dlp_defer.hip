@@ -144,9 +144,10 @@ __device__ inline T block_tree(T v, T* s, Better better) {
 // LEAN, LCH = 0: the coefficient chain streams through a per-wave LDS ring by LDS-DMA, two
 // steps per DMA, kRatioRingPairs DMAs in flight (launch-time LDS, kRatioRing bytes: see
 // kProwRing).
+// (RP = kRatioRingPairs; 16 for tuning: DLP_RING_DEPTH=16)
 constexpr int kRatioRingPairs = 8;
-constexpr size_t kRatioRing = (kRatioDeferThreads / 64) * kRatioRingPairs * 128 * sizeof(double);
-template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4>
+constexpr size_t ratio_ring_bytes(int rp) { return (size_t)(kRatioDeferThreads / 64) * rp * 128 * sizeof(double); }
+template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4, int RP = kRatioRingPairs>
 __device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
@@ -155,7 +156,8 @@ __device__ __forceinline__ void ratio_defer_body(
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, int nblocks, const double* __restrict__ Ccp = nullptr,
     const double* __restrict__ Pp = nullptr, int prev_seal = -1, const XPeers* xp = nullptr,
-    uint32_t xseq = 0, uint32_t* bcnt = nullptr, int brb = 1, int bnt = 0, const double* Tn = nullptr) {
+    uint32_t xseq = 0, uint32_t* bcnt = nullptr, int brb = 1, int bnt = 0, const double* Tn = nullptr,
+    int xsel = 0) {
     __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
     __shared__ Cand lds_c[kRatioDeferThreads / 64];
     __shared__ int s_last;
@@ -207,7 +209,7 @@ __device__ __forceinline__ void ratio_defer_body(
             wdone = __builtin_amdgcn_readfirstlane(c0 == (uint32_t)bnt && c1 == (uint32_t)bnt ? 1 : 0) != 0;
         }
     const int L0 = wdone ? kp : 0;
-    auto ring_at = [&](int p) { return s_dyn + (wv * kRatioRingPairs + p % kRatioRingPairs) * 128; };
+    auto ring_at = [&](int p) { return s_dyn + (wv * RP + p % RP) * 128; };
     auto sbase = [&](int l) -> const double* {   // wave-uniform: step l's row i0 (l clamped)
         l = l < J ? l : J - 1;
         return (l < kp ? Ccp + (int64_t)l * ldcc : Cc + (int64_t)(l - kp) * ldcc) + i0;
@@ -218,7 +220,7 @@ __device__ __forceinline__ void ratio_defer_body(
     if constexpr (RING)
         if (wave_rows && J > L0)
 #pragma unroll
-            for (int p = 0; p < kRatioRingPairs; ++p) glds16(csrc(p), lds_addr(ring_at(p)));
+            for (int p = 0; p < RP; ++p) glds16(csrc(p), lds_addr(ring_at(p)));
     const int64_t ic = i < rows ? i : rows;   // clamped: loads need no guard
     double f[LEAN ? 1 : KMAX];
     if constexpr (!LEAN) {
@@ -300,12 +302,12 @@ __device__ __forceinline__ void ratio_defer_body(
         if (wave_rows) {
             const int npairs = (J - L0 + 1) >> 1;
             for (int p = 0; p < npairs; ++p) {
-                vmwait<kRatioRingPairs - 1>();   // pair p landed: only ring DMAs issue in this loop
+                vmwait<RP - 1>();   // pair p landed: only ring DMAs issue in this loop
                 double* rs = ring_at(p);
                 const double f0 = rs[wl], f1 = rs[64 + wl];
                 step(L0 + 2 * p, f0, true);
                 step(L0 + 2 * p + 1, f1, L0 + 2 * p + 1 < J);
-                glds16(csrc(p + kRatioRingPairs), lds_addr(rs));
+                glds16(csrc(p + RP), lds_addr(rs));
             }
             vmwait<0>();
             // no step replayed (first selection of a block on a finished band): the RHS cache
@@ -426,6 +428,22 @@ __device__ __forceinline__ void ratio_defer_body(
             release_go(st);
         }
     }
+    if (xp && xsel) {
+        // the selection in this workgroup (no select launch): wait for every rank's candidate of
+        // this exchange, reduce them in rank order, select (every rank reaches the same p)
+        __shared__ Cand s_xc[kMaxRanks];
+        __shared__ int s_xok;
+        if (!x_gather_cands(xp, xseq, s_xc, &s_xok)) {
+            if (threadIdx.x == 0) st->status = kStatusXFail;
+            return;
+        }
+        if (threadIdx.x == 0) {
+            Cand w = cand_empty();
+            for (int r = 0; r < xp->nranks; ++r)
+                if (cand_better(s_xc[r], w)) w = s_xc[r];
+            do_select(st, w, q, basis, row_first, rows, pricing, log, log_cap, true);
+        }
+    }
     if constexpr (LEAN) CHAIN_STAMP(slot, 6);
 }
 
@@ -437,15 +455,15 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
-    int prev_seal, const XPeers* xp, uint32_t xseq) {
+    int prev_seal, const XPeers* xp, uint32_t xseq, int xsel) {
     ratio_defer_body<KMAX, false>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                   ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                   tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
-                                  xp, xseq);
+                                  xp, xseq, nullptr, 1, 0, nullptr, xsel);
 }
 
 // The LEAN selection kernel, held to 32 VGPRs (lookahead at K = 64, beside the pass).
-template <int KMAX, int LCH>
+template <int KMAX, int LCH, int RP = kRatioRingPairs>
 __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(32))) void ratio_lean_kernel(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
@@ -453,11 +471,12 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
-    int prev_seal, const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn) {
-    ratio_defer_body<KMAX, false, true, LCH>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
+    int prev_seal, const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn,
+    int xsel) {
+    ratio_defer_body<KMAX, false, true, LCH, RP>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                         ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                         tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
-                                        xp, xseq, bcnt, brb, bnt, Tn);
+                                        xp, xseq, bcnt, brb, bnt, Tn, xsel);
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
@@ -500,15 +519,15 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
 // T0[p], divided by the pivot element (IEEE division).  fused (single rank):
 // commit_row as well.  Otherwise the owner writes the fp64 bits and every
 // other rank INT64_MIN for the int64 MAX exchange.
-constexpr int kProwRingSteps = 8;
-constexpr size_t kProwRing = 4 * kProwRingSteps * 128 * sizeof(double);
-template <bool LEAN>
+constexpr int kProwRingSteps = 8;   // (RS; 16 for tuning: DLP_RING_DEPTH=16)
+constexpr size_t prow_ring_bytes(int rs) { return (size_t)4 * rs * 128 * sizeof(double); }
+template <bool LEAN, int RS = kProwRingSteps>
 __device__ __forceinline__ void prow_defer_body(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
     int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
     int fused, const double* __restrict__ Cp, const double* __restrict__ Pp, int prev_seal,
-    const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn) {
+    const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn, int xcommit) {
     __shared__ PricePart lds_pp[4];
     __shared__ double s_cp[kMaxReplay];
     __shared__ int32_t s_pl[kMaxReplay];
@@ -518,7 +537,7 @@ __device__ __forceinline__ void prow_defer_body(
     // (launch-time LDS, kProwRing bytes: static LDS of that size makes hipcc's descriptor ask for
     // the VGPRs its LDS-bound occupancy would leave, 176, and the kernel no longer fits beside
     // the pass)
-    constexpr int RING = kProwRingSteps;
+    constexpr int RING = RS;
     extern __shared__ double s_dyn[];
     auto s_ring = reinterpret_cast<double(*)[RING][128]>(s_dyn);
     if (st->status != DLP_RUNNING) return;
@@ -631,6 +650,28 @@ __device__ __forceinline__ void prow_defer_body(
         if (pl >= 0)      // (uniform per launch)
             x_push_row_chunk(xp, xseq, j, ld, __builtin_bit_cast(uint64_t, px),
                              __builtin_bit_cast(uint64_t, py));
+        if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 11);
+        if (!xcommit) return;
+        // the commit in this launch (no commit launch): the owner commits the row it holds, every
+        // other rank waits for this chunk's flag and reads the chunk from its own row region
+        if (pl < 0) {
+            __shared__ int s_xok;
+            if (threadIdx.x == 0) s_xok = x_wait(xp, x_rflag(xp, xp->me, blockIdx.x), xseq) ? 1 : 0;
+            __syncthreads();
+            if (!s_xok) {
+                if (threadIdx.x == 0) const_cast<DevState*>(st)->status = kStatusXFail;   // (st is writable memory)
+                return;
+            }
+            if (j < ld) {
+                uint64_t a = 0, b = 0;
+                x_read_row_pair(xp, j, &a, &b);
+                pr.x = __builtin_bit_cast(double, a);
+                pr.y = __builtin_bit_cast(double, b);
+            }
+        }
+        if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 13);
+        commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap, lds_pp);
+        if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 14);
         return;
     }
     if (!fused) {
@@ -653,9 +694,9 @@ __device__ __forceinline__ void prow_defer_body(
         const double *__restrict__ C, int64_t ldc, double *__restrict__ P, int64_t *__restrict__ bits,  \
         PricePart *pp, double tol_dj, dlp_pivot *log, int64_t log_cap, int fused,                    \
         const double *__restrict__ Cp, const double *__restrict__ Pp, int prev_seal, const XPeers *xp, \
-        uint32_t xseq, uint32_t *bcnt, int brb, int bnt, const double *Tn
+        uint32_t xseq, uint32_t *bcnt, int brb, int bnt, const double *Tn, int xcommit
 #define DLP_PROW_PASS T, ld, rows, ncols, nprice, st, C, ldc, P, bits, pp, tol_dj, log, log_cap, fused, Cp, Pp, \
-                      prev_seal, xp, xseq, bcnt, brb, bnt, Tn
+                      prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xcommit
 // The LEAN instance (lookahead at K = 64, beside the form-21 pass) is held to 32 VGPRs in its
 // kernel descriptor: the pass leaves 32 per SIMD (with the LDS-DMA asm, hipcc's descriptor
 // otherwise requested 176 for a body that uses 30, and the kernel could not share a CU).
@@ -663,10 +704,9 @@ template <bool LEAN = false>
 __global__ __launch_bounds__(256) void prow_defer_kernel(DLP_PROW_ARGS) {
     prow_defer_body<false>(DLP_PROW_PASS);
 }
-template <>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void prow_defer_kernel<true>(
-    DLP_PROW_ARGS) {
-    prow_defer_body<true>(DLP_PROW_PASS);
+template <int RS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void prow_lean_kernel(DLP_PROW_ARGS) {
+    prow_defer_body<true, RS>(DLP_PROW_PASS);
 }
 #undef DLP_PROW_ARGS
 #undef DLP_PROW_PASS
@@ -680,6 +720,8 @@ __global__ __launch_bounds__(256) void commit_defer_kernel(
     __shared__ PricePart lds_pp[4];
     __shared__ int s_ok;
     if (st->status != DLP_RUNNING) return;
+    const int64_t slot = st->npivots - 1;
+    if (blockIdx.x == 0) CHAIN_STAMP(slot, 12);
     const int s = st->blk - 1;
     const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
     d2 pr;
@@ -688,18 +730,23 @@ __global__ __launch_bounds__(256) void commit_defer_kernel(
     if (xp) {   // peer exchange: this chunk's flag, then the row from this rank's region
         if (threadIdx.x == 0) s_ok = x_wait(xp, x_rflag(xp, xp->me, blockIdx.x), xseq) ? 1 : 0;
         __syncthreads();
+        if (blockIdx.x == 0) CHAIN_STAMP(slot, 13);
         if (!s_ok) {
             if (threadIdx.x == 0) st->status = kStatusXFail;
             return;
         }
-        const uint64_t* row = x_row(xp, xp->me);
-        if (j < ld) pr.x = __builtin_bit_cast(double, x_load(row + j));
-        if (j + 1 < ld) pr.y = __builtin_bit_cast(double, x_load(row + j + 1));
+        if (j < ld) {
+            uint64_t a = 0, b = 0;
+            x_read_row_pair(xp, j, &a, &b);
+            pr.x = __builtin_bit_cast(double, a);
+            pr.y = __builtin_bit_cast(double, b);
+        }
     } else if (j < ld) {
         pr = *(const d2*)(bits + j);
     }
     commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
                lds_pp);
+    if (blockIdx.x == 0) CHAIN_STAMP(slot, 14);
 }
 
 // Single rank: ratio test, selection and pivot row in ONE launch (saves a kernel
@@ -2110,6 +2157,13 @@ __global__ __launch_bounds__(64) void seal_kernel(DevState* st, int slot, uint32
 
 }  // namespace
 
+// LDS-ring depth of the LEAN chain kernels (tuning only: DLP_RING_DEPTH=16; default 8)
+static int ring_depth() {
+    static const int d = std::getenv("DLP_RING_DEPTH") ? std::atoi(std::getenv("DLP_RING_DEPTH")) : 8;
+    return d;
+}
+#define COMMA ,
+
 int ratio_defer_blocks(const Geometry& g) {
     return (int)((g.rows + 1 + kRatioDeferThreads - 1) / kRatioDeferThreads);
 }
@@ -2119,9 +2173,10 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
                               const Defer* prev, int prev_seal, const XPeers* xp, uint32_t xseq,
-                              const BandPub* bp) {
+                              const BandPub* bp, bool xfuse) {
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
+    xfuse = xfuse && xp && nranks > 1;
     if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
     nblocks = ratio_defer_blocks(g);
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
@@ -2132,7 +2187,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     ratio_defer_kernel<KM><<<nblocks, kRatioDeferThreads, 0, s>>>(                               \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, \
         d.Cc, d.ldcc, d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing,   \
-        log, log_cap, Ccp, Pp, prev_seal, xp, xseq)
+        log, log_cap, Ccp, Pp, prev_seal, xp, xseq, xfuse ? 1 : 0)
     if (steps <= 8)
         DLP_RATIO_DEFER(8);
     else if (steps <= 16)
@@ -2149,14 +2204,16 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
         d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
         xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,   \
-        pub ? bp->Tn : nullptr)
+        pub ? bp->Tn : nullptr, xfuse ? 1 : 0)
         // the LDS ring (0); 4 or 8 coefficient loads per round trip for tuning only (DLP_LEAN_LCH)
         if (lch == 8)
             DLP_RATIO_LEAN(8, 0);
         else if (lch == 4)
             DLP_RATIO_LEAN(4, 0);
+        else if (ring_depth() == 16)
+            DLP_RATIO_LEAN(0 COMMA 16, ratio_ring_bytes(16));
         else
-            DLP_RATIO_LEAN(0, kRatioRing);
+            DLP_RATIO_LEAN(0, ratio_ring_bytes(kRatioRingPairs));
 #undef DLP_RATIO_LEAN
     }
 #undef DLP_RATIO_DEFER
@@ -2208,22 +2265,30 @@ int fused_pivot_capacity(int K, int cus) {
 hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* st,
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
                              int64_t log_cap, int nranks, hipStream_t s, const Defer* prev,
-                             int prev_seal, const XPeers* xp, uint32_t xseq, const BandPub* bp) {
+                             int prev_seal, const XPeers* xp, uint32_t xseq, const BandPub* bp,
+                             bool xfuse) {
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
+    const int xc = (xfuse && xp && nranks > 1) ? 1 : 0;
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
-    if (prev_seal >= 0 && d.K > 32)   // lookahead at K = 64: beside the form-21 pass
-        prow_defer_kernel<true><<<blocks, 256, kProwRing, s>>>(
-            g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap,
-            nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal, nranks == 1 ? nullptr : xp, xseq,
-            pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,
-            pub ? bp->Tn : nullptr);
-    else
+    if (prev_seal >= 0 && d.K > 32) {   // lookahead at K = 64: beside the form-21 pass
+#define DLP_PROW_LEAN(RS)                                                                                  \
+    prow_lean_kernel<RS><<<blocks, 256, prow_ring_bytes(RS), s>>>(                                          \
+        g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap,     \
+        nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal, nranks == 1 ? nullptr : xp, xseq,                \
+        pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,           \
+        pub ? bp->Tn : nullptr, xc)
+        if (ring_depth() == 16)
+            DLP_PROW_LEAN(16);
+        else
+            DLP_PROW_LEAN(kProwRingSteps);
+#undef DLP_PROW_LEAN
+    } else
         prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,
                                                  d.P, prow_bits, pp, tol_dj, log, log_cap,
                                                  nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
                                                  prev_seal >= 0 ? prev->P : nullptr, prev_seal,
-                                                 nranks == 1 ? nullptr : xp, xseq, nullptr, 1, 0, nullptr);
+                                                 nranks == 1 ? nullptr : xp, xseq, nullptr, 1, 0, nullptr, xc);
     return hipGetLastError();
 }
 

@@ -5,6 +5,7 @@
 #pragma once
 
 typedef double d2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u4x __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------- reductions
 __device__ inline void pp_combine(PricePart& a, const PricePart& b) {
@@ -138,10 +139,14 @@ __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* ba
 
 
 // ------------------------------------------------------------- peer exchange
-// (dlp_internal.h, XPeers).  System-scope relaxed atomics: the stores are written
-// through to memory, the loads are served from memory (the blocks are uncached), so a
-// message written by another device (xGMI) or by another XCD is seen once its flag is.
-constexpr uint64_t kXWaitTicks = 30ull * 100000000ull;   // 30 s of the 100 MHz constant clock
+// (dlp_internal.h, XPeers).  Every store of a message is a system-scope (sc0 sc1) store into an
+// uncached block: written through to its memory, local or across xGMI, and complete once the
+// storing wave's vmcnt has drained.  So a message is published by: its stores, every storing
+// wave's s_waitcnt vmcnt(0), a workgroup barrier where several waves stored, then ONE flag
+// store (the "drained" form: MI355X_MICROARCH.md, inter-workgroup visibility, {sc0 sc1 stores
+// and loads both sides}), and read by sc0 sc1 loads after the flag matched.  No release fence:
+// on gfx950 a system-scope fence is an L2 write-back + invalidate of the whole XCD L2 (the
+// pass's dirty lines included), which the drained form does not need.
 
 __device__ inline void x_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -149,7 +154,11 @@ __device__ inline void x_store(uint64_t* p, uint64_t v) {
 __device__ inline uint64_t x_load(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// Bounded wait for *flag == seq: false on timeout or when the host raised the abort word.
+// This wave's system-scope stores complete (the drained form above).
+__device__ inline void x_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+constexpr int kXAux = 1 | 16;   // buffer-op cache policy sc0 sc1 (system scope)
+// Bounded wait for *flag == seq: false after xp->wait_ticks (the session's exchange timeout + 5 s;
+// 0 = no bound of its own) or when the host raised the abort word.
 __device__ inline bool x_wait(const XPeers* xp, const uint64_t* flag, uint64_t seq) {
     if (x_load(flag) == seq) return true;
     const uint64_t t0 = wall_clock64();
@@ -160,7 +169,7 @@ __device__ inline bool x_wait(const XPeers* xp, const uint64_t* flag, uint64_t s
             if (xp->abort_word &&
                 __hip_atomic_load(xp->abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
                 return false;
-            if (wall_clock64() - t0 > kXWaitTicks) return false;
+            if (xp->wait_ticks && wall_clock64() - t0 > xp->wait_ticks) return false;
         }
     }
 }
@@ -184,7 +193,7 @@ __device__ inline void x_push_cand(const XPeers* xp, uint32_t seq, const Cand& c
 #pragma unroll
         for (int k = 0; k < 4; ++k) x_store(slot + k, cv[k]);
     }
-    __threadfence_system();   // the slots reach memory before any flag
+    x_drain();   // the slots are complete before any flag
     for (int r = 0; r < xp->nranks; ++r) x_store(x_cflag(xp, r, par, xp->me), seq);
 }
 
@@ -209,16 +218,35 @@ __device__ inline bool x_gather_cands(const XPeers* xp, uint32_t seq, Cand* lds,
 }
 
 // Workgroup of 256 lanes, chunk = blockIdx.x (512 columns, 2 per lane from column j):
-// the owner's row values (v0, v1) into every rank's row region, then the chunk flags.
+// the owner's row values (v0, v1) into every rank's row region (one 16-B sc0 sc1 store per lane
+// and rank; j is even and the region 4 KiB aligned and padded to whole chunks), then, once every
+// wave has drained its stores, the chunk flags.
 __device__ inline void x_push_row_chunk(const XPeers* xp, uint32_t seq, int64_t j, int64_t ld,
                                         uint64_t v0, uint64_t v1) {
-    if (j < ld)
+    if (j < ld) {
+        u4x v;
+        v.x = (uint32_t)v0;
+        v.y = (uint32_t)(v0 >> 32);
+        v.z = (uint32_t)v1;
+        v.w = (uint32_t)(v1 >> 32);
         for (int r = 0; r < xp->nranks; ++r) {
-            uint64_t* row = x_row(xp, r);
-            x_store(row + j, v0);
-            if (j + 1 < ld) x_store(row + j + 1, v1);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)x_row(xp, r), (short)0, (int)(xp->nchunks * kXChunk * 8), 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(j * 8), 0, kXAux);
         }
-    __threadfence_system();   // every lane's stores reach memory before the flags
+    }
+    x_drain();
     __syncthreads();
     for (int r = threadIdx.x; r < xp->nranks; r += blockDim.x) x_store(x_rflag(xp, r, blockIdx.x), seq);
+}
+
+// Lane j of a chunk (j even): the two row words of this rank's region (one 16-B sc0 sc1 load),
+// once the chunk's flag has been seen.
+__device__ inline void x_read_row_pair(const XPeers* xp, int64_t j, uint64_t* v0, uint64_t* v1) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)x_row(xp, xp->me), (short)0, (int)(xp->nchunks * kXChunk * 8), 0x00020000);
+    const u4x v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(j * 8), 0, kXAux);
+    const uint32_t a = v.x, b = v.y, c = v.z, d = v.w;   // (scalars: no element bit-casts)
+    *v0 = (uint64_t)a | ((uint64_t)b << 32);
+    *v1 = (uint64_t)c | ((uint64_t)d << 32);
 }

@@ -95,8 +95,9 @@ __host__ __device__ inline bool cand_better(const Cand& a, const Cand& b) {
 //   [off_cslot, +8P)           candidate slots  cslot[parity][sender]  (4 words = 32 B)
 //   [off_rflag, +nchunks)      pivot-row chunk flags (512 columns per chunk)
 //   [off_row, +ld)             the pivot row (fp64 bits), written by its owner
-// Every wait is bounded (kXWaitTicks of the 100 MHz constant clock, or the host's abort
-// word): a stall sets DevState.status = kStatusXFail and the host returns DLP_ERR_HIP.
+// Every wait is bounded (wait_ticks of the 100 MHz constant clock: the host's exchange timeout
+// + 5 s, 0 = none; and the host's abort word): a stall sets DevState.status = kStatusXFail and
+// the host returns DLP_ERR_RCCL, as for every exchange failure.
 constexpr int kMaxRanks = 64;
 constexpr int kXChunk = 512;                       // pivot-row chunk (= prow / commit workgroup)
 constexpr int32_t kStatusXFail = 6;                // DevState.status: a peer exchange timed out
@@ -104,6 +105,7 @@ struct XPeers {
     uint64_t* base[kMaxRanks];   // every rank's exchange block as this device addresses it
     const uint32_t* abort_word;  // host-pinned; nonzero ends every wait (dlp_session_abort)
     int32_t nranks, me;
+    uint64_t wait_ticks;         // bound of one wait (0: the abort word only)
     int64_t nchunks;
     int64_t off_cslot, off_rflag, off_row;
 };
@@ -216,7 +218,14 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
                               const Defer* prev = nullptr, int prev_seal = -1,
-                              const XPeers* xp = nullptr, uint32_t seq = 0, const BandPub* bp = nullptr);
+                              const XPeers* xp = nullptr, uint32_t seq = 0, const BandPub* bp = nullptr,
+                              bool xfuse = false);
+// xfuse (peer exchange, nranks > 1): the last workgroup also waits for every rank's candidate and
+// selects (no select launch); launch_prow_defer's xfuse: the pivot-row launch also commits the
+// exchanged row (no commit launch).  Only where each rank's launches run on hardware queues of
+// their own (one rank per device or process): a wait inside a launch is then never queued behind
+// the launch of another rank that it waits for (dlp_sessions_run of ranks sharing a device does not
+// fuse).
 // nranks == 1: ratio test + selection + pivot row + objective row + pricing in ONE launch
 // (K <= 32; grid of fused_pivot_blocks(g), all of which must be resident at once).
 int fused_pivot_blocks(const Geometry& g);
@@ -233,7 +242,8 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
                              int64_t log_cap, int nranks, hipStream_t s,
                              const Defer* prev = nullptr, int prev_seal = -1,
-                             const XPeers* xp = nullptr, uint32_t seq = 0, const BandPub* bp = nullptr);
+                             const XPeers* xp = nullptr, uint32_t seq = 0, const BandPub* bp = nullptr,
+                             bool xfuse = false);
 // nranks > 1, after the MAX all-reduce: P[s] from the exchanged bits + objective row + pricing.
 // xp: each workgroup first waits for its chunk's flag (seq), then reads the row region
 // with system-scope loads (prow_bits = this rank's row region).

@@ -221,9 +221,12 @@ __global__ __launch_bounds__(256) void xrow_recv_kernel(const XPeers* xp, uint32
         return;
     }
     const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
-    const uint64_t* row = x_row(xp, xp->me);
-    if (j < ld) out[j] = (int64_t)x_load(row + j);
-    if (j + 1 < ld) out[j + 1] = (int64_t)x_load(row + j + 1);
+    if (j < ld) {   // (ld is a multiple of 16: j + 1 < ld)
+        uint64_t a = 0, b = 0;
+        x_read_row_pair(xp, j, &a, &b);
+        out[j] = (int64_t)a;
+        out[j + 1] = (int64_t)b;
+    }
 }
 
 // ---- general LPs: Phase I -> Phase II transition (include/dlp.h, "general LPs")

@@ -84,7 +84,7 @@ struct dlp_session {
     // X_RCCL = all-gather + MAX all-reduce, X_PEER = direct stores into the ranks'
     // exchange blocks (dlp_sessions_connect / dlp_session_connect_ipc /
     // dlp_session_set_exchange)
-    enum XMode { X_HOST = 0, X_RCCL = 1, X_PEER = 2 };
+    enum XMode { X_RCCL = DLP_XCHG_RCCL, X_PEER = DLP_XCHG_PEER, X_HOST = DLP_XCHG_HOST };
     int xmode = X_HOST;
     uint64_t* xblk = nullptr;            // this rank's exchange block (uncached device memory)
     bool xblk_uncached = false;
@@ -162,6 +162,15 @@ struct dlp_session {
     hipStream_t pstream = nullptr;
     hipEvent_t ev_seal = nullptr, ev_pass = nullptr;
     int prio_chain = 0, prio_pass = 0;   // the two streams' priorities (stream pool key)
+    // auto policies: lookahead (opt.lookahead < 0) and the pass form (no set_defer_tuning form);
+    // an exchange session's lookahead follows its exchange (la_policy)
+    bool la_auto = false;
+    bool form_auto = true;
+    // peer exchange, deferred: the selection inside the ratio launch and the commit inside the
+    // pivot-row launch (dlp::launch_ratio_defer's xfuse); off while dlp_sessions_run drives ranks
+    // that share a device (their phases must stay in separate launches)
+    bool xfuse = true;
+    std::string xreason;   // why an auto exchange fell back to RCCL (empty: it did not)
 };
 
 extern "C" int flush_pending(dlp_session* s);   // defined with the C entry points
@@ -378,10 +387,90 @@ int validate_options(const dlp_options* o) {
         set_error("invalid tolerance / pivot limit / check interval");
         return DLP_ERR_ARG;
     }
-    if (o->exchange != 0 && o->exchange != DLP_XCHG_RCCL && o->exchange != DLP_XCHG_PEER) {
-        set_error("exchange must be 0, DLP_XCHG_RCCL or DLP_XCHG_PEER");
+    if (o->exchange != DLP_XCHG_DEFAULT && o->exchange != DLP_XCHG_RCCL && o->exchange != DLP_XCHG_PEER) {
+        set_error("exchange must be DLP_XCHG_DEFAULT, DLP_XCHG_RCCL or DLP_XCHG_PEER");
         return DLP_ERR_ARG;
     }
+    return DLP_OK;
+}
+
+// The K = 64 streaming pass form, when the caller has not set one: form 21 (DPP coefficients
+// from registers) under lookahead, form 23 (LDS ring) with nothing beside the pass: C3 7.9 vs
+// 8.2 ms per pass in situ without lookahead, but under lookahead the ring's deeper memory queue
+// slows the selection chain beside it more than it speeds the pass (C3 6,578 vs 7,685 pivots/s,
+// profiles/r03d/)
+void pick_form(dlp_session* s) {
+    if (!s->form_auto || s->d.K != 64 || !s->streaming || (s->d.form != 21 && s->d.form != 23)) return;
+    s->d.form = s->la ? 21 : 23;
+    s->dslot[0].form = s->dslot[1].form = s->d.form;
+}
+
+int flush_pending_block(dlp_session* s);
+
+// Lookahead on: a second tableau buffer holding the same bytes, a second set of
+// block arrays (rhs shared), band counters, the pass stream.  Called at session creation or
+// between runs (la_policy): a pending block is applied first.  Silently stays off where it does
+// not apply (the form has no out-of-place pass, general LPs, the small-LP launch, per-phase
+// timing, a host-driven rank unless forced, too little free memory).
+int la_enable(dlp_session* s, bool forced) {
+    if (s->la) return DLP_OK;
+    const bool host_driven = s->nranks > 1 && !s->use_rccl && s->xmode != dlp_session::X_PEER;
+    bool ok = s->d.K > 1 && 2 * s->d.K <= dlp::kMaxReplay && dlp::lookahead_form(s->d.form) &&
+              !s->general && !s->cluster && (!host_driven || forced) && s->opt.timing < 2;
+    const size_t tbytes = (size_t)(s->rows + 1) * s->ld * sizeof(double);
+    size_t freeb = 0, totalb = 0;
+    if (ok && hipMemGetInfo(&freeb, &totalb) == hipSuccess)
+        ok = (s->Tb[1] ? freeb + tbytes : freeb) > tbytes + tbytes / 8 + ((size_t)1 << 30);
+    else
+        ok = false;
+    if (!ok) return DLP_OK;
+    CALL_TRY(flush_pending_block(s));
+    const int c = (s->Tb[1] && s->T == s->Tb[1]) ? 1 : 0;   // the current buffer
+    if (!s->Tb[0]) s->Tb[0] = s->T;
+    if (!s->Tb[1 - c] && hipMalloc(&s->Tb[1 - c], tbytes) != hipSuccess) {
+        set_error("hipMalloc of the second tableau buffer failed");
+        return DLP_ERR_OOM;
+    }
+    // the whole buffer, padding included, so both hold the same bytes everywhere
+    HIP_TRY(hipMemcpyAsync(s->Tb[1 - c], s->Tb[c], tbytes, hipMemcpyDeviceToDevice, s->stream));
+    s->tread = s->tcur = s->zbuf = c;
+    s->cur = 0;
+    s->la_pending = false;
+    const dlp::Defer keep1 = s->dslot[1];
+    s->dslot[0] = s->d;
+    s->dslot[1] = s->d;
+    dlp::Defer& d1 = s->dslot[1];
+    const int64_t rows_total = s->rows + 1;
+    if (keep1.C) {   // arrays of an earlier lookahead period (their stale contents are never read)
+        d1.C = keep1.C;
+        d1.Cc = keep1.Cc;
+        d1.P = keep1.P;
+        d1.nzc = keep1.nzc;
+    } else {
+        const int64_t kt = s->d.K <= 4 ? 4 : s->d.K <= 8 ? 8 : s->d.K <= 16 ? 16 : s->d.K <= 32 ? 32 : 64;
+        d1.C = d1.Cc = d1.P = nullptr;
+        d1.nzc = nullptr;
+        HIP_TRY(hipMalloc(&d1.C, sizeof(double) * s->d.K * (rows_total + 1)));
+        HIP_TRY(hipMalloc(&d1.Cc, sizeof(double) * s->d.K * s->d.ldcc));
+        HIP_TRY(hipMalloc(&d1.P, sizeof(double) * kt * s->ld));
+        HIP_TRY(hipMalloc(&d1.nzc, sizeof(int32_t) * (s->rows + 1)));
+        HIP_TRY(hipMemsetAsync(d1.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
+        HIP_TRY(hipMemsetAsync(d1.Cc, 0, sizeof(double) * s->d.K * s->d.ldcc, s->stream));
+        HIP_TRY(hipMemsetAsync(d1.P, 0, sizeof(double) * kt * s->ld, s->stream));
+    }
+    if (!s->band_cnt) {
+        s->band_stride = (s->rows + 63) / 64 + 1;   // bands of >= 64 rows
+        HIP_TRY(hipMalloc(&s->band_cnt, sizeof(uint32_t) * 2 * s->band_stride));
+    }
+    HIP_TRY(hipMemsetAsync(s->band_cnt, 0, sizeof(uint32_t) * 2 * s->band_stride, s->stream));
+    if (!s->pstream) HIP_TRY(acquire_stream(s->device, s->prio_pass, &s->pstream));
+    if (!s->ev_seal) HIP_TRY(hipEventCreateWithFlags(&s->ev_seal, hipEventDisableTiming));
+    if (!s->ev_pass) HIP_TRY(hipEventCreateWithFlags(&s->ev_pass, hipEventDisableTiming));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->la = true;
+    s->opt.lookahead = 1;
+    if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
+    if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
     return DLP_OK;
 }
 
@@ -635,68 +724,16 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     s->Tb[0] = s->T;
     clk.mark("create: fill + state");
 
-    // lookahead: deferred, a pass form with an out-of-place instance, the exchange (if
-    // any) driven by the session, no per-phase timing, and room for a second tableau
-    {
-        // (a multi-rank session without an id: only when asked for, as it runs only once its
-        // ranks are connected by the peer exchange; the step API turns it off)
-        const bool host_driven = nranks > 1 && !rccl;
-        bool ok = s->d.K > 1 && 2 * s->d.K <= dlp::kMaxReplay && dlp::lookahead_form(s->d.form) &&
-                  !s->general && !s->cluster && (!host_driven || opt->lookahead == 1) && opt->timing < 2;
-        size_t freeb = 0, totalb = 0;
-        if (ok && hipMemGetInfo(&freeb, &totalb) == hipSuccess)
-            ok = freeb > tbytes + tbytes / 8 + ((size_t)1 << 30);
-        else
-            ok = false;
-        // auto: from 4 GiB of tableau, where the pass is several times the pivot chain it
-        // hides (C3 17 GB: 4,492 -> 4,935 pivots/s).  Below that the chain, slowed by
-        // the concurrent pass and by replaying two blocks, costs more than the pass it
-        // hides (C2 268 MB: 39.0k -> 30.2k; profiles/r02h/)
-        // At K = 64 the selections replay up to 127 steps through the LEAN kernels (23 and
-        // 21 VGPRs), which fit beside the form-21 pass (3 waves x 160 VGPRs per SIMD); the
-        // 256-VGPR chain kernel waited for pass workgroups to drain instead (C3: lookahead
-        // 6,715 vs 5,970 pivots/s off; 5,473 with the fat kernel; profiles/r02j/)
-        // Multi-rank: auto off.  The per-pivot RCCL kernels of the exchange need more registers
-        // than the form-21 pass leaves free on a CU, so under lookahead each collective would
-        // wait for pass workgroups to drain, as the fat selection kernel did (forced on, the
-        // 1-rank RCCL path is tested: tests/test_gpu_lookahead.py)
-        const bool want = opt->lookahead == 1 ||
-                          (opt->lookahead < 0 && tbytes >= ((size_t)4 << 30) && nranks == 1);
-        if (ok && want) {
-            if (hipMalloc(&s->Tb[1], tbytes) != hipSuccess) {
-                set_error("hipMalloc of the second tableau buffer failed");
-                return DLP_ERR_OOM;
-            }
-            // the whole buffer, padding included, so both hold the same bytes everywhere
-            HIP_TRY(hipMemcpyAsync(s->Tb[1], s->Tb[0], tbytes, hipMemcpyDeviceToDevice, s->stream));
-            s->dslot[0] = s->d;
-            s->dslot[1] = s->d;
-            dlp::Defer& d1 = s->dslot[1];
-            const int64_t kt = s->d.K <= 4 ? 4 : s->d.K <= 8 ? 8 : s->d.K <= 16 ? 16 : s->d.K <= 32 ? 32 : 64;
-            HIP_TRY(hipMalloc(&d1.C, sizeof(double) * s->d.K * (rows_total + 1)));
-            HIP_TRY(hipMalloc(&d1.Cc, sizeof(double) * s->d.K * s->d.ldcc));
-            HIP_TRY(hipMalloc(&d1.P, sizeof(double) * kt * s->ld));
-            HIP_TRY(hipMalloc(&d1.nzc, sizeof(int32_t) * (s->rows + 1)));
-            HIP_TRY(hipMemsetAsync(d1.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
-            HIP_TRY(hipMemsetAsync(d1.Cc, 0, sizeof(double) * s->d.K * s->d.ldcc, s->stream));
-            HIP_TRY(hipMemsetAsync(d1.P, 0, sizeof(double) * kt * s->ld, s->stream));
-            s->band_stride = (s->rows + 63) / 64 + 1;   // bands of >= 64 rows
-            HIP_TRY(hipMalloc(&s->band_cnt, sizeof(uint32_t) * 2 * s->band_stride));
-            HIP_TRY(hipMemsetAsync(s->band_cnt, 0, sizeof(uint32_t) * 2 * s->band_stride, s->stream));
-            HIP_TRY(acquire_stream(s->device, prio_least, &s->pstream));
-            HIP_TRY(hipEventCreateWithFlags(&s->ev_seal, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&s->ev_pass, hipEventDisableTiming));
-            HIP_TRY(hipStreamSynchronize(s->stream));
-            s->la = true;
-        }
-        s->opt.lookahead = s->la ? 1 : 0;
-        // a K = 64 streaming pass with nothing beside it (no lookahead: a multi-rank session,
-        // or lookahead off) streams its rows through the LDS ring (form 23: C3 7.9 vs 8.2 ms
-        // per pass in situ, 7.3 in the lab).  Under lookahead form 21 stays: the ring's
-        // deeper memory queue slows the selection chain beside it more than it speeds the pass
-        // (C3 6,578 vs 7,685 pivots/s, profiles/r03d/)
-        if (s->d.form == 21 && s->d.K == 64 && s->streaming && !s->la) s->d.form = 23;
-    }
+    // lookahead: forced on, or auto on a single-rank tableau of >= 4 GiB, where
+    // the pass is several times the pivot chain it hides (C3 17 GB: 4,492 -> 4,935 pivots/s).
+    // Below that the chain, slowed by the concurrent pass and by replaying two blocks, costs more
+    // than the pass it hides (C2 268 MB: 39.0k -> 30.2k; profiles/r02h/).  An exchange session
+    // decides once its exchange is known (la_policy): on with the peer exchange, off with RCCL.
+    s->la_auto = opt->lookahead < 0;
+    if (opt->lookahead == 1 || (s->la_auto && !s->exchange && tbytes >= ((size_t)4 << 30)))
+        CALL_TRY(la_enable(s, opt->lookahead == 1));
+    s->opt.lookahead = s->la ? 1 : 0;
+    pick_form(s);
 
     if (comm_in) {
         s->comm = comm_in;
@@ -833,6 +870,28 @@ int la_disable(dlp_session* s) {
     s->d.form = form;
     s->la = false;
     s->opt.lookahead = 0;
+    pick_form(s);
+    return DLP_OK;
+}
+
+// The single-buffer path's pending block applied (la_enable's precondition).
+int flush_pending_block(dlp_session* s) {
+    if (!s->la && s->d.K > 1 && s->since_flush > 0) CALL_TRY(enqueue_flush(s));
+    return DLP_OK;
+}
+
+// An exchange session's auto lookahead, once its exchange is known (creation, connect,
+// dlp_session_set_exchange; between runs): on with the peer exchange at K = 64 on a streaming
+// rank tableau, where every per-pivot kernel fits beside the form-21 pass (select, commit and
+// the LEAN ratio / pivot-row kernels: <= 32 VGPRs, tests/test_isa.py); off with RCCL, whose
+// collective kernels need more registers than the pass leaves on a CU and would each wait for
+// pass workgroups to drain.  A caller's explicit lookahead setting is kept.
+int la_policy(dlp_session* s) {
+    if (!s->la_auto || !s->exchange) return DLP_OK;
+    const bool want = s->xmode == dlp_session::X_PEER && s->d.K == 64 && s->streaming && !s->general;
+    if (want && !s->la) CALL_TRY(la_enable(s, false));
+    if (!want && s->la) CALL_TRY(la_disable(s));
+    pick_form(s);
     return DLP_OK;
 }
 
@@ -851,6 +910,7 @@ inline const dlp::XPeers* xp_of(const dlp_session* s) {
 int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     const dlp_options& o = s->opt;
     const dlp::XPeers* xp = xp_of(s);
+    const bool xf = xp && s->xfuse && s->nranks > 1;   // selection + commit inside the chain launches
     // timing 2: 5 events per pivot (every phase); timing 1: 2 events around the pass only
     hipEvent_t* ev = s->ev_per_pivot == 5 ? &s->ev[(size_t)slot * 5] : nullptr;
     hipEvent_t* evp = s->ev_per_pivot == 2 ? &s->ev[(size_t)slot * 2] : nullptr;
@@ -881,7 +941,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         HIP_TRY(dlp::launch_ratio_defer(gsel, *dcur, s->basis, s->pp, s->st, s->partials,
                                         s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
                                         o.tol_piv, o.pricing, s->log, s->log_cap, s->stream, dprev,
-                                        pseal, xp, s->xseq_c, &bp));
+                                        pseal, xp, s->xseq_c, &bp, xf));
         if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
         if (s->xmode == dlp_session::X_RCCL)
             NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,
@@ -890,20 +950,20 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     }
     if (phase == 1) {
         if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) return DLP_OK;
-        if (s->exchange)
+        if (s->exchange && !xf)
             HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, o.pricing,
                                        s->log, s->log_cap, s->stream, false, true, xp, s->xseq_c));
         if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
         if (xp) s->xseq_r += 1;
         HIP_TRY(dlp::launch_prow_defer(gsel, *dcur, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
                                        s->log_cap, s->exchange ? 2 : 1, s->stream, dprev, pseal, xp,
-                                       s->xseq_r, &bp));
+                                       s->xseq_r, &bp, xf));
         if (s->xmode == dlp_session::X_RCCL)
             NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
                                    s->comm, s->stream));
         return DLP_OK;
     }
-    if (s->exchange)
+    if (s->exchange && !xf)
         HIP_TRY(dlp::launch_commit_defer(gsel, *dcur, s->st, s->prow_recv, s->pp, o.tol_dj, s->log,
                                          s->log_cap, s->stream, xp, s->xseq_r));
     if (ev) HIP_TRY(hipEventRecord(ev[3], s->stream));
@@ -1168,9 +1228,10 @@ int wait_stream(dlp_session* s) {
     for (int64_t spin = 0;; ++spin) {
         const hipError_t e = hipStreamQuery(s->stream);
         if (e == hipSuccess) return DLP_OK;
-        if (e != hipErrorNotReady) {
-            set_error(std::string("hipStreamQuery: ") + hipGetErrorString(e));
+        if (e != hipErrorNotReady) {   // a device error, not an exchange one: DLP_ERR_HIP
             (void)abort_exchange(s, hipGetErrorString(e));
+            s->status = DLP_ERR_HIP;
+            set_error(std::string("hipStreamQuery: ") + hipGetErrorString(e));
             return DLP_ERR_HIP;
         }
         if (s->abort_req.load(std::memory_order_relaxed)) return abort_exchange(s, "dlp_session_abort");
@@ -1186,7 +1247,8 @@ int wait_stream(dlp_session* s) {
         }
         const double el = std::chrono::duration<double>(clk::now() - t0).count();
         if (s->stall_limit_s > 0 && el > s->stall_limit_s)
-            return abort_exchange(s, "no progress for " + std::to_string(el) + " s");
+            return abort_exchange(s, "window not complete after " + std::to_string(el) +
+                                         " s (exchange timeout)");
         if (spin < 2000)
             std::this_thread::yield();
         else
@@ -1201,11 +1263,11 @@ int poll(dlp_session* s) {
                            s->stream));
     CALL_TRY(wait_stream(s));
     s->npivots = s->host_st->npivots;
-    if (s->host_st->status == dlp::kStatusXFail) {
-        s->status = DLP_ERR_HIP;
-        set_error("peer exchange: a wait for another rank timed out or was aborted (rank " +
+    if (s->host_st->status == dlp::kStatusXFail) {   // an exchange failure, as every other one
+        s->status = DLP_ERR_RCCL;
+        set_error("exchange aborted: a peer-exchange wait for another rank timed out or was aborted (rank " +
                   std::to_string(s->rank) + ")");
-        return DLP_ERR_HIP;
+        return DLP_ERR_RCCL;
     }
     if (s->host_st->status != DLP_RUNNING && s->host_st->status != dlp::kStatusSkip &&
         s->status == DLP_RUNNING)
@@ -1463,8 +1525,23 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
         return DLP_OK;
     });
     // owner-rooted peer exchange: every rank's block addressed directly (peer access between
-    // the devices, no IPC inside one process); the communicators stay for set-up only
-    if (res == DLP_OK && o.exchange == DLP_XCHG_PEER) res = dlp_sessions_connect(ss.data(), P);
+    // the devices, no IPC inside one process); auto (DLP_XCHG_DEFAULT) falls back to RCCL when
+    // the devices cannot connect; then each rank's auto lookahead follows its exchange
+    std::string xwhy;
+    if (res == DLP_OK && (o.exchange == DLP_XCHG_PEER || o.exchange == DLP_XCHG_DEFAULT)) {
+        res = dlp_sessions_connect(ss.data(), P);
+        if (res != DLP_OK && o.exchange == DLP_XCHG_DEFAULT) {
+            xwhy = dlp_last_error();
+            res = DLP_OK;
+            for (dlp_session* s : ss) s->xmode = dlp_session::X_RCCL;
+        }
+    }
+    if (res == DLP_OK)
+        res = on_ranks([&](int r) {
+            ss[r]->xreason = xwhy;
+            HIP_TRY(hipSetDevice(ss[r]->device));
+            return la_policy(ss[r]);
+        });
     if (res == DLP_OK) {
         res = on_ranks([&](int r) {
             if (const char* e = std::getenv("DLP_TEST_FAIL_RANK"))   // tests: fail this rank's 2nd poll
@@ -1485,6 +1562,18 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
                 delete r;
         }
     }
+    // No rank's exchange block may be freed while another rank's kernels can still push into
+    // it: after a failure every rank's device waits are ended (abort words), then every stream
+    // drains, and only then is anything freed.
+    if (res != DLP_OK)
+        for (auto* s : ss)
+            if (s && s->xabort) __atomic_store_n(s->xabort, 1u, __ATOMIC_SEQ_CST);
+    for (auto* s : ss)
+        if (s) {
+            (void)hipSetDevice(s->device);
+            if (s->stream) (void)hipStreamSynchronize(s->stream);
+            if (s->pstream) (void)hipStreamSynchronize(s->pstream);
+        }
     for (auto* s : ss)
         if (s) free_session(s);
     for (auto c : comms)
@@ -1524,12 +1613,19 @@ int ensure_xblock(dlp_session* s) {
     return DLP_OK;
 }
 
+// Device-side bound of one peer-exchange wait (100 MHz constant clock): the host's window limit
+// plus 5 s, so that the host (which reports why) acts first; 0 = wait on the abort word only.
+uint64_t xwait_ticks(double stall_limit_s) {
+    return stall_limit_s > 0 ? (uint64_t)((stall_limit_s + 5.0) * 1e8) : 0;
+}
+
 // Install the peer table (bases[r] = rank r's block as this device addresses it).
 int install_peers(dlp_session* s, const std::vector<uint64_t*>& bases) {
     dlp::XPeers& x = s->xpeers_host;
     (void)dlp::xblock_layout(s->nranks, s->ld, &x);
     for (int r = 0; r < dlp::kMaxRanks; ++r) x.base[r] = r < (int)bases.size() ? bases[r] : nullptr;
     x.me = s->rank;
+    x.wait_ticks = xwait_ticks(s->stall_limit_s);
     void* dabort = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dabort, s->xabort, 0));
     x.abort_word = (const uint32_t*)dabort;
@@ -1558,7 +1654,162 @@ int connect_ipc(dlp_session* s, const uint8_t* handles) {
         s->ipc_open.push_back(p);
         bases[r] = (uint64_t*)p;
     }
+    CALL_TRY(install_peers(s, bases));
+    return la_policy(s);
+}
+
+// ---- choosing the exchange over the communicator --------------------
+// Every rank's record, all-gathered: its exchange block's IPC handle, whether it could make
+// one, the PCI bus id of its device (mapped to this process's ordinals, so peer access is
+// checked for the devices really involved) and the reason when not.
+struct XRec {
+    uint8_t handle[64];
+    int32_t ok;
+    int32_t pad;
+    char bus[32];
+    char why[152];
+};
+static_assert(sizeof(XRec) == 256, "XRec is 256 bytes");
+
+// All-gather `bytes` per rank over the session's communicator (a blocking collective with
+// the window wait's failure containment).
+int comm_allgather(dlp_session* s, const void* mine, void* all, size_t bytes) {
+    uint8_t* dbuf = nullptr;
+    HIP_TRY(hipMalloc(&dbuf, bytes * (s->nranks + 1)));
+    int rc = DLP_OK;
+    if (hipMemcpy(dbuf + bytes * s->nranks, mine, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("hipMemcpy (exchange set-up)");
+        rc = DLP_ERR_HIP;
+    }
+    if (rc == DLP_OK) {
+        const ncclResult_t nr = ncclAllGather(dbuf + bytes * s->nranks, dbuf, bytes, ncclUint8, s->comm, s->stream);
+        if (nr != ncclSuccess) {
+            set_error(std::string("ncclAllGather (exchange set-up): ") + ncclGetErrorString(nr));
+            rc = DLP_ERR_RCCL;
+        }
+    }
+    if (rc == DLP_OK) rc = wait_stream(s);
+    if (rc == DLP_OK && hipMemcpy(all, dbuf, bytes * s->nranks, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("hipMemcpy (exchange set-up)");
+        rc = DLP_ERR_HIP;
+    }
+    (void)hipFree(dbuf);
+    return rc;
+}
+
+// Owner-rooted peer exchange over the communicator, agreed by every rank: each rank makes its
+// block and IPC handle, the records are all-gathered, each rank checks peer access to every
+// other rank's device and opens their blocks, and a second all-gather agrees on the outcome.
+// DLP_ERR_UNSUPPORTED (on every rank alike, *why set, nothing installed) when any rank could
+// not; other errors are failures of the communicator itself.  DLP_TEST_PEER_FAIL=<rank>
+// (tests only) makes that rank report a failure.
+int peer_connect_collective(dlp_session* s, std::string* why) {
+    XRec me{};
+    me.ok = 1;
+    auto fail = [&](const std::string& w) {
+        if (!me.ok) return;
+        me.ok = 0;
+        std::snprintf(me.why, sizeof(me.why), "%s", w.c_str());
+    };
+    if (const char* e = std::getenv("DLP_TEST_PEER_FAIL"))
+        if (std::atoi(e) == s->rank) fail("injected (DLP_TEST_PEER_FAIL)");
+    if (me.ok && ensure_xblock(s) != DLP_OK) fail(std::string("exchange block: ") + dlp_last_error());
+    if (me.ok) {
+        hipIpcMemHandle_t h;
+        if (hipIpcGetMemHandle(&h, s->xblk) != hipSuccess) {
+            (void)hipGetLastError();
+            fail("hipIpcGetMemHandle of the exchange block failed");
+        } else {
+            std::memcpy(me.handle, &h, sizeof(h));
+        }
+    }
+    if (hipDeviceGetPCIBusId(me.bus, (int)sizeof(me.bus), s->device) != hipSuccess) {
+        (void)hipGetLastError();
+        fail("hipDeviceGetPCIBusId failed");
+    }
+    std::vector<XRec> all(s->nranks);
+    CALL_TRY(comm_allgather(s, &me, all.data(), sizeof(XRec)));
+    for (int r = 0; r < s->nranks; ++r)
+        if (!all[r].ok) {
+            *why = "rank " + std::to_string(r) + ": " + std::string(all[r].why, strnlen(all[r].why, sizeof(all[r].why)));
+            return DLP_ERR_UNSUPPORTED;
+        }
+    // peer access to every other rank's device, then its block
+    XRec me2{};
+    me2.ok = 1;
+    std::vector<void*> opened;
+    std::vector<uint64_t*> bases(s->nranks, nullptr);
+    for (int r = 0; r < s->nranks && me2.ok; ++r) {
+        if (r == s->rank) {
+            bases[r] = s->xblk;
+            continue;
+        }
+        int dev = -1, can = 0;
+        all[r].bus[sizeof(all[r].bus) - 1] = 0;
+        if (hipDeviceGetByPCIBusId(&dev, all[r].bus) != hipSuccess || dev < 0) {
+            (void)hipGetLastError();
+            std::snprintf(me2.why, sizeof(me2.why), "rank %d's device %s is not visible to this process",
+                          r, all[r].bus);
+            me2.ok = 0;
+            break;
+        }
+        if (dev != s->device && (hipDeviceCanAccessPeer(&can, s->device, dev) != hipSuccess || !can)) {
+            (void)hipGetLastError();
+            std::snprintf(me2.why, sizeof(me2.why), "device %d cannot access device %d (rank %d)", s->device,
+                          dev, r);
+            me2.ok = 0;
+            break;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, all[r].handle, sizeof(h));
+        void* p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            std::snprintf(me2.why, sizeof(me2.why), "hipIpcOpenMemHandle of rank %d's block: %s", r,
+                          hipGetErrorString(e));
+            me2.ok = 0;
+            break;
+        }
+        opened.push_back(p);
+        bases[r] = (uint64_t*)p;
+    }
+    std::vector<XRec> all2(s->nranks);
+    const int rc = comm_allgather(s, &me2, all2.data(), sizeof(XRec));
+    int bad = -1;
+    for (int r = 0; r < s->nranks && rc == DLP_OK && bad < 0; ++r)
+        if (!all2[r].ok) bad = r;
+    if (rc != DLP_OK || bad >= 0) {
+        for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+        if (rc != DLP_OK) return rc;
+        *why = "rank " + std::to_string(bad) + ": " + std::string(all2[bad].why, strnlen(all2[bad].why, sizeof(all2[bad].why)));
+        return DLP_ERR_UNSUPPORTED;
+    }
+    s->ipc_open.insert(s->ipc_open.end(), opened.begin(), opened.end());
     return install_peers(s, bases);
+}
+
+// A communicator session's exchange: `mode` DLP_XCHG_RCCL, DLP_XCHG_PEER (an error when the
+// ranks cannot connect) or DLP_XCHG_DEFAULT (peer where every rank pair connects, else RCCL
+// with the reason kept for dlp_session_exchange_reason); then the auto lookahead follows.
+int settle_exchange(dlp_session* s, int mode) {
+    if (mode == DLP_XCHG_PEER || mode == DLP_XCHG_DEFAULT) {
+        std::string why;
+        const int rc = peer_connect_collective(s, &why);
+        if (rc == DLP_ERR_UNSUPPORTED) {
+            if (mode == DLP_XCHG_PEER) {
+                set_error("peer exchange unavailable: " + why);
+                return rc;
+            }
+            s->xreason = why;
+            s->xmode = dlp_session::X_RCCL;
+        } else if (rc != DLP_OK) {
+            return rc;
+        }
+    } else {
+        s->xmode = dlp_session::X_RCCL;
+    }
+    return la_policy(s);
 }
 
 // Phase-interleaved multi-rank run (dlp_sessions_run): every rank's phase p before any
@@ -1613,7 +1864,7 @@ const char* dlp_status_string(int st) {
         case DLP_ERR_ARG: return "invalid argument";
         case DLP_ERR_OOM: return "out of device memory";
         case DLP_ERR_HIP: return "HIP error";
-        case DLP_ERR_RCCL: return "RCCL error";
+        case DLP_ERR_RCCL: return "exchange (RCCL / peer) error";
         case DLP_ERR_NODEVICE: return "no HIP device";
         case DLP_ERR_STATE: return "invalid state";
         case DLP_ERR_UNSUPPORTED: return "unsupported";
@@ -1895,8 +2146,7 @@ int dlp_session_create_rank(const dlp_problem* prob, const dlp_options* opt, int
         set_error(std::string("session_init: ") + e.what());
         rc = DLP_ERR_OOM;
     }
-    if (rc == DLP_OK && uid && opt->exchange == DLP_XCHG_PEER)
-        rc = dlp_session_set_exchange(s, DLP_XCHG_PEER);   // collective over the new communicator
+    if (rc == DLP_OK && uid) rc = settle_exchange(s, opt->exchange);   // collective over the new communicator
     if (rc != DLP_OK) {
         free_session(s);
         return rc;
@@ -2164,6 +2414,7 @@ int dlp_session_set_defer_tuning(dlp_session* s, int occupancy, int form) {
         return DLP_ERR_ARG;
     }
     s->defer_occ = occupancy;
+    if (form >= 0) s->form_auto = false;
     if (form >= 0 && s->la && !dlp::lookahead_form(form)) CALL_TRY(la_disable(s));
     if (form >= 0) {
         s->d.form = form;
@@ -2188,6 +2439,10 @@ int dlp_sessions_connect(dlp_session* const* ranks, int nranks) {
         }
         by[s->rank] = s;
     }
+    if (const char* e = std::getenv("DLP_TEST_PEER_FAIL")) {   // tests only
+        set_error("rank " + std::string(e) + ": injected (DLP_TEST_PEER_FAIL)");
+        return DLP_ERR_UNSUPPORTED;
+    }
     for (dlp_session* s : by) CALL_TRY(ensure_xblock(s));
     // direct peer access between the devices involved (xGMI)
     for (dlp_session* a : by)
@@ -2211,6 +2466,7 @@ int dlp_sessions_connect(dlp_session* const* ranks, int nranks) {
         HIP_TRY(hipSetDevice(s->device));
         HIP_TRY(hipStreamSynchronize(s->stream));
         CALL_TRY(install_peers(s, bases));
+        CALL_TRY(la_policy(s));
     }
     return DLP_OK;
 }
@@ -2237,43 +2493,31 @@ int dlp_session_connect_ipc(dlp_session* s, const void* handles) {
 int dlp_session_set_exchange(dlp_session* s, int mode) {
     if (!s || (mode != DLP_XCHG_RCCL && mode != DLP_XCHG_PEER)) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
     if (mode == DLP_XCHG_RCCL) {
         if (!s->comm) {
             set_error("the session has no RCCL communicator");
             return DLP_ERR_STATE;
         }
-        HIP_TRY(hipStreamSynchronize(s->stream));
         s->xmode = dlp_session::X_RCCL;
-        return DLP_OK;
+        return la_policy(s);
     }
     if (s->xpeers_host.nranks == s->nranks && s->xpeers_host.base[s->rank] == s->xblk && s->xblk) {
         s->xmode = dlp_session::X_PEER;   // connected before
-        return DLP_OK;
+        return la_policy(s);
     }
     if (!s->comm) {
         set_error("dlp_session_set_exchange(PEER) without a communicator: use dlp_sessions_connect "
                   "or dlp_session_connect_ipc");
         return DLP_ERR_STATE;
     }
-    // every rank's IPC handle over the communicator itself (one all-gather at set-up)
-    CALL_TRY(ensure_xblock(s));
-    const size_t hb = sizeof(hipIpcMemHandle_t);
-    std::vector<uint8_t> all(hb * s->nranks);
-    uint8_t* dbuf = nullptr;
-    HIP_TRY(hipMalloc(&dbuf, hb * (s->nranks + 1)));
-    hipIpcMemHandle_t h;
-    HIP_TRY(hipIpcGetMemHandle(&h, s->xblk));
-    HIP_TRY(hipMemcpy(dbuf + hb * s->nranks, &h, hb, hipMemcpyHostToDevice));
-    const ncclResult_t nr = ncclAllGather(dbuf + hb * s->nranks, dbuf, hb, ncclUint8, s->comm, s->stream);
-    if (nr != ncclSuccess) {
-        (void)hipFree(dbuf);
-        set_error(std::string("ncclAllGather (IPC handles): ") + ncclGetErrorString(nr));
-        return DLP_ERR_RCCL;
-    }
-    CALL_TRY(wait_stream(s));
-    HIP_TRY(hipMemcpy(all.data(), dbuf, hb * s->nranks, hipMemcpyDeviceToHost));
-    HIP_TRY(hipFree(dbuf));
-    return connect_ipc(s, all.data());
+    return settle_exchange(s, DLP_XCHG_PEER);   // every rank's IPC handle over the communicator
+}
+
+int dlp_session_exchange_reason(dlp_session* s, char* buf, size_t cap) {
+    if (!s || !buf || cap == 0) return DLP_ERR_ARG;
+    std::snprintf(buf, cap, "%s", s->xreason.c_str());
+    return DLP_OK;
 }
 
 int dlp_session_get_exchange(dlp_session* s, int* mode) {
@@ -2294,6 +2538,25 @@ int dlp_sessions_run(dlp_session* const* ranks, int nranks, int64_t max_pivots, 
     dlp_session* s0 = ss[0];
     const int64_t start = s0->npivots;
     int64_t budget = std::min<int64_t>(max_pivots, s0->opt.max_pivots - s0->launched);
+    // ranks that share a device keep every wait in a launch of its own (no xfuse): their
+    // streams may share a hardware queue, where a launch that waits must come after the
+    // launches of the other ranks it waits for (the phase interleaving below)
+    bool shared = false;
+    for (int a = 0; a < nranks; ++a)
+        for (int b = a + 1; b < nranks; ++b) shared = shared || ss[a]->device == ss[b]->device;
+    struct FuseGuard {
+        std::vector<dlp_session*>& v;
+        std::vector<bool> keep;
+        FuseGuard(std::vector<dlp_session*>& v_, bool off) : v(v_) {
+            for (dlp_session* s : v) {
+                keep.push_back(s->xfuse);
+                if (off) s->xfuse = false;
+            }
+        }
+        ~FuseGuard() {
+            for (size_t k = 0; k < v.size(); ++k) v[k]->xfuse = keep[k];
+        }
+    } fuse_guard(ss, shared);
     auto poll_all = [&]() -> int {
         for (dlp_session* s : ss) {
             HIP_TRY(hipSetDevice(s->device));
@@ -2348,6 +2611,12 @@ int dlp_sessions_run(dlp_session* const* ranks, int nranks, int64_t max_pivots, 
 int dlp_session_set_exchange_timeout(dlp_session* s, double seconds) {
     if (!s || !(seconds >= 0.0)) return DLP_ERR_ARG;
     s->stall_limit_s = seconds;
+    if (s->xpeers) {   // the device waits' own bound follows (between runs: the stream is idle)
+        s->xpeers_host.wait_ticks = xwait_ticks(seconds);
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        HIP_TRY(hipMemcpy(s->xpeers, &s->xpeers_host, sizeof(s->xpeers_host), hipMemcpyHostToDevice));
+    }
     return DLP_OK;
 }
 

@@ -358,6 +358,12 @@ class Session:
         L.check(L.lib().dlp_session_get_exchange(self._h, C.byref(m)), "dlp_session_get_exchange")
         return m.value
 
+    def exchange_reason(self) -> str:
+        """Why the auto exchange (XCHG_DEFAULT) fell back to RCCL ("" when it did not)."""
+        buf = C.create_string_buffer(512)
+        L.check(L.lib().dlp_session_exchange_reason(self._h, buf, 512), "dlp_session_exchange_reason")
+        return buf.value.decode()
+
     def set_defer_tuning(self, occupancy: int, form: int = -1):
         """Deferred pass: workgroups/CU cap (0 = none) and form (0 wide, 1/2 narrow x 2/4 rows;
         scalar-coefficient 3 = 1 double x 4 rows, 4 = 2 doubles x 2 rows, 5 = 1 double x 8 rows)."""

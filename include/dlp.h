@@ -156,13 +156,17 @@ typedef struct dlp_options {
     int32_t lookahead;       /* deferred sessions: select block b+1 while the pass of block b
                                 runs, on a second tableau buffer (results unchanged, bit for
                                 bit; 2x the tableau memory): 1 = on where supported, 0 = off,
-                                -1 = auto (default: tableaus of >= 4 GiB that fit twice; at
+                                -1 = auto (default: a single-rank tableau of >= 4 GiB that
+                                fits twice; a row-block rank at K = 64 on a streaming (> 1 GiB)
+                                tableau once it runs the peer exchange, never with RCCL; at
                                 K = 64 the selections replay up to 127 steps) */
     int32_t exchange;        /* row-block exchange of dlp_solve(n_gpus = N) and of rank sessions
-                                created with an RCCL id: 0 (default) or DLP_XCHG_RCCL = RCCL
-                                candidate all-gather + pivot-row MAX all-reduce; DLP_XCHG_PEER =
-                                owner-rooted peer stores (dlp_sessions_connect in process; the
-                                IPC handles all-gathered over the communicator per process) */
+                                created with an RCCL id: DLP_XCHG_DEFAULT (0, the default) = the
+                                peer exchange where every rank pair connects (peer access + IPC
+                                open, agreed by all ranks), else RCCL (the reason:
+                                dlp_session_exchange_reason); DLP_XCHG_RCCL = RCCL candidate
+                                all-gather + pivot-row MAX all-reduce; DLP_XCHG_PEER = owner-
+                                rooted peer stores, an error when the ranks cannot connect */
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
  * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;
@@ -347,25 +351,34 @@ int dlp_session_get_lookahead(dlp_session* s, int* on);
  *     an RCCL id, dlp_session_set_exchange(s, DLP_XCHG_PEER) does that over RCCL.
  * dlp_session_set_exchange switches between the two on a session that has both (every
  * rank at the same point, between runs). */
-#define DLP_XCHG_HOST  0   /* caller-driven (dlp_session_step_*) */
-#define DLP_XCHG_RCCL  1
-#define DLP_XCHG_PEER  2
+#define DLP_XCHG_DEFAULT 0   /* dlp_options.exchange: peer where every rank pair connects, else RCCL */
+#define DLP_XCHG_RCCL    1
+#define DLP_XCHG_PEER    2
+#define DLP_XCHG_HOST    3   /* dlp_session_get_exchange: caller-driven (dlp_session_step_*) */
 int dlp_sessions_connect(dlp_session* const* ranks, int nranks);
 int dlp_session_exchange_handle(dlp_session* s, void* out64);
 int dlp_session_connect_ipc(dlp_session* s, const void* handles /* nranks x 64 B, rank order */);
 int dlp_session_set_exchange(dlp_session* s, int mode);
 int dlp_session_get_exchange(dlp_session* s, int* mode);
+/* Why an auto exchange (DLP_XCHG_DEFAULT) fell back to RCCL ("" when it did not). */
+int dlp_session_exchange_reason(dlp_session* s, char* buf, size_t cap);
 int dlp_sessions_run(dlp_session* const* ranks, int nranks, int64_t max_pivots, int64_t* pivots_done);
 
-/* Failure containment on the RCCL exchange.  A session with a
- * communicator never blocks in a wait that a peer must end: its window waits poll
- * the stream, ncclCommGetAsyncError and an abort word; on an RCCL error, an abort
- * request or `seconds` without progress (default 600; 0 = no limit) it calls
- * ncclCommAbort and dlp_session_run returns DLP_ERR_RCCL (the session is then
- * unusable; free it).  dlp_solve(n_gpus = N) aborts every rank's communicator
- * when one rank fails and returns that rank's error.  dlp_session_abort may be
- * called from any thread.  dlp_session_inject_fault (tests): the (after_polls+1)-th
- * window wait fails as if the exchange had died. */
+/* Failure containment on the exchange.  A session with an exchange
+ * never blocks in a wait that a peer must end: its window waits poll the stream,
+ * ncclCommGetAsyncError and an abort word; on an RCCL error, an abort request, a
+ * peer-exchange wait that timed out, or a window not complete after `seconds` (the
+ * exchange timeout: default 600; 0 = no limit) it raises the device abort word, calls
+ * ncclCommAbort and dlp_session_run returns DLP_ERR_RCCL, the status of every exchange
+ * failure (the session is then unusable; free it).  A device error returns DLP_ERR_HIP.
+ * Each peer-exchange wait on the device is bounded by the same timeout + 5 s.
+ * dlp_solve(n_gpus = N) aborts every rank's exchange when one rank fails and returns
+ * that rank's error.  dlp_session_abort may be called from any thread.
+ * dlp_session_inject_fault (tests): the (after_polls+1)-th window wait fails as if the
+ * exchange had died.
+ * Freeing connected ranks: a rank's exchange block receives its peers' stores, so a
+ * connected rank session may be freed only after every rank's stream has drained
+ * (e.g. a barrier after the last run / result on every rank). */
 int dlp_session_set_exchange_timeout(dlp_session* s, double seconds);
 int dlp_session_abort(dlp_session* s);
 int dlp_session_inject_fault(dlp_session* s, int64_t after_polls);

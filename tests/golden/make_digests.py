@@ -19,6 +19,8 @@ for the GPU to reproduce.  Run in the build container (CPU only):
       bench's 256-pivot second-exchange window at N > 1): sha256 of all
       32,769 rows (objective row last), each its first `width` doubles, streamed
       in row order; plus the log prefix and basis digests at each stop.
+  c5  every LP of the C5 batches (4,096 x 64x128 and 4,096 x 64x64, seed 5000): per-field
+      digests of status, pivot count, objective bits, basis and the first 64 log entries.
 
 The digests hash little-endian fp64 / int32 bytes of the oracle's outputs
 (tests/oracle_py.py), so the GPU side compares bit for bit."""
@@ -93,6 +95,46 @@ def c3_tableau(stops=(136, 160, C3_K64_PIVOTS, C3_K64_PIVOTS + 256)):
     return out
 
 
+C5_SHAPES = [(64, 64), (64, 128)]
+
+
+def c5_records(st, npiv, obj, basis, logs):
+    """The per-LP digests of a C5 batch (GPU and oracle alike): status, pivot count, objective
+    bits, basis and the first <= 64 log entries of every LP, each field hashed in LP order."""
+    h = hashlib.sha256()
+    for k in range(len(st)):
+        h.update(np.ascontiguousarray(logs[k][:min(64, int(npiv[k]))]).tobytes())
+    return {"status_sha256": sha(np.asarray(st, np.int32)), "num_pivots_sha256": sha(np.asarray(npiv, np.int64)),
+            "objective_sha256": sha(np.asarray(obj, np.float64)), "basis_sha256": sha(np.asarray(basis, np.int32)),
+            "log64_sha256": h.hexdigest()}
+
+
+def c5(nlp=4096, seed=5000):
+    """C5 (BASELINE.json: 4,096 independent 64 x 128 LPs) and its 64 x 64 twin: the oracle's
+    solve of EVERY LP of the batch (LP k = generated dense LP of seed `seed + k`), digested
+    per field (VERDICT r03 #4: all 4,096 LPs pinned, not a sample)."""
+    out = {}
+    for m, n in C5_SHAPES:
+        t0 = time.time()
+        st = np.zeros(nlp, np.int32)
+        npiv = np.zeros(nlp, np.int64)
+        obj = np.zeros(nlp)
+        basis = np.zeros((nlp, m), np.int32)
+        logs = []
+        for k in range(nlp):
+            A, b, c = O.gen_dense(m, n, seed + k)
+            r = O.solve_dense(A, b, c, nthreads=1)
+            st[k], npiv[k], obj[k] = r.status, r.num_pivots, r.objective
+            basis[k] = r.basis
+            logs.append(np.ascontiguousarray(r.pivot_log[:64]))
+        d = {"m": m, "n": n, "nlp": nlp, "seed": seed, "max_pivots": int(npiv.max()),
+             "all_optimal": bool((st == 0).all())}
+        d.update(c5_records(st, npiv, obj, basis, logs))
+        d["oracle_seconds"] = time.time() - t0
+        out[f"{m}x{n}"] = d
+    return out
+
+
 def main():
     which = sys.argv[1:] or ["c2", "c3"]
     d = {}
@@ -100,7 +142,8 @@ def main():
         with open(OUT) as f:
             d = json.load(f)
     for w in which:
-        d[w] = {"c2": c2, "c3": c3, "c3_k64": lambda: c3(C3_K64_PIVOTS), "c3_tableau": c3_tableau}[w]()
+        d[w] = {"c2": c2, "c3": c3, "c3_k64": lambda: c3(C3_K64_PIVOTS), "c3_tableau": c3_tableau,
+                "c5": c5}[w]()
         with open(OUT, "w") as f:
             json.dump(d, f, indent=1)
         print(w, json.dumps(d[w]), flush=True)

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("defer", [1, 16])
 def test_injected_fault_one_rank_rccl_session(defer):
     A, b, c = O.gen_dense(200, 400, 1)
-    with dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
+    with dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(), exchange=L.XCHG_RCCL,
                      defer=defer, check_interval=16) as s:
         s.inject_fault(1)   # the second window's wait fails
         t0 = time.time()
@@ -36,19 +36,19 @@ def test_injected_fault_in_process_n_gpus():
     try:
         t0 = time.time()
         with pytest.raises(L.DLPError) as e:
-            dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, check_interval=8, small_lp=-1)
+            dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, exchange=L.XCHG_RCCL, check_interval=8, small_lp=-1)
         assert "rank 0" in str(e.value) and "injected" in str(e.value)
         assert time.time() - t0 < 30
     finally:
         del os.environ["DLP_TEST_FAIL_RANK"]
     # the process is healthy afterwards: the same solve succeeds
-    res = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1)
+    res = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, exchange=L.XCHG_RCCL)
     assert res.status == L.OK
 
 
 def test_abort_from_another_thread():
     """dlp_session_abort while dlp_session_run is waiting on the exchange path."""
-    with dlp.Session(dlp.Problem.random(4096, 4096, 2), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
+    with dlp.Session(dlp.Problem.random(4096, 4096, 2), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(), exchange=L.XCHG_RCCL,
                      check_interval=4096, max_pivots=10 ** 6) as s:
         out = {}
 
@@ -72,9 +72,9 @@ def test_abort_from_another_thread():
 def test_stall_limit():
     """A window that makes no progress for longer than the exchange timeout is
     aborted (here a 1 ms limit against a 4096-pivot C2 window of ~100 ms)."""
-    with dlp.Session(dlp.Problem.random(4096, 4096, 2), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
+    with dlp.Session(dlp.Problem.random(4096, 4096, 2), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(), exchange=L.XCHG_RCCL,
                      check_interval=4096) as s:
         s.set_exchange_timeout(0.001)
         with pytest.raises(L.DLPError) as e:
             s.run(4096)
-        assert e.value.status == L.ERR_RCCL and "no progress" in str(e.value)
+        assert e.value.status == L.ERR_RCCL and "exchange timeout" in str(e.value)

@@ -140,7 +140,7 @@ def test_general_solve_n_gpus_in_process(name):
     cs = next(c for c in CASES if c["name"] == name)
     lp = fixture_lp(cs)
     ref = O.solve_general(lp)
-    res = dlp.solve(dlp.Problem.general(*lp_arrays(lp)), n_gpus=1)
+    res = dlp.solve(dlp.Problem.general(*lp_arrays(lp)), n_gpus=1, exchange=L.XCHG_RCCL)
     _check(res, ref)
 
 
@@ -151,7 +151,7 @@ def test_general_rccl_exchange_single_rank(name, defer):
     lp = fixture_lp(cs)
     ref = O.solve_general(lp)
     with dlp.Session(dlp.Problem.general(*lp_arrays(lp)), rank=0, nranks=1,
-                     rccl_id=dlp.comm_unique_id(), timing=2, check_interval=5,
+                     rccl_id=dlp.comm_unique_id(), exchange=L.XCHG_RCCL, timing=2, check_interval=5,
                      defer=defer) as s:
         st, _ = s.run(10 ** 6)
         res = s.result()

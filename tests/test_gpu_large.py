@@ -193,11 +193,24 @@ def test_c2_full_solve_digest(lookahead):
 
 @pytest.mark.parametrize("m,n", [(64, 64), (64, 128)])
 def test_c5_full_batch(m, n):
-    """4,096 independent LPs (C5; BASELINE.json: 64 x 128): statuses and sampled
-    LPs against the oracle (pivot count, objective bits, pivot log)."""
+    """4,096 independent LPs (C5; BASELINE.json: 64 x 128): EVERY LP of the batch against the
+    oracle's committed digests (tests/golden/make_digests.py c5: status, pivot count, objective
+    bits, basis and the first 64 pivot-log entries of each LP, hashed in LP order), and sampled
+    LPs against the oracle itself."""
     nlp, seed = 4096, 5000
     br = dlp.batched_solve(nlp, m, n, seed, log_cap=64, want_basis=True)
     assert (br.status == 0).all()
+    want = load_golden("digests.json")["c5"][f"{m}x{n}"]
+    assert (want["nlp"], want["seed"]) == (nlp, seed)
+    h = hashlib.sha256()
+    for k in range(nlp):
+        h.update(np.ascontiguousarray(br.logs[k][:min(64, int(br.num_pivots[k]))]).tobytes())
+    got = {"status_sha256": _sha(np.asarray(br.status, np.int32)),
+           "num_pivots_sha256": _sha(np.asarray(br.num_pivots, np.int64)),
+           "objective_sha256": _sha(np.asarray(br.objective, np.float64)),
+           "basis_sha256": _sha(np.asarray(br.basis, np.int32)), "log64_sha256": h.hexdigest()}
+    for key, val in got.items():
+        assert val == want[key], key
     for k in (0, 1, 777, 2047, 3000, 4095):
         A, b, c = O.gen_dense(m, n, seed + k)
         ref = O.solve_dense(A, b, c, nthreads=1)

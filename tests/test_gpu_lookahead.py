@@ -181,7 +181,7 @@ def test_lookahead_rccl_exchange_single_rank(defer, form):
     selection kernels of the multi-GPU C3 geometry, 128-step replays)."""
     A, b, c = O.gen_dense(200, 400, 1)
     ref = O.solve_dense(A, b, c)
-    with dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
+    with dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(), exchange=L.XCHG_RCCL,
                      defer=defer, check_interval=40, lookahead=1) as s:
         if form >= 0:
             s.set_defer_tuning(0, form)

@@ -193,7 +193,7 @@ def test_solve_n_gpus_in_process(defer):
     one host thread per device, RCCL exchange, merged result) on this box's GPU."""
     A, b, c = O.gen_dense(200, 400, 1)
     ref = O.solve_dense(A, b, c)
-    res = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, defer=defer)
+    res = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, exchange=L.XCHG_RCCL, defer=defer)
     _check_equal(res, ref)
     with pytest.raises(L.DLPError):
         dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=dlp.device_count() + 1)
@@ -207,7 +207,7 @@ def test_rccl_exchange_path_single_rank(defer):
     A, b, c = O.gen_dense(200, 400, 1)
     ref = O.solve_dense(A, b, c)
     with dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1,
-                     rccl_id=dlp.comm_unique_id(), timing=2, defer=defer) as s:
+                     rccl_id=dlp.comm_unique_id(), exchange=L.XCHG_RCCL, timing=2, defer=defer) as s:
         assert s.update_stats()[2] == (defer or 1)
         st, done = s.run(10 ** 6)
         res = s.result()

@@ -191,6 +191,61 @@ def test_rccl_session_switches_exchange(defer):
         _check(s.result(), ref)
 
 
+@pytest.mark.parametrize("inject", [False, True])
+@pytest.mark.parametrize("defer", [1, 16])
+def test_auto_exchange_rank_session(inject, defer):
+    """exchange = DLP_XCHG_DEFAULT (auto) on a 1-rank RCCL session: the ranks agree on the
+    peer exchange when every one can make and open the blocks; a rank that cannot
+    (DLP_TEST_PEER_FAIL injects it) makes every rank fall back to RCCL, with the reason
+    reported.  Bit-exact either way."""
+    A, b, c = O.gen_dense(200, 400, 1)
+    ref = O.solve_dense(A, b, c)
+    if inject:
+        os.environ["DLP_TEST_PEER_FAIL"] = "0"
+    try:
+        s = dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
+                        defer=defer, check_interval=16, small_lp=-1)
+    finally:
+        os.environ.pop("DLP_TEST_PEER_FAIL", None)
+    with s:
+        if inject:
+            assert s.get_exchange() == L.XCHG_RCCL
+            assert "injected" in s.exchange_reason() and "rank 0" in s.exchange_reason()
+        else:
+            assert s.get_exchange() == L.XCHG_PEER and s.exchange_reason() == ""
+        st, _ = s.run(10 ** 6)
+        assert st == L.OK
+        _check(s.result(), ref)
+
+
+def test_strict_peer_exchange_fails_when_a_rank_cannot():
+    """exchange = DLP_XCHG_PEER is not downgraded: the session creation fails."""
+    A, b, c = O.gen_dense(64, 64, 3)
+    os.environ["DLP_TEST_PEER_FAIL"] = "0"
+    try:
+        with pytest.raises(L.DLPError) as e:
+            dlp.Session(dlp.Problem.dense(A, b, c), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
+                        exchange=L.XCHG_PEER)
+        assert e.value.status == L.ERR_UNSUPPORTED and "injected" in str(e.value)
+    finally:
+        os.environ.pop("DLP_TEST_PEER_FAIL", None)
+
+
+@pytest.mark.parametrize("inject", [False, True])
+def test_solve_n_gpus_auto_exchange(inject):
+    """dlp_solve(n_gpus = 1) with the default exchange: peer, or RCCL after a failed
+    connect (injected); bit-exact either way."""
+    A, b, c = O.gen_dense(200, 400, 1)
+    ref = O.solve_dense(A, b, c)
+    if inject:
+        os.environ["DLP_TEST_PEER_FAIL"] = "0"
+    try:
+        res = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, defer=16, small_lp=-1)
+    finally:
+        os.environ.pop("DLP_TEST_PEER_FAIL", None)
+    _check(res, ref)
+
+
 def test_peer_wait_is_bounded():
     """A rank that never runs: the other rank's select kernel waits for its
     candidate; the host stall limit raises the abort word, the device wait ends and
@@ -202,29 +257,37 @@ def test_peer_wait_is_bounded():
         t0 = time.time()
         with pytest.raises(L.DLPError) as e:
             sess[0].run(100)   # rank 1 never enqueues anything
-        assert e.value.status in (L.ERR_RCCL, L.ERR_HIP)
+        assert e.value.status == L.ERR_RCCL
         assert time.time() - t0 < 30
     finally:
         for s in sess:
             s.close()
 
 
-def test_c3_row_partition_peer_exchange_one_gpu():
+@pytest.mark.parametrize("lookahead", [-1, 0])
+def test_c3_row_partition_peer_exchange_one_gpu(lookahead):
     """BASELINE.json C3 (32768 x 32768) as the 8-GPU split runs it, on ONE MI355X:
-    8 rank sessions (4,096 local rows each; K = 64, form 23, 256-row bands), the
-    exchange through the peer blocks, 160 pivots (two full blocks + a 32-pivot tail),
-    against the oracle's committed digests: pivot log, basis, objective and the
-    whole tableau."""
+    8 rank sessions (4,096 local rows each; K = 64, 256-row bands), the exchange through
+    the peer blocks, 160 pivots (two full blocks + a 32-pivot tail), against the
+    oracle's committed digests: pivot log, basis, objective and the whole tableau.
+    lookahead -1 (auto): once connected by the peer exchange every rank selects block
+    b+1 beside the form-21 pass of block b (band publication on); 0: no lookahead, the
+    form-23 pass."""
     g = load_golden("digests.json")
     tab = g["c3_tableau"]
     k, P = 160, 8
     want = tab["stops"][str(k)]
     prob = dlp.Problem.random(tab["m"], tab["n"], tab["seed"])
-    sess = [dlp.Session(prob, rank=r, nranks=P, defer=64, check_interval=64) for r in range(P)]
+    sess = [dlp.Session(prob, rank=r, nranks=P, defer=64, check_interval=64, lookahead=lookahead)
+            for r in range(P)]
     try:
         for s in sess:
             assert s.get_defer_tuning()[1:] == (23, 64) and s.get_tuning()[1] == 256
+            assert not s.lookahead()   # a host-driven rank until connected
         dlp.Session.connect_peers(sess)
+        for s in sess:
+            on = lookahead != 0
+            assert s.lookahead() == on and s.get_defer_tuning()[1] == (21 if on else 23)
         st, done = dlp.Session.run_ranks(sess, k)
         assert done == k
         for s in sess:
@@ -250,7 +313,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _ipc_worker(rank, world, port, m, n, seed, defer, q):
+def _ipc_worker(rank, world, port, m, n, seed, defer, q, late=0.0):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -262,6 +325,8 @@ def _ipc_worker(rank, world, port, m, n, seed, defer, q):
         dist.all_gather_object(hs, s.exchange_handle())
         s.connect_ipc(hs)
         s.set_exchange_timeout(60.0)
+        if rank == world - 1 and late > 0:
+            time.sleep(late)   # a rank whose run starts late: its peers' device waits hold
         st, done = s.run(10 ** 6)
         res = s.result()
         q.put((rank, st, done, np.ascontiguousarray(res.pivot_log).tobytes(), res.objective,
@@ -274,8 +339,11 @@ def _ipc_worker(rank, world, port, m, n, seed, defer, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("defer", [1, 16])
-def test_peer_exchange_two_processes_ipc(defer):
+@pytest.mark.parametrize("defer,late", [(1, 0.0), (16, 0.0), (16, 32.0)])
+def test_peer_exchange_two_processes_ipc(defer, late):
+    """late = 32 s: the last rank starts its run 32 s after the first; the first rank's
+    device waits are bounded by its exchange timeout (60 s + 5 s), not by a fixed limit of
+    their own (round 3 had 30 s), so the solve completes."""
     import torch.multiprocessing as mp
     m, n, seed, world = 120, 150, 4, 2
     A, b, c = O.gen_dense(m, n, seed)
@@ -283,7 +351,7 @@ def test_peer_exchange_two_processes_ipc(defer):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ipc_worker, args=(r, world, port, m, n, seed, defer, q))
+    procs = [ctx.Process(target=_ipc_worker, args=(r, world, port, m, n, seed, defer, q, late))
              for r in range(world)]
     for p in procs:
         p.start()

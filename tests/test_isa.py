@@ -141,8 +141,8 @@ def test_lookahead_kernels_fit_beside_the_form21_pass():
         assert hits, sub
         return max(hits)
     assert one("pass_d_kernel") <= 160, c
-    assert one("ratio_lean_kernelILi128ELi4E") <= 32
-    assert one("prow_defer_kernelILb1E") <= 32
+    assert one("ratio_lean_kernel") <= 32   # every instance (ring depths 8 / 16, LCH 4 / 8)
+    assert one("prow_lean_kernel") <= 32
 
 
 def _functions(text):
@@ -159,25 +159,33 @@ def _functions(text):
     return funcs
 
 
-def test_peer_row_push_stores_both_halves():
-    """hipcc (ROCm 7.2) compiles __builtin_bit_cast(T, v.y) of an ext_vector element as a
-    cast of element 0.  In the deferred pivot-row kernel that made the peer exchange push
-    the even column's value into both words of every column pair (found by
-    tests/test_gpu_peer.py).  The kernel now copies the elements to scalars first: its
-    two system-scope row stores (columns j and j + 1) must store different registers."""
+def test_peer_row_push_is_drained():
+    """The peer exchange publishes the pivot row in the drained form (include/dlp.h, DESIGN.md
+    §5): every lane's 16-B system-scope (sc0 sc1) store of its two row words, then
+    s_waitcnt vmcnt(0) and a workgroup barrier, then the chunk flag (an 8-B sc0 sc1 store):
+    no flag store may come before the wait and the barrier.  (The elements of the 16-B store
+    are built from scalars: round 3's hipcc bit-cast of a vector element pushed the even
+    column twice; the source guard below keeps that out.)"""
     funcs = _functions(_disasm())
     checked = 0
     for name, ins in funcs.items():
-        if "prow_defer_kernel" not in name:
+        if not any(k in name for k in ("prow_defer_kernel", "prow_lean_kernel", "xrow_send_kernel")):
             continue
-        st = [i for i in ins if i.startswith(("flat_store_dwordx2", "global_store_dwordx2")) and "sc0 sc1" in i]
-        hi = [i for i in st if "offset:8" in i]
-        lo = [i for i in st if "offset:8" not in i]
-        assert hi and lo, (name, st)
-        data = lambda i: i.split(None, 1)[1].split(",")[1].strip()
-        assert {data(i) for i in hi}.isdisjoint({data(i) for i in lo}), (name, st)
+        k = next((i for i, x in enumerate(ins) if x.startswith("buffer_store_dwordx4") and "sc0 sc1" in x), None)
+        assert k is not None, name
+        seen_wait = seen_bar = False
+        for x in ins[k + 1:]:
+            if x.startswith("s_waitcnt") and "vmcnt(0)" in x:
+                seen_wait = True
+            if x.startswith("s_barrier"):
+                seen_bar = True
+            if x.startswith(("global_store_dwordx2", "flat_store_dwordx2")) and "sc0 sc1" in x:
+                assert seen_wait and seen_bar, (name, x)
+                break
+        else:
+            raise AssertionError(f"{name}: no flag store after the row push")
         checked += 1
-    assert checked >= 2, checked
+    assert checked >= 4, checked
 
 
 def test_no_bit_cast_of_a_vector_element_in_kernels():
@@ -191,3 +199,29 @@ def test_no_bit_cast_of_a_vector_element_in_kernels():
                 for k, line in enumerate(fh, 1):
                     code = line.split("//")[0]
                     assert not pat.search(code), f"{f}:{k}: {line.strip()}"
+
+
+def test_band_publication_is_drained():
+    """Band publication relies on the write-through hand-off form
+    (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table) rather than
+    release / acquire fences, which on gfx950 write back / invalidate the whole XCD L2 (ADVICE
+    r03).  Pinned here on the shipped code object: the publishing passes store every output
+    row write-through (sc1) and add to the band counter only behind s_waitcnt vmcnt(0) and a
+    workgroup barrier; the LEAN selection kernels poll the counter with sc1 loads and read the
+    published rows with sc1 loads."""
+    funcs = _functions(_disasm())
+    pubs = [n for n in funcs if ("pass_d_kernelILb1ELb1E" in n or
+                                 (n.startswith("_ZN3dlp12_GLOBAL__N_113pass_q_kernel") and n.count("ELb1EE")))]
+    assert len(pubs) >= 2, pubs
+    for name in pubs:
+        ins = funcs[name]
+        stores = [x for x in ins if x.startswith("buffer_store")]
+        assert stores and all(" sc1" in x for x in stores), (name, stores[:3])
+        k = max(i for i, x in enumerate(ins) if x.startswith("global_atomic_add"))
+        bar = max(i for i in range(k) if ins[i].startswith("s_barrier"))
+        wait = max(i for i in range(bar) if ins[i].startswith("s_waitcnt") and "vmcnt(0)" in ins[i])
+        assert not any(x.startswith(("buffer_store", "global_store")) for x in ins[wait:k]), name
+    for sub in ("ratio_lean_kernelILi128ELi0E", "prow_lean_kernel"):
+        ins = next(v for n, v in funcs.items() if sub in n)
+        assert any(re.match(r"global_load_dword\b.*\bsc1\b", x) for x in ins), sub       # the counter
+        assert any(re.match(r"global_load_dwordx2\b.*\bsc1\b", x) for x in ins), sub     # the rows

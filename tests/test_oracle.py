@@ -165,3 +165,26 @@ def test_slices_equal_single_rank():
             assert lg.tobytes() == ref.pivot_log.tobytes()
         for e in eng:
             e.close()
+
+
+def test_c5_batch_digests_reproduce():
+    """tests/golden/digests.json c5 (the GPU test compares all 4,096 LPs against it): the
+    64 x 64 batch re-solved here by the oracle gives the committed per-field digests."""
+    import hashlib
+    import numpy as np
+    g = load_golden("digests.json")["c5"]["64x64"]
+    st, npiv, obj, basis, h = [], [], [], [], hashlib.sha256()
+    for k in range(g["nlp"]):
+        A, b, c = O.gen_dense(64, 64, g["seed"] + k)
+        r = O.solve_dense(A, b, c, nthreads=1)
+        st.append(r.status)
+        npiv.append(r.num_pivots)
+        obj.append(r.objective)
+        basis.append(r.basis)
+        h.update(np.ascontiguousarray(r.pivot_log[:64]).tobytes())
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    assert sha(np.asarray(st, np.int32)) == g["status_sha256"]
+    assert sha(np.asarray(npiv, np.int64)) == g["num_pivots_sha256"]
+    assert sha(np.asarray(obj, np.float64)) == g["objective_sha256"]
+    assert sha(np.asarray(basis, np.int32)) == g["basis_sha256"]
+    assert h.hexdigest() == g["log64_sha256"]

@@ -27,9 +27,20 @@ st = st[ok]
 names = ["ratio: pricing reduce (start -> q)", "ratio: T0[i][q] + P[l][q] in", "ratio: replay (lane 0)",
          "ratio: block reduce", "ratio: partials + ticket", "ratio: last workgroup select (ticket -> end)",
          "gap ratio end -> prow start", "prow: step table + T0[p] in", "prow: replay + divide",
-         "prow: commit (P, objective row, pricing)"]
+         "prow: commit (P, objective row, pricing) / exchange push"]
 pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 8), (8, 9), (9, 10), (10, 11)]
 res = {n: float(np.median(st[:, b] - st[:, a])) for n, (a, b) in zip(names, pairs)}
+if (st[:, 13:15] > 0).all() and not (st[:, 12] > 0).any():   # peer, fused: the commit in the prow launch
+    res["prow: commit wait (push end -> chunk flag)"] = float(np.median(st[:, 13] - st[:, 11]))
+    res["prow: commit (P, objective row, pricing)"] = float(np.median(st[:, 14] - st[:, 13]))
+    res["pivot total (ratio start -> commit end)"] = float(np.median(st[:, 14] - st[:, 0]))
+    res["pivot period (ratio start -> next ratio start)"] = float(np.median(np.diff(np.sort(st[:, 0]))))
+elif (st[:, 12:15] > 0).all():   # exchange sessions: the pivot row is pushed, then committed
+    for n, (a, b) in zip(["gap prow end -> commit start", "commit: wait for the row chunk",
+                          "commit: P, objective row, pricing"], [(11, 12), (12, 13), (13, 14)]):
+        res[n] = float(np.median(st[:, b] - st[:, a]))
+    res["pivot total (ratio start -> commit end)"] = float(np.median(st[:, 14] - st[:, 0]))
+    res["pivot period (ratio start -> next ratio start)"] = float(np.median(np.diff(np.sort(st[:, 0]))))
 res["ratio total (start -> end)"] = float(np.median(st[:, 6] - st[:, 0]))
 res["prow total"] = float(np.median(st[:, 11] - st[:, 8]))
 print(json.dumps({"pivots_sampled": int(ok.sum()), "bench_value": line["value"],
