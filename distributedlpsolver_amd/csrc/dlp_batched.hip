@@ -295,6 +295,44 @@ __device__ __forceinline__ void each(F&& f) {
     each_(f, std::make_integer_sequence<int, N>{});
 }
 
+// Wave-wide minimum by DPP (xor 1, xor 2, half-row and row mirrors, then the row broadcasts
+// 15 and 31: the full minimum lands in lane 63, read back as a uniform value) — a few cycles
+// per step against the LDS round trip of each ds_bpermute a shuffle costs.  No NaN reaches
+// them (the callers map NaN to +inf first).
+template <int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_f64(double v, double id) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v), d = __builtin_bit_cast(uint64_t, id);
+    const uint32_t lo = __builtin_amdgcn_update_dpp((int)(uint32_t)d, (int)(uint32_t)u, CTRL, RMASK, 0xf, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(d >> 32), (int)(uint32_t)(u >> 32), CTRL, RMASK, 0xf, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_min_f64(double v) {
+    const double id = __builtin_inf();
+    double o;
+    o = dpp_f64<0xB1, 0xf>(v, id); v = o < v ? o : v;    // quad_perm [1,0,3,2]
+    o = dpp_f64<0x4E, 0xf>(v, id); v = o < v ? o : v;    // quad_perm [2,3,0,1]
+    o = dpp_f64<0x141, 0xf>(v, id); v = o < v ? o : v;   // row_half_mirror
+    o = dpp_f64<0x140, 0xf>(v, id); v = o < v ? o : v;   // row_mirror
+    o = dpp_f64<0x142, 0xa>(v, id); v = o < v ? o : v;   // row_bcast:15
+    o = dpp_f64<0x143, 0xc>(v, id); v = o < v ? o : v;   // row_bcast:31
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, 63), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), 63);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int CTRL, int RMASK>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(kNoIndex, v, CTRL, RMASK, 0xf, false);
+}
+__device__ __forceinline__ int wave_min_i32(int v) {
+    v = min(v, dpp_i32<0xB1, 0xf>(v));
+    v = min(v, dpp_i32<0x4E, 0xf>(v));
+    v = min(v, dpp_i32<0x141, 0xf>(v));
+    v = min(v, dpp_i32<0x140, 0xf>(v));
+    v = min(v, dpp_i32<0x142, 0xa>(v));
+    v = min(v, dpp_i32<0x143, 0xc>(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 // Rows of the register-resident elimination in inline asm.  The entering column's entry f
 // and the pivot row index are the same for every lane of the LP, so each test is a uniform
 // exec mask (all lanes or none) set by SALU, with no branch: a row costs one compare and one
@@ -442,20 +480,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         {
             const bool cand = sl < n;
             const double z = cand && t[M] < __builtin_inf() ? t[M] : __builtin_inf();   // (as z < zmin: NaN skipped)
-            double zmin = z;
-#pragma unroll
-            for (int sh = 32; sh >= 1; sh >>= 1) {
-                const double o = __shfl_xor(zmin, sh);
-                zmin = o < zmin ? o : zmin;
-            }
+            const double zmin = wave_min_f64(z);
             const int vz = cand && z == zmin ? var : kNoIndex;
             const int vbl = cand && z < -tol_dj ? var : kNoIndex;
-            int vmin = vz, vb = vbl;
-#pragma unroll
-            for (int sh = 32; sh >= 1; sh >>= 1) {
-                vmin = min(vmin, __shfl_xor(vmin, sh));
-                vb = min(vb, __shfl_xor(vb, sh));
-            }
+            const int vmin = wave_min_i32(vz), vb = wave_min_i32(vbl);
             // the slots of the two winners (variables are distinct: one lane each)
             const uint64_t wz = __ballot(vz == vmin && vmin != kNoIndex);
             const uint64_t wb = __ballot(vbl == vb && vb != kNoIndex);
@@ -507,20 +535,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
                 ratio = rhs / a;
             }
             const uint64_t anyv = __ballot(valid);
-            double rmin = ratio;
-#pragma unroll
-            for (int sh = 32; sh >= 1; sh >>= 1) {
-                const double o = __shfl_xor(rmin, sh);
-                rmin = o < rmin ? o : rmin;
-            }
+            const double rmin = wave_min_f64(ratio);
             const bool tie = valid && ratio == rmin;
             const int bv = s_basis[lane];
             const uint64_t ties = __ballot(tie);
             int wl = __ffsll((unsigned long long)ties) - 1;
             if (__popcll(ties) > 1) {   // exact ties: the smallest basis variable
-                int bmin = tie ? bv : kNoIndex;
-#pragma unroll
-                for (int sh = 32; sh >= 1; sh >>= 1) bmin = min(bmin, __shfl_xor(bmin, sh));
+                const int bmin = wave_min_i32(tie ? bv : kNoIndex);
                 wl = __ffsll((unsigned long long)__ballot(tie && bv == bmin)) - 1;
             }
             Cand best;

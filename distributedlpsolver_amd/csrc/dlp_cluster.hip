@@ -37,7 +37,6 @@ namespace {
 
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u2v __attribute__((ext_vector_type(2)));
-constexpr int kSc1 = 16;          // buffer-op cache policy: sc1
 constexpr int kSpin = 1 << 24;    // bounded waits (each poll sleeps ~64 cycles)
 
 // One workgroup's LDS image (dynamic): slice T[(m+1)][cw] (row-major, stride

@@ -118,33 +118,16 @@ __device__ int g_chain_stamps_on;
         if (g_chain_stamps_on && threadIdx.x == 0) g_chain_stamps[(slot) & 63][k] = wall_clock64(); \
     } while (0)
 
-// Block reductions through an LDS tree (LEAN kernels: fewer VGPRs than the wave shuffles of
-// block_cand / block_price).  Both orders are total, so the winner is the same.
-template <typename T, typename Better>
-__device__ inline T block_tree(T v, T* s, Better better) {
-    s[threadIdx.x] = v;
-    __syncthreads();
-    for (int h = blockDim.x / 2; h > 0; h >>= 1) {
-        if ((int)threadIdx.x < h) {
-            const T o = s[threadIdx.x + h];
-            if (better(o, s[threadIdx.x])) s[threadIdx.x] = o;
-        }
-        __syncthreads();
-    }
-    const T r = s[0];
-    __syncthreads();
-    return r;
-}
-
 // LEAN (lookahead beside the form-21 pass): no register-resident chain (coefficients in
-// pairs during the replay) and LDS-tree block reductions, 23 VGPRs, so the kernel fits in
-// the 32 VGPRs per SIMD that three pass waves (3 x 160) leave free.  Same operations in
+// pairs during the replay) and DPP wave minima for the block reductions (round 3: LDS trees),
+// 30 VGPRs, so the kernel fits in the 32 VGPRs per SIMD that three pass waves (3 x 160) leave
+// free.  Same operations in
 // the same order.  (Staging the chain in LDS by LDS-DMA, 32 steps per round trip, measured
 // no faster beside the pass: 96 vs 95 us per selection, profiles/r02j/.)
 // LEAN, LCH = 0: the coefficient chain streams through a per-wave LDS ring by LDS-DMA, two
 // steps per DMA, kRatioRingPairs DMAs in flight (launch-time LDS, kRatioRing bytes: see
 // kProwRing).
-// (RP = kRatioRingPairs; 16 for tuning: DLP_RING_DEPTH=16)
+// (RP = kRatioRingPairs: 16 measured equal at C3, 8,239-8,267 vs 8,262-8,263 pivots/s, profiles/r04c/)
 constexpr int kRatioRingPairs = 8;
 constexpr size_t ratio_ring_bytes(int rp) { return (size_t)(kRatioDeferThreads / 64) * rp * 128 * sizeof(double); }
 template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4, int RP = kRatioRingPairs>
@@ -163,14 +146,7 @@ __device__ __forceinline__ void ratio_defer_body(
     __shared__ int s_last;
     __shared__ double s_pq[KMAX], s_pn[KMAX];
     __shared__ int32_t s_pl[KMAX];
-    __shared__ Cand s_ct[LEAN ? kRatioDeferThreads : 1];
-    __shared__ PricePart s_pt[LEAN ? kRatioDeferThreads : 1];
-    auto cand_red = [&](Cand v) {
-        if constexpr (LEAN)
-            return block_tree(v, s_ct, [](const Cand& x, const Cand& y) { return cand_better(x, y); });
-        else
-            return block_cand(v, lds_c);
-    };
+    auto cand_red = [&](Cand v) { return block_cand(v, lds_c); };
     // this lane's pricing partial is requested first: it depends on nothing, and the reduce
     // below then waits for it alongside the step-table loads instead of after them
     const PricePart pp0 = (int)threadIdx.x < ntiles ? pp[threadIdx.x] : pp_empty();
@@ -240,23 +216,7 @@ __device__ __forceinline__ void ratio_defer_body(
     PricePart acc = pp_empty();
     pp_combine(acc, pp0);
     for (int k = threadIdx.x + blockDim.x; k < ntiles; k += blockDim.x) pp_combine(acc, pp[k]);
-    if constexpr (LEAN) {
-        // the tree keeps one side per pair: pp_combine's outcome, as a "better" test
-        s_pt[threadIdx.x] = acc;
-        __syncthreads();
-        for (int h = blockDim.x / 2; h > 0; h >>= 1) {
-            if ((int)threadIdx.x < h) {
-                PricePart x = s_pt[threadIdx.x];
-                pp_combine(x, s_pt[threadIdx.x + h]);
-                s_pt[threadIdx.x] = x;
-            }
-            __syncthreads();
-        }
-        acc = s_pt[0];
-        __syncthreads();
-    } else {
-        acc = block_price(acc, lds_pp);
-    }
+    acc = block_price(acc, lds_pp);   // (DPP wave minima: LEAN too, within its 32 VGPRs)
     int32_t q;
     if (st->bland)
         q = acc.jbland;
@@ -519,7 +479,7 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
 // T0[p], divided by the pivot element (IEEE division).  fused (single rank):
 // commit_row as well.  Otherwise the owner writes the fp64 bits and every
 // other rank INT64_MIN for the int64 MAX exchange.
-constexpr int kProwRingSteps = 8;   // (RS; 16 for tuning: DLP_RING_DEPTH=16)
+constexpr int kProwRingSteps = 8;   // (RS: 16 measured equal, with the ratio ring's 16)
 constexpr size_t prow_ring_bytes(int rs) { return (size_t)4 * rs * 128 * sizeof(double); }
 template <bool LEAN, int RS = kProwRingSteps>
 __device__ __forceinline__ void prow_defer_body(
@@ -2157,13 +2117,6 @@ __global__ __launch_bounds__(64) void seal_kernel(DevState* st, int slot, uint32
 
 }  // namespace
 
-// LDS-ring depth of the LEAN chain kernels (tuning only: DLP_RING_DEPTH=16; default 8)
-static int ring_depth() {
-    static const int d = std::getenv("DLP_RING_DEPTH") ? std::atoi(std::getenv("DLP_RING_DEPTH")) : 8;
-    return d;
-}
-#define COMMA ,
-
 int ratio_defer_blocks(const Geometry& g) {
     return (int)((g.rows + 1 + kRatioDeferThreads - 1) / kRatioDeferThreads);
 }
@@ -2210,8 +2163,6 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
             DLP_RATIO_LEAN(8, 0);
         else if (lch == 4)
             DLP_RATIO_LEAN(4, 0);
-        else if (ring_depth() == 16)
-            DLP_RATIO_LEAN(0 COMMA 16, ratio_ring_bytes(16));
         else
             DLP_RATIO_LEAN(0, ratio_ring_bytes(kRatioRingPairs));
 #undef DLP_RATIO_LEAN
@@ -2278,10 +2229,7 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
         nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal, nranks == 1 ? nullptr : xp, xseq,                \
         pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,           \
         pub ? bp->Tn : nullptr, xc)
-        if (ring_depth() == 16)
-            DLP_PROW_LEAN(16);
-        else
-            DLP_PROW_LEAN(kProwRingSteps);
+        DLP_PROW_LEAN(kProwRingSteps);
 #undef DLP_PROW_LEAN
     } else
         prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,

@@ -24,14 +24,6 @@ __device__ inline PricePart pp_empty() {
     return p;
 }
 
-__device__ inline PricePart pp_shfl_xor(const PricePart& v, int m) {
-    PricePart o;
-    o.zmin = __shfl_xor(v.zmin, m);
-    o.jmin = __shfl_xor(v.jmin, m);
-    o.jbland = __shfl_xor(v.jbland, m);
-    return o;
-}
-
 __device__ inline Cand cand_empty() {
     Cand c;
     c.ratio = 0.0;
@@ -43,25 +35,83 @@ __device__ inline Cand cand_empty() {
     return c;
 }
 
-__device__ inline Cand cand_shfl_xor(const Cand& v, int m) {
+// ---- wave-wide minima by DPP (quad permutes, half-row and row mirrors, row broadcasts 15 and
+// 31: the minimum lands in lane 63 and is read back uniform): a few cycles per step against the
+// LDS round trip of every ds_bpermute a shuffle costs (C5: 6.15 M vs 5.07 M LPs/s, profiles/r04c/).
+// Whole waves only; no NaN reaches them (partials and ratios are never NaN: see the callers).
+template <int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_f64(double v, double id) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v), d = __builtin_bit_cast(uint64_t, id);
+    const uint32_t lo = __builtin_amdgcn_update_dpp((int)(uint32_t)d, (int)(uint32_t)u, CTRL, RMASK, 0xf, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(d >> 32), (int)(uint32_t)(u >> 32), CTRL, RMASK,
+                                                    0xf, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_min_f64(double v) {
+    const double id = __builtin_inf();
+    double o;
+    o = dpp_f64<0xB1, 0xf>(v, id); v = o < v ? o : v;    // quad_perm [1,0,3,2]
+    o = dpp_f64<0x4E, 0xf>(v, id); v = o < v ? o : v;    // quad_perm [2,3,0,1]
+    o = dpp_f64<0x141, 0xf>(v, id); v = o < v ? o : v;   // row_half_mirror
+    o = dpp_f64<0x140, 0xf>(v, id); v = o < v ? o : v;   // row_mirror
+    o = dpp_f64<0x142, 0xa>(v, id); v = o < v ? o : v;   // row_bcast:15
+    o = dpp_f64<0x143, 0xc>(v, id); v = o < v ? o : v;   // row_bcast:31
+    return readlane_f64(v, 63);
+}
+template <int CTRL, int RMASK>
+__device__ __forceinline__ int32_t dpp_i32(int32_t v) {
+    return __builtin_amdgcn_update_dpp(kNoIndex, v, CTRL, RMASK, 0xf, false);
+}
+__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
+    v = min(v, dpp_i32<0xB1, 0xf>(v));
+    v = min(v, dpp_i32<0x4E, 0xf>(v));
+    v = min(v, dpp_i32<0x141, 0xf>(v));
+    v = min(v, dpp_i32<0x140, 0xf>(v));
+    v = min(v, dpp_i32<0x142, 0xa>(v));
+    v = min(v, dpp_i32<0x143, 0xc>(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Wave results of the two reductions, field by field (the same total orders as pp_combine and
+// cand_better, so every grouping picks the same winner; uniform results).
+// Pricing: min z, the smallest j among the lanes holding it, the smallest Bland j.  (A partial's
+// zmin is never NaN: price_pair takes z only when z < zmin.)
+__device__ inline PricePart wave_price(const PricePart& v) {
+    PricePart o;
+    o.zmin = wave_min_f64(v.zmin);
+    o.jmin = wave_min_i32(v.zmin == o.zmin ? v.jmin : kNoIndex);
+    o.jbland = wave_min_i32(v.jbland);
+    return o;
+}
+// Ratio test: valid first, then the min ratio, then the smallest basis variable (one lane holds
+// it: basis variables are distinct).  A valid ratio is never NaN (max(b, 0) / a with a > tol_piv);
+// an invalid lane enters as +inf and never ties.
+__device__ inline Cand wave_cand(const Cand& c) {
+    const double rmin = wave_min_f64(c.valid ? c.ratio : __builtin_inf());
+    const bool tie = c.valid && c.ratio == rmin;
+    const int32_t bmin = wave_min_i32(tie ? c.basis_var : kNoIndex);
+    const uint64_t w = __ballot(tie && c.basis_var == bmin);
+    if (w == 0) return cand_empty();
+    const int wl = __builtin_amdgcn_readfirstlane(__ffsll((unsigned long long)w) - 1);
     Cand o;
-    o.ratio = __shfl_xor(v.ratio, m);
-    o.basis_var = __shfl_xor(v.basis_var, m);
-    o.row = __shfl_xor(v.row, m);
-    o.valid = __shfl_xor(v.valid, m);
+    o.ratio = readlane_f64(c.ratio, wl);
+    o.basis_var = __builtin_amdgcn_readlane(c.basis_var, wl);
+    o.row = __builtin_amdgcn_readlane(c.row, wl);
+    o.valid = 1;
     o.pad0 = 0;
-    o.pivot = __shfl_xor(v.pivot, m);
+    o.pivot = readlane_f64(c.pivot, wl);
     return o;
 }
 
-// Block-wide reduction (blockDim.x = 256 = 4 waves): wave shuffles, then LDS.
-template <typename T, typename Shfl, typename Comb>
-__device__ inline T block_reduce(T v, T* lds4, Shfl shfl, Comb comb) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        T o = shfl(v, m);
-        comb(v, o);
-    }
+// Block-wide reduction (whole waves): the wave result, then the waves' results through LDS.
+template <typename T, typename Wave, typename Comb>
+__device__ inline T block_reduce(T v, T* lds4, Wave wave, Comb comb) {
+    v = wave(v);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (lane == 0) lds4[wid] = v;
     __syncthreads();
@@ -74,13 +124,13 @@ __device__ inline T block_reduce(T v, T* lds4, Shfl shfl, Comb comb) {
 
 __device__ inline PricePart block_price(PricePart v, PricePart* lds4) {
     return block_reduce(
-        v, lds4, [](const PricePart& x, int m) { return pp_shfl_xor(x, m); },
+        v, lds4, [](const PricePart& x) { return wave_price(x); },
         [](PricePart& a, const PricePart& b) { pp_combine(a, b); });
 }
 
 __device__ inline Cand block_cand(Cand v, Cand* lds4) {
     return block_reduce(
-        v, lds4, [](const Cand& x, int m) { return cand_shfl_xor(x, m); },
+        v, lds4, [](const Cand& x) { return wave_cand(x); },
         [](Cand& a, const Cand& b) {
             if (cand_better(b, a)) a = b;
         });

@@ -881,14 +881,19 @@ int flush_pending_block(dlp_session* s) {
 }
 
 // An exchange session's auto lookahead, once its exchange is known (creation, connect,
-// dlp_session_set_exchange; between runs): on with the peer exchange at K = 64 on a streaming
-// rank tableau, where every per-pivot kernel fits beside the form-21 pass (select, commit and
-// the LEAN ratio / pivot-row kernels: <= 32 VGPRs, tests/test_isa.py); off with RCCL, whose
-// collective kernels need more registers than the pass leaves on a CU and would each wait for
-// pass workgroups to drain.  A caller's explicit lookahead setting is kept.
+// dlp_session_set_exchange; between runs): with the peer exchange, the single-rank rule (K = 64,
+// a rank tableau of >= 4 GiB: C3 at P <= 4), where every per-pivot kernel fits beside the form-21
+// pass (the LEAN ratio and pivot-row launches, with the selection and the commit inside: <= 32
+// VGPRs, tests/test_isa.py).  A smaller rank's pass is shorter than its selection chain and
+// lookahead only slows the chain (one rank of C3 at P = 8, 2.15 GB: 20,857 vs 21,352 pivots/s,
+// profiles/r04e/).  Off with RCCL, whose collective kernels need more registers than the pass
+// leaves on a CU and would each wait for pass workgroups to drain.  A caller's
+// explicit lookahead setting is kept.
 int la_policy(dlp_session* s) {
     if (!s->la_auto || !s->exchange) return DLP_OK;
-    const bool want = s->xmode == dlp_session::X_PEER && s->d.K == 64 && s->streaming && !s->general;
+    const size_t tbytes = (size_t)(s->rows + 1) * s->ld * sizeof(double);
+    const bool want = s->xmode == dlp_session::X_PEER && s->d.K == 64 && tbytes >= ((size_t)4 << 30) &&
+                      !s->general;
     if (want && !s->la) CALL_TRY(la_enable(s, false));
     if (!want && s->la) CALL_TRY(la_disable(s));
     pick_form(s);
@@ -910,7 +915,7 @@ inline const dlp::XPeers* xp_of(const dlp_session* s) {
 int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     const dlp_options& o = s->opt;
     const dlp::XPeers* xp = xp_of(s);
-    const bool xf = xp && s->xfuse && s->nranks > 1;   // selection + commit inside the chain launches
+    const bool xf = xp && s->xfuse;   // selection + commit inside the chain launches
     // timing 2: 5 events per pivot (every phase); timing 1: 2 events around the pass only
     hipEvent_t* ev = s->ev_per_pivot == 5 ? &s->ev[(size_t)slot * 5] : nullptr;
     hipEvent_t* evp = s->ev_per_pivot == 2 ? &s->ev[(size_t)slot * 2] : nullptr;

@@ -185,7 +185,7 @@ def test_peer_row_push_is_drained():
         else:
             raise AssertionError(f"{name}: no flag store after the row push")
         checked += 1
-    assert checked >= 4, checked
+    assert checked >= 3, checked
 
 
 def test_no_bit_cast_of_a_vector_element_in_kernels():
