@@ -349,6 +349,25 @@ __device__ __forceinline__ void ratio_defer_body(
     }
     c = cand_red(c);
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 4);
+    if (xp && xsel) {
+        // peer exchange, selection in this launch: every workgroup's candidate straight into slot
+        // [seq & 1][me][blockIdx] of every rank (no partials, no ticket); workgroup 0 of every rank
+        // waits for all of them, reduces them in the candidate order and selects (every rank
+        // reaches the same p).  A workgroup's reads of the state are done before it pushes, so the
+        // selection never races them.
+        if (threadIdx.x == 0) x_push_cand(xp, xseq, c, (int)blockIdx.x);
+        if (blockIdx.x != 0) return;
+        __shared__ int s_xok;
+        Cand w;
+        if (!x_gather_all(xp, xseq, &w, &s_xok)) {
+            if (threadIdx.x == 0) st->status = kStatusXFail;
+            return;
+        }
+        w = cand_red(w);
+        if (threadIdx.x == 0) do_select(st, w, q, basis, row_first, rows, pricing, log, log_cap, true);
+        if constexpr (LEAN) CHAIN_STAMP(slot, 6);
+        return;
+    }
 
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)partials, (short)0, (int)(nblocks * sizeof(Cand)), 0x00020000);
@@ -388,22 +407,7 @@ __device__ __forceinline__ void ratio_defer_body(
             release_go(st);
         }
     }
-    if (xp && xsel) {
-        // the selection in this workgroup (no select launch): wait for every rank's candidate of
-        // this exchange, reduce them in rank order, select (every rank reaches the same p)
-        __shared__ Cand s_xc[kMaxRanks];
-        __shared__ int s_xok;
-        if (!x_gather_cands(xp, xseq, s_xc, &s_xok)) {
-            if (threadIdx.x == 0) st->status = kStatusXFail;
-            return;
-        }
-        if (threadIdx.x == 0) {
-            Cand w = cand_empty();
-            for (int r = 0; r < xp->nranks; ++r)
-                if (cand_better(s_xc[r], w)) w = s_xc[r];
-            do_select(st, w, q, basis, row_first, rows, pricing, log, log_cap, true);
-        }
-    }
+
     if constexpr (LEAN) CHAIN_STAMP(slot, 6);
 }
 
@@ -575,16 +579,19 @@ __device__ __forceinline__ void prow_defer_body(
         pr.y = t.y / piv;
     } else if (owner_lane) {
         d2 t = t0;
-        // chunks of CH pivot rows: loads issued back to back (row index clamped), then applied
-        // in order
-        constexpr int CH = 8;
-        for (int l0 = 0; l0 < S; l0 += CH) {
-            d2 pv[CH];
+        // chunks of CH pivot rows (row index clamped), double-buffered: the next chunk's loads are
+        // issued before this chunk is applied, so up to 2 CH rows are in flight (c3r8: the replay
+        // was 7 us per pivot with one chunk of 8 in flight, profiles/r04e/)
+        constexpr int CH = 16;
+        d2 pa[CH], pb[CH];
+        auto fetch = [&](d2 (&pv)[CH], int l0) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 const int l = min(l0 + u, S - 1);
                 pv[u] = *(const d2*)((l < kp ? Pp + (int64_t)l * ld : P + (int64_t)(l - kp) * ld) + j);
             }
+        };
+        auto apply = [&](const d2 (&pv)[CH], int l0) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 const int l = l0 + u;
@@ -597,6 +604,14 @@ __device__ __forceinline__ void prow_defer_body(
                     }
                 }
             }
+        };
+        if (S > 0) fetch(pa, 0);
+        for (int l0 = 0; l0 < S; l0 += 2 * CH) {
+            if (l0 + CH < S) fetch(pb, l0 + CH);
+            apply(pa, l0);
+            if (l0 + CH >= S) break;
+            if (l0 + 2 * CH < S) fetch(pa, l0 + 2 * CH);
+            apply(pb, l0 + CH);
         }
         const double piv = st->piv;
         pr.x = t.x / piv;

@@ -159,7 +159,9 @@ __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* ba
         return;
     }
     const int32_t p = best.row;
-    const int32_t leaving = basis[p];
+    // the leaving variable: every candidate carries basis[row] (ratio and drive-out kernels), so no
+    // dependent load of basis[p] on the selection's critical path
+    const int32_t leaving = best.basis_var;
     basis[p] = q;
     st->q = q;
     st->p = p;
@@ -223,28 +225,57 @@ __device__ inline bool x_wait(const XPeers* xp, const uint64_t* flag, uint64_t s
         }
     }
 }
-__device__ inline uint64_t* x_cflag(const XPeers* xp, int rank, int parity, int sender) {
-    return xp->base[rank] + (int64_t)parity * xp->nranks + sender;
+__device__ inline uint64_t* x_cflag(const XPeers* xp, int rank, int parity, int sender, int w = 0) {
+    return xp->base[rank] + ((int64_t)parity * xp->nranks + sender) * xp->nslot + w;
 }
-__device__ inline uint64_t* x_cslot(const XPeers* xp, int rank, int parity, int sender) {
-    return xp->base[rank] + xp->off_cslot + ((int64_t)parity * xp->nranks + sender) * 4;
+__device__ inline uint64_t* x_cslot(const XPeers* xp, int rank, int parity, int sender, int w = 0) {
+    return xp->base[rank] + xp->off_cslot + (((int64_t)parity * xp->nranks + sender) * xp->nslot + w) * 4;
 }
 __device__ inline uint64_t* x_rflag(const XPeers* xp, int rank, int64_t chunk) {
     return xp->base[rank] + xp->off_rflag + chunk;
 }
 __device__ inline uint64_t* x_row(const XPeers* xp, int rank) { return xp->base[rank] + xp->off_row; }
 
-// One lane: this rank's candidate into slot [seq & 1][me] of every rank, then the flags.
-__device__ inline void x_push_cand(const XPeers* xp, uint32_t seq, const Cand& c) {
+// One lane: a candidate into slot [seq & 1][me][w] of every rank, then the flags.
+__device__ inline void x_push_cand(const XPeers* xp, uint32_t seq, const Cand& c, int w = 0) {
     const int par = (int)(seq & 1u);
     const uint64_t* cv = (const uint64_t*)&c;
     for (int r = 0; r < xp->nranks; ++r) {
-        uint64_t* slot = x_cslot(xp, r, par, xp->me);
+        uint64_t* slot = x_cslot(xp, r, par, xp->me, w);
 #pragma unroll
         for (int k = 0; k < 4; ++k) x_store(slot + k, cv[k]);
     }
     x_drain();   // the slots are complete before any flag
-    for (int r = 0; r < xp->nranks; ++r) x_store(x_cflag(xp, r, par, xp->me), seq);
+    for (int r = 0; r < xp->nranks; ++r) x_store(x_cflag(xp, r, par, xp->me, w), seq);
+}
+
+// Workgroup (xfuse): every rank's ratio-workgroup candidates of exchange seq, reduced in the
+// candidate order (any grouping gives the same winner); false when a wait failed.  Lane t takes
+// slots t, t + blockDim, ... of the flattened (sender, workgroup) list.
+__device__ inline bool x_gather_all(const XPeers* xp, uint32_t seq, Cand* best, int* s_ok) {
+    const int par = (int)(seq & 1u);
+    if (threadIdx.x == 0) *s_ok = 1;
+    __syncthreads();
+    Cand b = cand_empty();
+    int r = 0, base = 0;   // the sender of slot t: nrat prefix sums, walked forward with t
+    for (int t = threadIdx.x;; t += blockDim.x) {
+        while (r < xp->nranks && t >= base + xp->nrat[r]) base += xp->nrat[r++];
+        if (r >= xp->nranks) break;
+        const int w = t - base;
+        if (!x_wait(xp, x_cflag(xp, xp->me, par, r, w), seq)) {
+            *s_ok = 0;
+            break;
+        }
+        const uint64_t* slot = x_cslot(xp, xp->me, par, r, w);
+        Cand o;
+        uint64_t* ov = (uint64_t*)&o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ov[k] = x_load(slot + k);
+        if (cand_better(o, b)) b = o;
+    }
+    *best = b;
+    __syncthreads();
+    return *s_ok != 0;
 }
 
 // Workgroup (>= nranks lanes): the P candidates of exchange seq into lds[0..P); false

@@ -91,8 +91,11 @@ __host__ __device__ inline bool cand_better(const Cand& a, const Cand& b) {
 // between devices; plain stores between sessions on one device), each message followed by
 // a tagged flag, instead of an RCCL all-gather + all-reduce.  One block per rank, in
 // uncached device memory, laid out identically on every rank (uint64 words):
-//   [0, 2P)                    candidate flags  cflag[parity][sender]  (= exchange seq)
-//   [off_cslot, +8P)           candidate slots  cslot[parity][sender]  (4 words = 32 B)
+//   [0, 2PS)                   candidate flags  cflag[parity][sender][w]  (= exchange seq)
+//   [off_cslot, +8PS)          candidate slots  cslot[parity][sender][w]  (4 words = 32 B)
+// with S = nslot slots per sender: slot w = 0 carries the rank's candidate (the select kernel's
+// exchange), or, when the ratio launch selects (xfuse), w = the ratio workgroup: every workgroup
+// pushes its own candidate and workgroup 0 of every rank reduces all of them (no ticket).
 //   [off_rflag, +nchunks)      pivot-row chunk flags (512 columns per chunk)
 //   [off_row, +ld)             the pivot row (fp64 bits), written by its owner
 // Every wait is bounded (wait_ticks of the 100 MHz constant clock: the host's exchange timeout
@@ -108,9 +111,11 @@ struct XPeers {
     uint64_t wait_ticks;         // bound of one wait (0: the abort word only)
     int64_t nchunks;
     int64_t off_cslot, off_rflag, off_row;
+    int32_t nslot;               // candidate slots per sender (>= every rank's ratio workgroups)
+    int32_t nrat[kMaxRanks];     // ratio workgroups of each rank (its candidates under xfuse)
 };
-// Block size (bytes) and offsets for nranks ranks and row length ld.
-size_t xblock_layout(int nranks, int64_t ld, XPeers* xp);
+// Block size (bytes) and offsets for nranks ranks, row length ld and nslot slots per sender.
+size_t xblock_layout(int nranks, int64_t ld, int nslot, XPeers* xp);
 
 // Deferred rank-k update (dlp_defer.hip).  Up to K pivots are selected against
 // the stale HBM tableau T0 through "replayed" views (column q and pivot row p

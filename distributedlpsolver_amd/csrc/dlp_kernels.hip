@@ -814,14 +814,15 @@ hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32
     return hipGetLastError();
 }
 
-size_t xblock_layout(int nranks, int64_t ld, XPeers* xp) {
-    const int64_t P = nranks;
+size_t xblock_layout(int nranks, int64_t ld, int nslot, XPeers* xp) {
+    const int64_t P = nranks, S = nslot;
     const int64_t nch = (ld + kXChunk - 1) / kXChunk;
-    const int64_t off_cslot = (2 * P + 7) / 8 * 8;
-    const int64_t off_rflag = off_cslot + 8 * P;
+    const int64_t off_cslot = (2 * P * S + 7) / 8 * 8;
+    const int64_t off_rflag = off_cslot + 8 * P * S;
     const int64_t off_row = (off_rflag + nch + 511) / 512 * 512;   // 4 KiB aligned
     if (xp) {
         xp->nranks = nranks;
+        xp->nslot = nslot;
         xp->nchunks = nch;
         xp->off_cslot = off_cslot;
         xp->off_rflag = off_rflag;

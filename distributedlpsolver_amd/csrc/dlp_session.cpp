@@ -171,6 +171,9 @@ struct dlp_session {
     // that share a device (their phases must stay in separate launches)
     bool xfuse = true;
     std::string xreason;   // why an auto exchange fell back to RCCL (empty: it did not)
+    // allocations from the buffer pool (size class per pointer), returned to it at free
+    std::vector<std::pair<void*, size_t>> pooled;
+    bool pool_ok = true;   // false once the stream failed: its buffers are freed, not pooled
 };
 
 extern "C" int flush_pending(dlp_session* s);   // defined with the C entry points
@@ -217,6 +220,76 @@ void release_stream(int device, int prio, hipStream_t s) {
     }
     (void)hipGetLastError();
     (void)hipStreamDestroy(s);
+}
+
+// Small device buffers (and the pinned state copy) are reused across sessions the same way:
+// C1 (200 x 400) spent 0.6 ms of its 6.7 ms end to end in the ~18 hipFree calls of a session's
+// teardown and ~0.2 ms in the allocations (DLP_TRACE_CREATE, profiles/r03g/).  Freed buffers of at
+// most kBufPoolMax bytes go to a per-device pool keyed by their power-of-two size class (at most
+// kBufPoolTotal bytes and kBufPoolCount entries cached); a session takes an exact class match.
+// Tableaus and other large buffers are never pooled.  Contents are not cleared: every buffer is
+// initialised by the session before it is read, as a fresh hipMalloc's would have to be.
+constexpr size_t kBufPoolMax = (size_t)16 << 20;
+constexpr size_t kBufPoolTotal = (size_t)256 << 20;
+constexpr size_t kBufPoolCount = 256;
+struct PooledBuf {
+    int device;   // -1: pinned host memory
+    size_t cls;
+    void* p;
+};
+std::mutex g_buf_mu;
+std::vector<PooledBuf> g_buf_pool;
+size_t g_buf_total = 0;
+
+size_t size_class(size_t bytes) {
+    size_t c = 256;
+    while (c < bytes) c <<= 1;
+    return c;
+}
+
+// device < 0: pinned host memory (hipHostMallocDefault)
+hipError_t pool_alloc(dlp_session* s, int device, void** p, size_t bytes) {
+    const size_t cls = size_class(bytes);
+    if (cls <= kBufPoolMax) {
+        std::lock_guard<std::mutex> lk(g_buf_mu);
+        for (size_t k = g_buf_pool.size(); k-- > 0;)
+            if (g_buf_pool[k].device == device && g_buf_pool[k].cls == cls) {
+                *p = g_buf_pool[k].p;
+                g_buf_total -= cls;
+                g_buf_pool.erase(g_buf_pool.begin() + (ptrdiff_t)k);
+                s->pooled.push_back({*p, cls});
+                return hipSuccess;
+            }
+    }
+    const bool pool = cls <= kBufPoolMax;
+    const hipError_t e = device < 0 ? hipHostMalloc(p, pool ? cls : bytes, hipHostMallocDefault)
+                                    : hipMalloc(p, pool ? cls : bytes);
+    if (e == hipSuccess && pool) s->pooled.push_back({*p, cls});
+    return e;
+}
+
+// Free p (a session buffer): back to the pool when it came from it and the session is healthy.
+void pool_release(dlp_session* s, int device, void* p) {
+    if (!p) return;
+    size_t cls = 0;
+    for (auto& e : s->pooled)
+        if (e.first == p) {
+            cls = e.second;
+            e.first = nullptr;
+            break;
+        }
+    if (cls && s->pool_ok) {
+        std::lock_guard<std::mutex> lk(g_buf_mu);
+        if (g_buf_total + cls <= kBufPoolTotal && g_buf_pool.size() < kBufPoolCount) {
+            g_buf_pool.push_back({device, cls, p});
+            g_buf_total += cls;
+            return;
+        }
+    }
+    if (device < 0)
+        (void)hipHostFree(p);
+    else
+        (void)hipFree(p);
 }
 
 // DLP_TRACE_CREATE=1: milliseconds of each stage of session creation / free on stderr
@@ -335,7 +408,9 @@ void free_session(dlp_session* s) {
     if (!s) return;
     StageClock clk;
     if (s->device >= 0) (void)hipSetDevice(s->device);
-    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->stream && hipStreamSynchronize(s->stream) != hipSuccess) s->pool_ok = false;
+    if (s->pstream && hipStreamSynchronize(s->pstream) != hipSuccess) s->pool_ok = false;
+    (void)hipGetLastError();
     clk.mark("free: sync");
     // diagnostics: DLP_CHAIN_STAMPS=<file> dumps the chain kernels' phase stamps (tools only)
     if (const char* path = std::getenv("DLP_CHAIN_STAMPS")) {
@@ -354,22 +429,20 @@ void free_session(dlp_session* s) {
     void* dev[] = {s->Tb[0] ? s->Tb[0] : s->T, s->Tb[1], s->colq, s->prow_send, s->partials,
                    s->cand_send, s->cand_recv, s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc,
                    s->d.P, s->d.rhs, s->d.nzc, s->cl_gran, s->band_cnt};
-    for (void* p : dev)
-        if (p) (void)hipFree(p);
+    for (void* p : dev) pool_release(s, s->device, p);
     if (s->la || s->dslot[1].C) {   // slot 0 aliases s->d
         void* sl[] = {s->dslot[1].C, s->dslot[1].Cc, s->dslot[1].P, s->dslot[1].nzc};
-        for (void* p : sl)
-            if (p) (void)hipFree(p);
+        for (void* p : sl) pool_release(s, s->device, p);
     }
     if (s->ev_seal) (void)hipEventDestroy(s->ev_seal);
     if (s->ev_pass) (void)hipEventDestroy(s->ev_pass);
     if (s->pstream) release_stream(s->device, s->prio_pass, s->pstream);
-    if (s->prow_recv && s->prow_recv != s->prow_send) (void)hipFree(s->prow_recv);
+    if (s->prow_recv && s->prow_recv != s->prow_send) pool_release(s, s->device, s->prow_recv);
     for (void* p : s->ipc_open) (void)hipIpcCloseMemHandle(p);
     if (s->xblk) (void)hipFree(s->xblk);
     if (s->xpeers) (void)hipFree(s->xpeers);
     if (s->xabort) (void)hipHostFree(s->xabort);
-    if (s->host_st) (void)hipHostFree(s->host_st);
+    pool_release(s, -1, s->host_st);
     clk.mark("free: buffers");
     if (s->stream) release_stream(s->device, s->prio_chain, s->stream);
     clk.mark("free: stream");
@@ -427,7 +500,7 @@ int la_enable(dlp_session* s, bool forced) {
     CALL_TRY(flush_pending_block(s));
     const int c = (s->Tb[1] && s->T == s->Tb[1]) ? 1 : 0;   // the current buffer
     if (!s->Tb[0]) s->Tb[0] = s->T;
-    if (!s->Tb[1 - c] && hipMalloc(&s->Tb[1 - c], tbytes) != hipSuccess) {
+    if (!s->Tb[1 - c] && pool_alloc(s, s->device, (void**)&s->Tb[1 - c], tbytes) != hipSuccess) {
         set_error("hipMalloc of the second tableau buffer failed");
         return DLP_ERR_OOM;
     }
@@ -450,17 +523,17 @@ int la_enable(dlp_session* s, bool forced) {
         const int64_t kt = s->d.K <= 4 ? 4 : s->d.K <= 8 ? 8 : s->d.K <= 16 ? 16 : s->d.K <= 32 ? 32 : 64;
         d1.C = d1.Cc = d1.P = nullptr;
         d1.nzc = nullptr;
-        HIP_TRY(hipMalloc(&d1.C, sizeof(double) * s->d.K * (rows_total + 1)));
-        HIP_TRY(hipMalloc(&d1.Cc, sizeof(double) * s->d.K * s->d.ldcc));
-        HIP_TRY(hipMalloc(&d1.P, sizeof(double) * kt * s->ld));
-        HIP_TRY(hipMalloc(&d1.nzc, sizeof(int32_t) * (s->rows + 1)));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&d1.C, sizeof(double) * s->d.K * (rows_total + 1)));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&d1.Cc, sizeof(double) * s->d.K * s->d.ldcc));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&d1.P, sizeof(double) * kt * s->ld));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&d1.nzc, sizeof(int32_t) * (s->rows + 1)));
         HIP_TRY(hipMemsetAsync(d1.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
         HIP_TRY(hipMemsetAsync(d1.Cc, 0, sizeof(double) * s->d.K * s->d.ldcc, s->stream));
         HIP_TRY(hipMemsetAsync(d1.P, 0, sizeof(double) * kt * s->ld, s->stream));
     }
     if (!s->band_cnt) {
         s->band_stride = (s->rows + 63) / 64 + 1;   // bands of >= 64 rows
-        HIP_TRY(hipMalloc(&s->band_cnt, sizeof(uint32_t) * 2 * s->band_stride));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->band_cnt, sizeof(uint32_t) * 2 * s->band_stride));
     }
     HIP_TRY(hipMemsetAsync(s->band_cnt, 0, sizeof(uint32_t) * 2 * s->band_stride, s->stream));
     if (!s->pstream) HIP_TRY(acquire_stream(s->device, s->prio_pass, &s->pstream));
@@ -638,14 +711,14 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block : auto_rows_per_block(s);
     g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
     const size_t tbytes = (size_t)rows_total * s->ld * sizeof(double);
-    if (hipMalloc(&s->T, tbytes) != hipSuccess) {
+    if (pool_alloc(s, s->device, (void**)&s->T, tbytes) != hipSuccess) {
         set_error("hipMalloc of the tableau failed (" + std::to_string(tbytes) + " bytes)");
         return DLP_ERR_OOM;
     }
     g.T = s->T;
     clk.mark("create: plan + tableau");
     if (s->cluster) {
-        HIP_TRY(hipMalloc(&s->cl_gran, sizeof(uint64_t) * dlp::cluster_granules(s->m, s->cl_wg)));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->cl_gran, sizeof(uint64_t) * dlp::cluster_granules(s->m, s->cl_wg)));
     }
     s->ratio_blocks = dlp::ratio_blocks(g);
     {
@@ -657,35 +730,35 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
                        dlp::fused_pivot_blocks(g) <= std::min(2 * cus, dlp::fused_pivot_capacity(s->d.K, cus));
     }
     s->ratio_blocks_max = std::max(s->ratio_blocks, dlp::ratio_defer_blocks(g));
-    HIP_TRY(hipMalloc(&s->colq, sizeof(double) * (rows_total + dlp::kColqPad)));
+    HIP_TRY(pool_alloc(s, s->device, (void**)&s->colq, sizeof(double) * (rows_total + dlp::kColqPad)));
     HIP_TRY(hipMemsetAsync(s->colq, 0, sizeof(double) * (rows_total + dlp::kColqPad), s->stream));
     s->exchange = nranks > 1 || rccl;
-    HIP_TRY(hipMalloc(&s->prow_send, sizeof(int64_t) * s->ld));
+    HIP_TRY(pool_alloc(s, s->device, (void**)&s->prow_send, sizeof(int64_t) * s->ld));
     if (s->exchange)
-        HIP_TRY(hipMalloc(&s->prow_recv, sizeof(int64_t) * s->ld));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->prow_recv, sizeof(int64_t) * s->ld));
     else
         s->prow_recv = s->prow_send;
-    HIP_TRY(hipMalloc(&s->partials, sizeof(dlp::Cand) * s->ratio_blocks_max));
-    HIP_TRY(hipMalloc(&s->cand_send, sizeof(dlp::Cand)));
-    HIP_TRY(hipMalloc(&s->cand_recv, sizeof(dlp::Cand) * nranks));
-    HIP_TRY(hipMalloc(&s->pp, sizeof(dlp::PricePart) * ((s->ld + 511) / 512)));
-    HIP_TRY(hipMalloc(&s->basis, sizeof(int32_t) * s->m));
-    HIP_TRY(hipMalloc(&s->st, sizeof(dlp::DevState)));
+    HIP_TRY(pool_alloc(s, s->device, (void**)&s->partials, sizeof(dlp::Cand) * s->ratio_blocks_max));
+    HIP_TRY(pool_alloc(s, s->device, (void**)&s->cand_send, sizeof(dlp::Cand)));
+    HIP_TRY(pool_alloc(s, s->device, (void**)&s->cand_recv, sizeof(dlp::Cand) * nranks));
+    HIP_TRY(pool_alloc(s, s->device, (void**)&s->pp, sizeof(dlp::PricePart) * ((s->ld + 511) / 512)));
+    HIP_TRY(pool_alloc(s, s->device, (void**)&s->basis, sizeof(int32_t) * s->m));
+    HIP_TRY(pool_alloc(s, s->device, (void**)&s->st, sizeof(dlp::DevState)));
     s->log_cap = opt->log_pivots ? std::max<int64_t>(1, opt->max_pivots) : 0;
-    if (s->log_cap > 0) HIP_TRY(hipMalloc(&s->log, sizeof(dlp_pivot) * s->log_cap));
-    HIP_TRY(hipHostMalloc(&s->host_st, sizeof(dlp::DevState), hipHostMallocDefault));
+    if (s->log_cap > 0) HIP_TRY(pool_alloc(s, s->device, (void**)&s->log, sizeof(dlp_pivot) * s->log_cap));
+    HIP_TRY(pool_alloc(s, -1, (void**)&s->host_st, sizeof(dlp::DevState)));
     if (s->d.K > 1) {
         s->d.ldc = s->d.K;
-        HIP_TRY(hipMalloc(&s->d.C, sizeof(double) * s->d.K * (rows_total + 1)));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->d.C, sizeof(double) * s->d.K * (rows_total + 1)));
         s->d.ldcc = (rows_total + 1 + 63) / 64 * 64;
-        HIP_TRY(hipMalloc(&s->d.Cc, sizeof(double) * s->d.K * s->d.ldcc));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->d.Cc, sizeof(double) * s->d.K * s->d.ldcc));
         HIP_TRY(hipMemsetAsync(s->d.Cc, 0, sizeof(double) * s->d.K * s->d.ldcc, s->stream));
         // P is sized for the pass template's block (K rounded up to 4/8/16/32/64), so a
         // kernel instance never addresses past it, whatever the session's K
         const int64_t kt = s->d.K <= 4 ? 4 : s->d.K <= 8 ? 8 : s->d.K <= 16 ? 16 : s->d.K <= 32 ? 32 : 64;
-        HIP_TRY(hipMalloc(&s->d.P, sizeof(double) * kt * s->ld));
-        HIP_TRY(hipMalloc(&s->d.rhs, sizeof(double) * (s->rows + 1)));
-        HIP_TRY(hipMalloc(&s->d.nzc, sizeof(int32_t) * (s->rows + 1)));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->d.P, sizeof(double) * kt * s->ld));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->d.rhs, sizeof(double) * (s->rows + 1)));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->d.nzc, sizeof(int32_t) * (s->rows + 1)));
         HIP_TRY(hipMemsetAsync(s->d.C, 0, sizeof(double) * s->d.K * (rows_total + 1), s->stream));
         HIP_TRY(hipMemsetAsync(s->d.P, 0, sizeof(double) * kt * s->ld, s->stream));
         s->defer_rb_req = opt->rows_per_block > 0 ? opt->rows_per_block : 0;
@@ -1587,6 +1660,23 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
 }
 
 // ---- peer exchange set-up ------------------------------------
+// Every rank's ratio workgroups (its candidates when the ratio launch selects) from the same row
+// partition every rank computes (dlp_rank_rows; a general LP with artificials carries its Phase II
+// objective row on the last rank); returns the slots per sender, identical on every rank.
+int xslots(const dlp_session* s, dlp::XPeers* x) {
+    const bool carry = s->general && s->prob_dims.sf.nart > 0;
+    int nslot = 1;
+    for (int r = 0; r < s->nranks && r < dlp::kMaxRanks; ++r) {
+        int64_t first = 0, count = 0;
+        (void)dlp_rank_rows(s->m, r, s->nranks, &first, &count);
+        if (carry && r == s->nranks - 1) count += 1;
+        const int nrat = (int)((count + 1 + dlp::kRatioDeferThreads - 1) / dlp::kRatioDeferThreads);
+        x->nrat[r] = nrat;
+        nslot = std::max(nslot, nrat);
+    }
+    return nslot;
+}
+
 // This rank's exchange block (uncached device memory, zeroed: flags start below every seq)
 // and the pinned abort word its waits read.
 int ensure_xblock(dlp_session* s) {
@@ -1600,7 +1690,7 @@ int ensure_xblock(dlp_session* s) {
         return DLP_ERR_UNSUPPORTED;
     }
     HIP_TRY(hipSetDevice(s->device));
-    const size_t bytes = dlp::xblock_layout(s->nranks, s->ld, &s->xpeers_host);
+    const size_t bytes = dlp::xblock_layout(s->nranks, s->ld, xslots(s, &s->xpeers_host), &s->xpeers_host);
     void* p = nullptr;
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess) {
         s->xblk_uncached = true;
@@ -1627,7 +1717,7 @@ uint64_t xwait_ticks(double stall_limit_s) {
 // Install the peer table (bases[r] = rank r's block as this device addresses it).
 int install_peers(dlp_session* s, const std::vector<uint64_t*>& bases) {
     dlp::XPeers& x = s->xpeers_host;
-    (void)dlp::xblock_layout(s->nranks, s->ld, &x);
+    (void)dlp::xblock_layout(s->nranks, s->ld, xslots(s, &x), &x);
     for (int r = 0; r < dlp::kMaxRanks; ++r) x.base[r] = r < (int)bases.size() ? bases[r] : nullptr;
     x.me = s->rank;
     x.wait_ticks = xwait_ticks(s->stall_limit_s);
