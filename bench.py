@@ -53,7 +53,12 @@ WORKLOADS = {
     # exchange stores a rank of the split runs; only the xGMI latency is missing
     "c3r8": (4096, 61440, 38, "C3 rank geometry at P = 8: dense LP 4096 x 61440 (+4096 slack), fp64 "
                               "tableau 4097 x 65537 = one rank of the 8-GPU C3 split, 1-rank exchange"),
+    "c3r4": (8192, 57344, 34, "C3 rank geometry at P = 4: dense LP 8192 x 57344 (+8192 slack), fp64 "
+                              "tableau 8193 x 65537 = one rank of the 4-GPU C3 split, 1-rank exchange"),
+    "c3r2": (16384, 49152, 32, "C3 rank geometry at P = 2: dense LP 16384 x 49152 (+16384 slack), fp64 "
+                               "tableau 16385 x 65537 = one rank of the 2-GPU C3 split, 1-rank exchange"),
 }
+RANK_WORKLOADS = ("c3r2", "c3r4", "c3r8")
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP64_PEAK_TFS = 77.3   # measured v_fma_f64 peak on MI355X (tools/passlab.hip valu probe)
 
@@ -286,8 +291,9 @@ def main():
         rccl_id = obj[0]
     else:
         dist = None
-        # c3r8: a 1-rank communicator, so the rank's exchange kernels run (select / commit waits)
-        rccl_id = dlp.comm_unique_id() if args.workload == "c3r8" else None
+        # c3r2/4/8: a 1-rank communicator, so the rank's exchange kernels run (candidate and row
+        # pushes, the waits)
+        rccl_id = dlp.comm_unique_id() if args.workload in RANK_WORKLOADS else None
     xsess = world > 1 or rccl_id is not None
     xopt = {"auto": getattr(L, "XCHG_DEFAULT", 0), "rccl": L.XCHG_RCCL, "peer": L.XCHG_PEER}[args.exchange]
 

@@ -140,7 +140,7 @@ __device__ __forceinline__ void ratio_defer_body(
     dlp_pivot* log, int64_t log_cap, int nblocks, const double* __restrict__ Ccp = nullptr,
     const double* __restrict__ Pp = nullptr, int prev_seal = -1, const XPeers* xp = nullptr,
     uint32_t xseq = 0, uint32_t* bcnt = nullptr, int brb = 1, int bnt = 0, const double* Tn = nullptr,
-    int xsel = 0) {
+    int xsel = 0, uint32_t rseq = 0) {
     __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
     __shared__ Cand lds_c[kRatioDeferThreads / 64];
     __shared__ int s_last;
@@ -228,6 +228,7 @@ __device__ __forceinline__ void ratio_defer_body(
             st->q = -1;
             st->status = DLP_OK;
             if constexpr (FUSED) release_go(st);
+            if (xsel == 2) sel_publish(st, rseq, DLP_OK, 0.0);   // the pivot-row workgroups end too
         }
         return;
     }
@@ -360,11 +361,20 @@ __device__ __forceinline__ void ratio_defer_body(
         __shared__ int s_xok;
         Cand w;
         if (!x_gather_all(xp, xseq, &w, &s_xok)) {
-            if (threadIdx.x == 0) st->status = kStatusXFail;
+            if (threadIdx.x == 0) {
+                st->status = kStatusXFail;
+                if (xsel == 2) sel_publish(st, rseq, kStatusXFail, 0.0);
+            }
             return;
         }
         w = cand_red(w);
-        if (threadIdx.x == 0) do_select(st, w, q, basis, row_first, rows, pricing, log, log_cap, true);
+        if (threadIdx.x == 0) {
+            // one-launch pivot: z_q (the objective row is current; this launch's commit writes it
+            // only after the record) before the selection, which writes the log entry's other fields
+            const double zq = xsel == 2 ? T[rows * ld + q] : 0.0;
+            do_select(st, w, q, basis, row_first, rows, pricing, log, log_cap, true, xsel != 2);
+            if (xsel == 2) sel_publish(st, rseq, st->status, zq);
+        }
         if constexpr (LEAN) CHAIN_STAMP(slot, 6);
         return;
     }
@@ -444,26 +454,27 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
-// pricing partial of this 512-column tile; objective value into the log.
+// pricing partial of this 512-column tile (pp[tile]); objective value into log[klog].
 // Same per-element operations as the eager update kernel's objective band.
-// z / zq: the caller's early loads of T[rows][j..j+1] and C[rows][s] (PRE), else loaded here
-template <bool PRE = false>
+// ZQ: 0 = z_q from C[rows][s]; 1 = the caller's early loads of T[rows][j..j+1] (zpre) and z_q
+// (zqv); 2 = z_q given (zqv: the selection record of a one-launch pivot), z loaded here
+template <int ZQ = 0>
 __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
-                                  int64_t nprice, const DevState* st, const double* __restrict__ C,
+                                  int64_t nprice, int64_t klog, const double* __restrict__ C,
                                   int64_t ldc, double* __restrict__ P, int s, int64_t j, d2 pr,
-                                  PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
-                                  PricePart* lds_pp, d2 zpre = d2{0.0, 0.0}, double zqpre = 0.0) {
+                                  PricePart* pp, int tile, double tol_dj, dlp_pivot* log, int64_t log_cap,
+                                  PricePart* lds_pp, d2 zpre = d2{0.0, 0.0}, double zqv = 0.0) {
     const int64_t width = (ncols + 16) & ~(int64_t)15;
     if (j < ld) {
         *(d2*)(P + (int64_t)s * ld + j) = pr;
         if (s == 0)   // block start: pivot rows 1..K-1 := +0 (see the ratio kernel's C tails)
             for (int64_t l = 1; l < ldc; ++l) *(d2*)(P + l * ld + j) = d2{0.0, 0.0};
     }
-    const double zq = PRE ? zqpre : C[rows * ldc + s];
+    const double zq = ZQ == 0 ? C[rows * ldc + s] : zqv;
     PricePart acc = pp_empty();
     if (j < width) {
         double* zp = T + rows * ld + j;
-        d2 z = PRE ? zpre : *(const d2*)zp;
+        d2 z = ZQ == 1 ? zpre : *(const d2*)zp;
         if (zq != 0.0) {
             z.x = __builtin_fma(-zq, pr.x, z.x);
             z.y = __builtin_fma(-zq, pr.y, z.y);
@@ -471,12 +482,11 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
         }
         price_pair(acc, z.x, z.y, j, nprice, tol_dj);
         if (log && j <= ncols && ncols < j + 2) {
-            const int64_t k = st->npivots - 1;
-            if (k >= 0 && k < log_cap) log[k].objective = (ncols == j) ? z.x : z.y;
+            if (klog >= 0 && klog < log_cap) log[klog].objective = (ncols == j) ? z.x : z.y;
         }
     }
     acc = block_price(acc, lds_pp);
-    if (threadIdx.x == 0) pp[blockIdx.x] = acc;
+    if (threadIdx.x == 0) pp[tile] = acc;
 }
 
 // a3 first half on the replayed pivot row: T_s[p] = steps 0..s-1 applied to
@@ -491,8 +501,11 @@ __device__ __forceinline__ void prow_defer_body(
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
     int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
     int fused, const double* __restrict__ Cp, const double* __restrict__ Pp, int prev_seal,
-    const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn, int xcommit) {
+    const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn, int xcommit,
+    int tile, int onelaunch = 0) {
     __shared__ PricePart lds_pp[4];
+    __shared__ SelView s_sel;
+    __shared__ int s_selok;
     __shared__ double s_cp[kMaxReplay];
     __shared__ int32_t s_pl[kMaxReplay];
     // LEAN: the replayed pivot rows stream through a per-wave LDS ring by LDS-DMA, RING steps
@@ -504,15 +517,32 @@ __device__ __forceinline__ void prow_defer_body(
     constexpr int RING = RS;
     extern __shared__ double s_dyn[];
     auto s_ring = reinterpret_cast<double(*)[RING][128]>(s_dyn);
-    if (st->status != DLP_RUNNING) return;
-    const int64_t slot = st->npivots - 1;
-    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 8);
-    const int s = st->blk - 1;
+    if (st->status != DLP_RUNNING) return;   // an earlier launch ended the solve
+    // the selection: from the state (a launch of its own), or, in a one-launch pivot (peer
+    // exchange), from the record the ratio workgroups of this launch publish (DevState::SelRec)
+    SelView sv;
+    if (onelaunch) {
+        if (!sel_wait(xp, st, xseq, &sv, &s_sel, &s_selok)) {
+            if (threadIdx.x == 0) const_cast<DevState*>(st)->status = kStatusXFail;   // (writable memory)
+            return;
+        }
+        if (sv.status != DLP_RUNNING) return;
+    } else {
+        sv.status = DLP_RUNNING;
+        sv.p_local = st->p_local;
+        sv.blk = st->blk;
+        sv.piv = st->piv;
+        sv.zq = 0.0;
+        sv.npivots = st->npivots;
+    }
+    const int64_t slot = sv.npivots - 1;
+    if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 8);
+    const int s = sv.blk - 1;
     // replayed steps: the sealed previous block first (lookahead), then this block's s
     const int kp = prev_seal >= 0 ? st->seal[prev_seal].blk : 0;
     const int S = kp + s;
-    const int32_t pl = st->p_local;
-    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    const int32_t pl = sv.p_local;
+    const int64_t j = ((int64_t)tile * blockDim.x + threadIdx.x) * 2;
     const bool owner_lane = pl >= 0 && j < ld;
     // LEAN, band publication: row p final in Tn (its band of the sealed block's pass is done):
     // start there and replay this block's steps only
@@ -556,7 +586,7 @@ __device__ __forceinline__ void prow_defer_body(
             s_pl[l] = l < kp ? st->seal[prev_seal].pl[l] : st->pl[l - kp];
         }
     __syncthreads();
-    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 9);
+    if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 9);
     d2 pr;
     pr.x = 0.0;
     pr.y = 0.0;
@@ -574,7 +604,7 @@ __device__ __forceinline__ void prow_defer_body(
             glds16(psrc(l + RING), lds_addr(&s_ring[wv][l % RING][0]));
         }
         vmwait<0>();   // the ring drained (the clamped tail DMAs) before the block exits
-        const double piv = st->piv;
+        const double piv = sv.piv;
         pr.x = t.x / piv;
         pr.y = t.y / piv;
     } else if (owner_lane) {
@@ -613,25 +643,25 @@ __device__ __forceinline__ void prow_defer_body(
             if (l0 + 2 * CH < S) fetch(pa, l0 + 2 * CH);
             apply(pb, l0 + CH);
         }
-        const double piv = st->piv;
+        const double piv = sv.piv;
         pr.x = t.x / piv;
         pr.y = t.y / piv;
     }
-    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 10);
+    if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 10);
     if (!fused && xp) {   // peer exchange: the owner's row into every rank's row region
         // (scalars first: hipcc of ROCm 7.2 compiles __builtin_bit_cast(T, v.y) of an
         // ext_vector element as a cast of element 0; tests/test_isa.py guards this site)
         const double px = pr.x, py = pr.y;
         if (pl >= 0)      // (uniform per launch)
             x_push_row_chunk(xp, xseq, j, ld, __builtin_bit_cast(uint64_t, px),
-                             __builtin_bit_cast(uint64_t, py));
-        if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 11);
+                             __builtin_bit_cast(uint64_t, py), tile);
+        if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 11);
         if (!xcommit) return;
         // the commit in this launch (no commit launch): the owner commits the row it holds, every
         // other rank waits for this chunk's flag and reads the chunk from its own row region
         if (pl < 0) {
             __shared__ int s_xok;
-            if (threadIdx.x == 0) s_xok = x_wait(xp, x_rflag(xp, xp->me, blockIdx.x), xseq) ? 1 : 0;
+            if (threadIdx.x == 0) s_xok = x_wait(xp, x_rflag(xp, xp->me, tile), xseq) ? 1 : 0;
             __syncthreads();
             if (!s_xok) {
                 if (threadIdx.x == 0) const_cast<DevState*>(st)->status = kStatusXFail;   // (st is writable memory)
@@ -644,9 +674,13 @@ __device__ __forceinline__ void prow_defer_body(
                 pr.y = __builtin_bit_cast(double, b);
             }
         }
-        if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 13);
-        commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap, lds_pp);
-        if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 14);
+        if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 13);
+        if (onelaunch)   // z_q from the record (C[rows][s] is another workgroup's store of this launch)
+            commit_row<2>(T, ld, rows, ncols, nprice, slot, C, ldc, P, s, j, pr, pp, tile, tol_dj, log, log_cap,
+                          lds_pp, d2{0.0, 0.0}, sv.zq);
+        else
+            commit_row(T, ld, rows, ncols, nprice, slot, C, ldc, P, s, j, pr, pp, tile, tol_dj, log, log_cap, lds_pp);
+        if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 14);
         return;
     }
     if (!fused) {
@@ -660,9 +694,9 @@ __device__ __forceinline__ void prow_defer_body(
         }
         return;
     }
-    commit_row<!LEAN>(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
-                      lds_pp, zpre, zqpre);
-    if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 11);
+    commit_row<LEAN ? 0 : 1>(T, ld, rows, ncols, nprice, slot, C, ldc, P, s, j, pr, pp, tile, tol_dj, log,
+                             log_cap, lds_pp, zpre, zqpre);
+    if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 11);
 }
 #define DLP_PROW_ARGS                                                                              \
     double *__restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice, const DevState *st, \
@@ -671,7 +705,7 @@ __device__ __forceinline__ void prow_defer_body(
         const double *__restrict__ Cp, const double *__restrict__ Pp, int prev_seal, const XPeers *xp, \
         uint32_t xseq, uint32_t *bcnt, int brb, int bnt, const double *Tn, int xcommit
 #define DLP_PROW_PASS T, ld, rows, ncols, nprice, st, C, ldc, P, bits, pp, tol_dj, log, log_cap, fused, Cp, Pp, \
-                      prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xcommit
+                      prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xcommit, (int)blockIdx.x
 // The LEAN instance (lookahead at K = 64, beside the form-21 pass) is held to 32 VGPRs in its
 // kernel descriptor: the pass leaves 32 per SIMD (with the LDS-DMA asm, hipcc's descriptor
 // otherwise requested 176 for a body that uses 30, and the kernel could not share a CU).
@@ -685,6 +719,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void prow
 }
 #undef DLP_PROW_ARGS
 #undef DLP_PROW_PASS
+
+// Peer exchange, one launch per pivot (dlp::launch_pivot_x): workgroups [0, nrat) run the ratio
+// test and the selection (every workgroup pushes its candidate to every rank, workgroup 0 reduces
+// all of them, selects and publishes the selection record); workgroups [nrat, nrat + nprow) are the
+// pivot-row workgroups, which wait for the record, replay and push the owner's row and commit it.
+// Workgroups are dispatched in index order, so the ratio workgroups never wait for a slot behind
+// the pivot-row workgroups that wait for them.  LEAN: beside the form-21 pass (32 VGPRs; both
+// bodies' LDS rings are the same size).
+#define DLP_PX_RATIO_ARGS                                                                                       \
+    double *__restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols, int64_t nprice,         \
+        int64_t row_first, int32_t *basis, PricePart *pp, int ntiles, DevState *st, double *__restrict__ C,     \
+        int64_t ldc, double *__restrict__ Cc, int64_t ldcc, double *__restrict__ P, double *__restrict__ rhs,   \
+        int32_t *__restrict__ nzc, int nrat, double tol_dj, double tol_piv, int pricing, dlp_pivot *log,         \
+        int64_t log_cap, const double *__restrict__ Ccp, const double *__restrict__ Pp,                          \
+        const double *__restrict__ Cp, int prev_seal, const XPeers *xp, uint32_t xseq, uint32_t *bcnt, int brb, \
+        int bnt, const double *Tn, int xs
+// (xs = 2, passed at launch: as a compile-time constant hipcc gave the LEAN instance 34 VGPRs, at
+// run time 30 of the 32 the form-21 pass leaves per SIMD)
+#define DLP_PX_BODIES(KM, LEAN_, LCH_, RP_, RS_)                                                                 \
+    if ((int)blockIdx.x < nrat) {                                                                                \
+        ratio_defer_body<KM, false, LEAN_, LCH_, RP_>(T, ld, rows, rows_elig, ncols, row_first, basis, pp,       \
+                                                     ntiles, st, C, ldc, Cc, ldcc, P, rhs, nzc, nullptr,          \
+                                                     nullptr, 2, tol_dj, tol_piv, pricing, log, log_cap, nrat,    \
+                                                     Ccp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xs, xseq); \
+        return;                                                                                                  \
+    }                                                                                                            \
+    prow_defer_body<LEAN_, RS_>(T, ld, rows, ncols, nprice, st, C, ldc, P, nullptr, pp,      \
+                                tol_dj, log, log_cap, 0, Cp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn, 1,     \
+                                (int)blockIdx.x - nrat, 1)
+template <int KMAX>
+__global__ __launch_bounds__(256) void pivot_x_kernel(DLP_PX_RATIO_ARGS) {
+    DLP_PX_BODIES(KMAX, false, 4, kRatioRingPairs, kProwRingSteps);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void pivot_x_lean_kernel(DLP_PX_RATIO_ARGS) {
+    DLP_PX_BODIES(128, true, 0, kRatioRingPairs, kProwRingSteps);
+}
+#undef DLP_PX_BODIES
 
 // Multi-rank: P[s] from the exchanged bits, then the objective row + pricing.
 __global__ __launch_bounds__(256) void commit_defer_kernel(
@@ -719,8 +790,8 @@ __global__ __launch_bounds__(256) void commit_defer_kernel(
     } else if (j < ld) {
         pr = *(const d2*)(bits + j);
     }
-    commit_row(T, ld, rows, ncols, nprice, st, C, ldc, P, s, j, pr, pp, tol_dj, log, log_cap,
-               lds_pp);
+    commit_row(T, ld, rows, ncols, nprice, st->npivots - 1, C, ldc, P, s, j, pr, pp, (int)blockIdx.x, tol_dj, log,
+               log_cap, lds_pp);
     if (blockIdx.x == 0) CHAIN_STAMP(slot, 14);
 }
 
@@ -2252,6 +2323,38 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                                                  nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
                                                  prev_seal >= 0 ? prev->P : nullptr, prev_seal,
                                                  nranks == 1 ? nullptr : xp, xseq, nullptr, 1, 0, nullptr, xc);
+    return hipGetLastError();
+}
+
+hipError_t launch_pivot_x(const Geometry& g, const Defer& d, int32_t* basis, PricePart* pp, DevState* st,
+                          double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
+                          hipStream_t s, const Defer* prev, int prev_seal, const XPeers* xp, uint32_t seq,
+                          const BandPub* bp) {
+    if (!xp) return hipErrorInvalidValue;
+    if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
+    const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
+    const int nrat = ratio_defer_blocks(g);
+    const int nprow = (int)((g.ld + kDeferTile - 1) / kDeferTile);
+    const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
+    const double* Ccp = prev_seal >= 0 ? prev->Cc : nullptr;
+    const double* Pp = prev_seal >= 0 ? prev->P : nullptr;
+    const double* Cp = prev_seal >= 0 ? prev->C : nullptr;
+    const int steps = prev_seal >= 0 ? 2 * d.K : d.K;
+#define DLP_PX_ARGS                                                                                          \
+    g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.nprice, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, \
+        d.ldcc, d.P, d.rhs, d.nzc, nrat, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, Cp, prev_seal, xp, \
+        seq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,     \
+        pub ? bp->Tn : nullptr, 2
+    if (steps > 64)   // lookahead at K = 64, beside the form-21 pass
+        pivot_x_lean_kernel<<<nrat + nprow, 256, std::max(ratio_ring_bytes(kRatioRingPairs),
+                                                          prow_ring_bytes(kProwRingSteps)), s>>>(DLP_PX_ARGS);
+    else if (steps <= 16)
+        pivot_x_kernel<16><<<nrat + nprow, 256, 0, s>>>(DLP_PX_ARGS);
+    else if (steps <= 32)
+        pivot_x_kernel<32><<<nrat + nprow, 256, 0, s>>>(DLP_PX_ARGS);
+    else
+        pivot_x_kernel<64><<<nrat + nprow, 256, 0, s>>>(DLP_PX_ARGS);
+#undef DLP_PX_ARGS
     return hipGetLastError();
 }
 

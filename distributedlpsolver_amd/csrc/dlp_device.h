@@ -151,9 +151,11 @@ __device__ inline void price_pair(PricePart& acc, double z0, double z1, int64_t 
 
 // a4: select + basis bookkeeping + pivot log (one lane).
 // track: deferred mode, record the step's local pivot row and count it in the block.
+// write_obj = false (one-launch pivot): the log entry's objective is left to the commit of the
+// same launch, which writes it from another workgroup (the two writes never share bytes).
 __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* basis,
                           int64_t row_first, int64_t rows, int pricing, dlp_pivot* log,
-                          int64_t log_cap, bool track = false) {
+                          int64_t log_cap, bool track = false, bool write_obj = true) {
     if (!best.valid) {
         st->status = DLP_UNBOUNDED;
         return;
@@ -177,14 +179,22 @@ __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* ba
     }
     const int64_t k = st->npivots;
     if (log && k < log_cap) {
-        dlp_pivot e;
-        e.q = q;
-        e.p = p;
-        e.leaving = leaving;
-        e.pad = 0;
-        e.ratio = best.ratio;
-        e.objective = __builtin_nan("");
-        log[k] = e;
+        if (write_obj) {
+            dlp_pivot e;
+            e.q = q;
+            e.p = p;
+            e.leaving = leaving;
+            e.pad = 0;
+            e.ratio = best.ratio;
+            e.objective = __builtin_nan("");
+            log[k] = e;
+        } else {
+            log[k].q = q;
+            log[k].p = p;
+            log[k].leaving = leaving;
+            log[k].pad = 0;
+            log[k].ratio = best.ratio;
+        }
     }
     st->npivots = k + 1;
 }
@@ -298,12 +308,89 @@ __device__ inline bool x_gather_cands(const XPeers* xp, uint32_t seq, Cand* lds,
     return *s_ok != 0;
 }
 
+// ---- the selection record (DevState::SelRec): ONE lane publishes, the pivot-row workgroups of
+// the same launch wait for it (bounded like every exchange wait)
+__device__ inline void sel_store32(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void sel_store64(void* p, uint64_t v) {
+    __hip_atomic_store((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void sel_publish(DevState* st, uint32_t seq, int32_t status, double zq) {
+    DevState::SelRec* r = &st->sel;
+    sel_store32(&r->status, status);
+    sel_store32(&r->p_local, st->p_local);
+    sel_store32(&r->blk, st->blk);
+    sel_store64(&r->piv, __builtin_bit_cast(uint64_t, st->piv));
+    sel_store64(&r->zq, __builtin_bit_cast(uint64_t, zq));
+    sel_store64(&r->npivots, (uint64_t)st->npivots);
+    x_drain();
+    __hip_atomic_store(&r->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+struct SelView {
+    int32_t status, p_local, blk;
+    double piv, zq;
+    int64_t npivots;
+};
+// Workgroup: wait for record seq (lane 0), then every lane gets its fields; false on a failed wait.
+__device__ inline bool sel_wait(const XPeers* xp, const DevState* st, uint32_t seq, SelView* out, SelView* lds,
+                                int* s_ok) {
+    if (threadIdx.x == 0) {
+        const DevState::SelRec* r = &st->sel;
+        bool ok = __hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq;
+        if (!ok) {
+            const uint64_t t0 = wall_clock64();
+            for (uint32_t it = 1;; ++it) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq) {
+                    ok = true;
+                    break;
+                }
+                if ((it & 255) == 0) {
+                    if (xp->abort_word &&
+                        __hip_atomic_load(xp->abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+                        break;
+                    if (xp->wait_ticks && wall_clock64() - t0 > xp->wait_ticks) break;
+                }
+            }
+        }
+        *s_ok = ok ? 1 : 0;
+        if (ok) {
+            lds->status = __hip_atomic_load(&r->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lds->p_local = __hip_atomic_load(&r->p_local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lds->blk = __hip_atomic_load(&r->blk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lds->piv = __builtin_bit_cast(
+                double, __hip_atomic_load((const uint64_t*)&r->piv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            lds->zq = __builtin_bit_cast(
+                double, __hip_atomic_load((const uint64_t*)&r->zq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            lds->npivots =
+                (int64_t)__hip_atomic_load((const uint64_t*)&r->npivots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    // uniform fields: to SGPRs (the LEAN kernels have 32 VGPRs)
+    auto u32 = [](int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane(v); };
+    auto u64 = [](uint64_t v) {
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+        return ((uint64_t)hi << 32) | lo;
+    };
+    out->status = u32(lds->status);
+    out->p_local = u32(lds->p_local);
+    out->blk = u32(lds->blk);
+    out->piv = __builtin_bit_cast(double, u64(__builtin_bit_cast(uint64_t, lds->piv)));
+    out->zq = __builtin_bit_cast(double, u64(__builtin_bit_cast(uint64_t, lds->zq)));
+    out->npivots = (int64_t)u64((uint64_t)lds->npivots);
+    const bool ok = u32(*s_ok) != 0;
+    __syncthreads();
+    return ok;
+}
+
 // Workgroup of 256 lanes, chunk = blockIdx.x (512 columns, 2 per lane from column j):
 // the owner's row values (v0, v1) into every rank's row region (one 16-B sc0 sc1 store per lane
 // and rank; j is even and the region 4 KiB aligned and padded to whole chunks), then, once every
 // wave has drained its stores, the chunk flags.
 __device__ inline void x_push_row_chunk(const XPeers* xp, uint32_t seq, int64_t j, int64_t ld,
-                                        uint64_t v0, uint64_t v1) {
+                                        uint64_t v0, uint64_t v1, int chunk) {
     if (j < ld) {
         u4x v;
         v.x = (uint32_t)v0;
@@ -318,7 +405,7 @@ __device__ inline void x_push_row_chunk(const XPeers* xp, uint32_t seq, int64_t 
     }
     x_drain();
     __syncthreads();
-    for (int r = threadIdx.x; r < xp->nranks; r += blockDim.x) x_store(x_rflag(xp, r, blockIdx.x), seq);
+    for (int r = threadIdx.x; r < xp->nranks; r += blockDim.x) x_store(x_rflag(xp, r, chunk), seq);
 }
 
 // Lane j of a chunk (j even): the two row words of this rank's region (one 16-B sc0 sc1 load),

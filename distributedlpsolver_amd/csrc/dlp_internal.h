@@ -45,7 +45,7 @@ static_assert(sizeof(Cand) == 32, "Cand must match dlp_candidate");
 
 // Device-resident solver state (one per rank).  Every decision of a pivot
 // lives here, so a window of pivots runs with no host round trip.
-struct alignas(16) DevState {
+struct alignas(128) DevState {
     int32_t status;    // DLP_RUNNING, DLP_OK (optimal), DLP_UNBOUNDED
     int32_t q;         // entering column
     int32_t p;         // pivot row, global index
@@ -73,6 +73,17 @@ struct alignas(16) DevState {
         int32_t pl[kMaxDefer];
         int32_t pad4;
     } seal[2];
+    // peer exchange, one launch per pivot (xfuse 2): the selection handed from the ratio
+    // workgroups to the pivot-row workgroups of the same launch, on a line of its own: the fields
+    // by sc1 (write-through) stores, drained, then seq (MI355X_MICROARCH.md, first row of the sc1
+    // hand-off table); read by sc1 loads after seq matched
+    struct alignas(128) SelRec {
+        uint32_t seq;
+        int32_t status, p_local, blk;
+        double piv, zq;
+        int64_t npivots;
+        uint32_t pad[22];
+    } sel;
 };
 // A pass's block: DevState::blk/pl (in-place passes) or a sealed copy (lookahead).
 typedef DevState::Seal BlockDesc;
@@ -231,6 +242,13 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
 // their own (one rank per device or process): a wait inside a launch is then never queued behind
 // the launch of another rank that it waits for (dlp_sessions_run of ranks sharing a device does not
 // fuse).
+// Peer exchange (xfuse sessions), ONE launch per pivot: the ratio test, the candidates of every
+// workgroup to every rank, the selection by workgroup 0, its record to the pivot-row workgroups of
+// the same launch, the owner's row push and every rank's commit.
+hipError_t launch_pivot_x(const Geometry& g, const Defer& d, int32_t* basis, PricePart* pp, DevState* st,
+                          double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
+                          hipStream_t s, const Defer* prev, int prev_seal, const XPeers* xp, uint32_t seq,
+                          const BandPub* bp);
 // nranks == 1: ratio test + selection + pivot row + objective row + pricing in ONE launch
 // (K <= 32; grid of fused_pivot_blocks(g), all of which must be resident at once).
 int fused_pivot_blocks(const Geometry& g);

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void xrow_send_kernel(const XPeers* xp, uint32
     uint64_t v0 = 0, v1 = 0;
     if (j < ld) v0 = (uint64_t)bits[j];
     if (j + 1 < ld) v1 = (uint64_t)bits[j + 1];
-    x_push_row_chunk(xp, seq, j, ld, v0, v1);
+    x_push_row_chunk(xp, seq, j, ld, v0, v1, (int)blockIdx.x);
 }
 
 __global__ __launch_bounds__(256) void xrow_recv_kernel(const XPeers* xp, uint32_t seq, int64_t ld,

@@ -426,6 +426,7 @@ void free_session(dlp_session* s) {
     for (auto e : s->ev) (void)hipEventDestroy(e);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     if (s->pstream) (void)hipStreamSynchronize(s->pstream);
+    clk.mark("free: graph, events, comm");
     void* dev[] = {s->Tb[0] ? s->Tb[0] : s->T, s->Tb[1], s->colq, s->prow_send, s->partials,
                    s->cand_send, s->cand_recv, s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc,
                    s->d.P, s->d.rhs, s->d.nzc, s->cl_gran, s->band_cnt};
@@ -434,6 +435,7 @@ void free_session(dlp_session* s) {
         void* sl[] = {s->dslot[1].C, s->dslot[1].Cc, s->dslot[1].P, s->dslot[1].nzc};
         for (void* p : sl) pool_release(s, s->device, p);
     }
+    clk.mark("free: pooled buffers");
     if (s->ev_seal) (void)hipEventDestroy(s->ev_seal);
     if (s->ev_pass) (void)hipEventDestroy(s->ev_pass);
     if (s->pstream) release_stream(s->device, s->prio_pass, s->pstream);
@@ -797,13 +799,15 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     s->Tb[0] = s->T;
     clk.mark("create: fill + state");
 
-    // lookahead: forced on, or auto on a single-rank tableau of >= 4 GiB, where
-    // the pass is several times the pivot chain it hides (C3 17 GB: 4,492 -> 4,935 pivots/s).
-    // Below that the chain, slowed by the concurrent pass and by replaying two blocks, costs more
-    // than the pass it hides (C2 268 MB: 39.0k -> 30.2k; profiles/r02h/).  An exchange session
-    // decides once its exchange is known (la_policy): on with the peer exchange, off with RCCL.
+    // lookahead: forced on, or auto at K = 64 on a streaming (> 1 GiB) tableau,
+    // where the 64-step pass is long enough to hide the selection chain: C3 17 GB 4,492 -> 4,935
+    // pivots/s (round 2), and round 4's rank geometries with the faster chain, 2.15 / 4.3 / 8.6 GB:
+    // +8 / +8 / +18 % (profiles/r04g/).  Smaller K (cache-resident tableaus) stays off: the chain,
+    // slowed by the concurrent pass and by replaying two blocks, costs more than the pass it hides
+    // (C2 268 MB, K = 16: 39.0k -> 30.2k; profiles/r02h/).  An exchange session decides once its
+    // exchange is known (la_policy): on with the peer exchange, off with RCCL.
     s->la_auto = opt->lookahead < 0;
-    if (opt->lookahead == 1 || (s->la_auto && !s->exchange && tbytes >= ((size_t)4 << 30)))
+    if (opt->lookahead == 1 || (s->la_auto && !s->exchange && s->d.K == 64 && streaming))
         CALL_TRY(la_enable(s, opt->lookahead == 1));
     s->opt.lookahead = s->la ? 1 : 0;
     pick_form(s);
@@ -954,19 +958,16 @@ int flush_pending_block(dlp_session* s) {
 }
 
 // An exchange session's auto lookahead, once its exchange is known (creation, connect,
-// dlp_session_set_exchange; between runs): with the peer exchange, the single-rank rule (K = 64,
-// a rank tableau of >= 4 GiB: C3 at P <= 4), where every per-pivot kernel fits beside the form-21
-// pass (the LEAN ratio and pivot-row launches, with the selection and the commit inside: <= 32
-// VGPRs, tests/test_isa.py).  A smaller rank's pass is shorter than its selection chain and
-// lookahead only slows the chain (one rank of C3 at P = 8, 2.15 GB: 20,857 vs 21,352 pivots/s,
-// profiles/r04e/).  Off with RCCL, whose collective kernels need more registers than the pass
-// leaves on a CU and would each wait for pass workgroups to drain.  A caller's
-// explicit lookahead setting is kept.
+// dlp_session_set_exchange; between runs): with the peer exchange, the single-rank rule (K = 64 on
+// a streaming tableau), where every per-pivot kernel fits beside the form-21 pass (the LEAN ratio
+// and pivot-row launches, with the selection and the commit inside: <= 32 VGPRs,
+// tests/test_isa.py).  Measured on the C3 rank geometries at P = 8 / 4 / 2 (c3r8 / c3r4 / c3r2):
+// 23,012 vs 21,358, 17,098 vs 15,881, 11,980 vs 10,183 pivots/s (profiles/r04g/).  Off with RCCL,
+// whose collective kernels need more registers than the pass leaves on a CU and would each wait
+// for pass workgroups to drain.  A caller's explicit lookahead setting is kept.
 int la_policy(dlp_session* s) {
     if (!s->la_auto || !s->exchange) return DLP_OK;
-    const size_t tbytes = (size_t)(s->rows + 1) * s->ld * sizeof(double);
-    const bool want = s->xmode == dlp_session::X_PEER && s->d.K == 64 && tbytes >= ((size_t)4 << 30) &&
-                      !s->general;
+    const bool want = s->xmode == dlp_session::X_PEER && s->d.K == 64 && s->streaming && !s->general;
     if (want && !s->la) CALL_TRY(la_enable(s, false));
     if (!want && s->la) CALL_TRY(la_disable(s));
     pick_form(s);
@@ -1015,6 +1016,17 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
                                             s->log_cap, s->stream));
             return DLP_OK;
         }
+        // peer exchange: the whole pivot in ONE launch (ratio test, selection, the selection record to
+        // the pivot-row workgroups, row push, commit); DLP_PEER_ONELAUNCH=0: two launches (A/B only)
+        static const bool onelaunch = !(std::getenv("DLP_PEER_ONELAUNCH") && std::atoi(std::getenv("DLP_PEER_ONELAUNCH")) == 0);
+        if (xf && onelaunch) {
+            s->xseq_c += 1;
+            s->xseq_r += 1;   // (equal: every pivot, drive-out and carry step advances both)
+            HIP_TRY(dlp::launch_pivot_x(gsel, *dcur, s->basis, s->pp, s->st, o.tol_dj, o.tol_piv, o.pricing, s->log,
+                                        s->log_cap, s->stream, dprev, pseal, xp, s->xseq_c, &bp));
+            if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
+            return DLP_OK;
+        }
         if (xp) s->xseq_c += 1;
         HIP_TRY(dlp::launch_ratio_defer(gsel, *dcur, s->basis, s->pp, s->st, s->partials,
                                         s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
@@ -1028,6 +1040,11 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     }
     if (phase == 1) {
         if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) return DLP_OK;
+        static const bool onelaunch = !(std::getenv("DLP_PEER_ONELAUNCH") && std::atoi(std::getenv("DLP_PEER_ONELAUNCH")) == 0);
+        if (xf && onelaunch) {   // (the whole pivot ran in phase 0's launch)
+            if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
+            return DLP_OK;
+        }
         if (s->exchange && !xf)
             HIP_TRY(dlp::launch_select(s->g, s->cand_recv, s->nranks, s->basis, s->st, o.pricing,
                                        s->log, s->log_cap, s->stream, false, true, xp, s->xseq_c));

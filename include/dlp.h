@@ -156,10 +156,10 @@ typedef struct dlp_options {
     int32_t lookahead;       /* deferred sessions: select block b+1 while the pass of block b
                                 runs, on a second tableau buffer (results unchanged, bit for
                                 bit; 2x the tableau memory): 1 = on where supported, 0 = off,
-                                -1 = auto (default: a single-rank tableau of >= 4 GiB that
-                                fits twice; a row-block rank at K = 64 on a streaming (> 1 GiB)
-                                tableau once it runs the peer exchange, never with RCCL; at
-                                K = 64 the selections replay up to 127 steps) */
+                                -1 = auto (default: K = 64 on a streaming (> 1 GiB) tableau
+                                that fits twice, single-rank or a row-block rank once it runs
+                                the peer exchange, never with RCCL; at K = 64 the selections
+                                replay up to 127 steps) */
     int32_t exchange;        /* row-block exchange of dlp_solve(n_gpus = N) and of rank sessions
                                 created with an RCCL id: DLP_XCHG_DEFAULT (0, the default) = the
                                 peer exchange where every rank pair connects (peer access + IPC

@@ -112,7 +112,7 @@ def test_lookahead_k64_tableau(form, rb, nt, ci):
 
 
 def test_lookahead_medium_tableau_and_auto_policy():
-    """2049 x 4097 doubles (75 MB, K = 16): auto leaves lookahead off below 4 GiB; forced
+    """2049 x 4097 doubles (75 MB, K = 16): auto leaves lookahead off (K = 64 streaming only); forced
     on, the same pivots and tableau rows as off.  (Auto-on at full size: test_gpu_large's
     C3 tests.)"""
     prob = dlp.Problem.random(2048, 2048, 2)

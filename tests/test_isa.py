@@ -143,6 +143,7 @@ def test_lookahead_kernels_fit_beside_the_form21_pass():
     assert one("pass_d_kernel") <= 160, c
     assert one("ratio_lean_kernel") <= 32   # every instance (ring depths 8 / 16, LCH 4 / 8)
     assert one("prow_lean_kernel") <= 32
+    assert one("pivot_x_lean_kernel") <= 32   # the one-launch peer pivot beside the pass
 
 
 def _functions(text):

@@ -22,13 +22,18 @@ cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--n
 out = subprocess.run(cmd, env=env, check=True, capture_output=True, text=True).stdout
 line = json.loads(out.strip().splitlines()[-1])
 st = np.fromfile(path, dtype=np.uint64).reshape(64, 16).astype(np.float64) / 100.0   # µs
-ok = (st[:, [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11]] > 0).all(axis=1)
+# (stamp 5, the ticket, is not taken when the ratio launch selects for the peer exchange)
+fused = not (st[:, 5] > 0).any()
+ok = (st[:, [0, 1, 2, 3, 4, 6, 8, 9, 10, 11] + ([] if fused else [5])] > 0).all(axis=1)
 st = st[ok]
 names = ["ratio: pricing reduce (start -> q)", "ratio: T0[i][q] + P[l][q] in", "ratio: replay (lane 0)",
          "ratio: block reduce", "ratio: partials + ticket", "ratio: last workgroup select (ticket -> end)",
          "gap ratio end -> prow start", "prow: step table + T0[p] in", "prow: replay + divide",
          "prow: commit (P, objective row, pricing) / exchange push"]
 pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 8), (8, 9), (9, 10), (10, 11)]
+if fused:   # every workgroup pushes its candidate; workgroup 0 gathers them all and selects
+    names = names[:4] + ["ratio: push + gather + select (wg 0: reduce -> end)"] + names[6:]
+    pairs = pairs[:4] + [(4, 6)] + pairs[6:]
 res = {n: float(np.median(st[:, b] - st[:, a])) for n, (a, b) in zip(names, pairs)}
 if (st[:, 13:15] > 0).all() and not (st[:, 12] > 0).any():   # peer, fused: the commit in the prow launch
     res["prow: commit wait (push end -> chunk flag)"] = float(np.median(st[:, 13] - st[:, 11]))
