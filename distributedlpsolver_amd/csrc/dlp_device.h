@@ -310,6 +310,9 @@ __device__ inline bool x_gather_cands(const XPeers* xp, uint32_t seq, Cand* lds,
 
 // ---- the selection record (DevState::SelRec): ONE lane publishes, the pivot-row workgroups of
 // the same launch wait for it (bounded like every exchange wait)
+#ifndef XSEL_SLEEP
+#define XSEL_SLEEP 8
+#endif
 __device__ inline void sel_store32(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -341,7 +344,9 @@ __device__ inline bool sel_wait(const XPeers* xp, const DevState* st, uint32_t s
         if (!ok) {
             const uint64_t t0 = wall_clock64();
             for (uint32_t it = 1;; ++it) {
-                __builtin_amdgcn_s_sleep(1);
+                // (one poller per pivot-row workgroup, ~130 of them on one line: a long sleep keeps
+                // the polls from crowding the memory queues the ratio workgroups wait in)
+                __builtin_amdgcn_s_sleep(XSEL_SLEEP);
                 if (__hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq) {
                     ok = true;
                     break;

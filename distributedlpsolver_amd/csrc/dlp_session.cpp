@@ -974,6 +974,12 @@ int la_policy(dlp_session* s) {
     return DLP_OK;
 }
 
+// DLP_PEER_ONELAUNCH=1: a peer pivot as one launch (read per pivot, so tests can switch it)
+bool peer_onelaunch() {
+    const char* e = std::getenv("DLP_PEER_ONELAUNCH");
+    return e && std::atoi(e) == 1;
+}
+
 // The exchange kernels' peer table (X_PEER) or NULL.
 inline const dlp::XPeers* xp_of(const dlp_session* s) {
     return s->xmode == dlp_session::X_PEER ? s->xpeers : nullptr;
@@ -1016,10 +1022,11 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
                                             s->log_cap, s->stream));
             return DLP_OK;
         }
-        // peer exchange: the whole pivot in ONE launch (ratio test, selection, the selection record to
-        // the pivot-row workgroups, row push, commit); DLP_PEER_ONELAUNCH=0: two launches (A/B only)
-        static const bool onelaunch = !(std::getenv("DLP_PEER_ONELAUNCH") && std::atoi(std::getenv("DLP_PEER_ONELAUNCH")) == 0);
-        if (xf && onelaunch) {
+        // peer exchange, DLP_PEER_ONELAUNCH=1 (opt-in): the whole pivot in ONE launch (ratio test,
+        // selection, the selection record to the pivot-row workgroups, row push, commit).  Bit-exact,
+        // but 1-3 % slower than two launches at the C3 rank geometries: the record's hand-off and its
+        // ~130 pollers cost what the launch boundary did (profiles/r04i/, r04j/)
+        if (xf && peer_onelaunch()) {
             s->xseq_c += 1;
             s->xseq_r += 1;   // (equal: every pivot, drive-out and carry step advances both)
             HIP_TRY(dlp::launch_pivot_x(gsel, *dcur, s->basis, s->pp, s->st, o.tol_dj, o.tol_piv, o.pricing, s->log,
@@ -1040,8 +1047,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     }
     if (phase == 1) {
         if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) return DLP_OK;
-        static const bool onelaunch = !(std::getenv("DLP_PEER_ONELAUNCH") && std::atoi(std::getenv("DLP_PEER_ONELAUNCH")) == 0);
-        if (xf && onelaunch) {   // (the whole pivot ran in phase 0's launch)
+        if (xf && peer_onelaunch()) {   // (the whole pivot ran in phase 0's launch)
             if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
             return DLP_OK;
         }

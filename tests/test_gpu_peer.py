@@ -218,6 +218,26 @@ def test_auto_exchange_rank_session(inject, defer):
         _check(s.result(), ref)
 
 
+@pytest.mark.parametrize("lookahead", [0, 1])
+def test_peer_one_launch_pivot(lookahead):
+    """DLP_PEER_ONELAUNCH=1: the peer pivot as ONE launch (the ratio workgroups publish the
+    selection record to the pivot-row workgroups of the same launch); bit-exact on a 1-rank
+    exchange session, with K = 64 blocks through lookahead (the LEAN instance) and without."""
+    m, n, seed = 400, 600, 11
+    A, b, c = O.gen_dense(m, n, seed)
+    ref = O.solve_dense(A, b, c)
+    os.environ["DLP_PEER_ONELAUNCH"] = "1"
+    try:
+        with dlp.Session(dlp.Problem.random(m, n, seed), rank=0, nranks=1, rccl_id=dlp.comm_unique_id(),
+                         defer=64, lookahead=lookahead, check_interval=50) as s:
+            assert s.get_exchange() == L.XCHG_PEER and s.lookahead() == bool(lookahead)
+            st, _ = s.run(10 ** 6)
+            assert st == L.OK
+            _check(s.result(), ref)
+    finally:
+        os.environ.pop("DLP_PEER_ONELAUNCH", None)
+
+
 def test_strict_peer_exchange_fails_when_a_rank_cannot():
     """exchange = DLP_XCHG_PEER is not downgraded: the session creation fails."""
     A, b, c = O.gen_dense(64, 64, 3)
