@@ -269,6 +269,7 @@ hipError_t pool_alloc(dlp_session* s, int device, void** p, size_t bytes) {
 }
 
 // Free p (a session buffer): back to the pool when it came from it and the session is healthy.
+int g_pool_freed = 0;   // DLP_TRACE_CREATE: buffers the last teardown freed instead of pooling
 void pool_release(dlp_session* s, int device, void* p) {
     if (!p) return;
     size_t cls = 0;
@@ -286,6 +287,7 @@ void pool_release(dlp_session* s, int device, void* p) {
             return;
         }
     }
+    ++g_pool_freed;
     if (device < 0)
         (void)hipHostFree(p);
     else
@@ -422,11 +424,14 @@ void free_session(dlp_session* s) {
             }
     }
     if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+    clk.mark(s->gexec ? "free: graph exec" : "free: (no graph)");
     if (s->graph) (void)hipGraphDestroy(s->graph);
+    clk.mark("free: graph");
     for (auto e : s->ev) (void)hipEventDestroy(e);
+    clk.mark("free: events");
     if (s->comm) (void)ncclCommDestroy(s->comm);
     if (s->pstream) (void)hipStreamSynchronize(s->pstream);
-    clk.mark("free: graph, events, comm");
+    clk.mark("free: comm");
     void* dev[] = {s->Tb[0] ? s->Tb[0] : s->T, s->Tb[1], s->colq, s->prow_send, s->partials,
                    s->cand_send, s->cand_recv, s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc,
                    s->d.P, s->d.rhs, s->d.nzc, s->cl_gran, s->band_cnt};
@@ -435,7 +440,8 @@ void free_session(dlp_session* s) {
         void* sl[] = {s->dslot[1].C, s->dslot[1].Cc, s->dslot[1].P, s->dslot[1].nzc};
         for (void* p : sl) pool_release(s, s->device, p);
     }
-    clk.mark("free: pooled buffers");
+    clk.mark(g_pool_freed ? "free: pooled buffers (some freed)" : "free: pooled buffers");
+    g_pool_freed = 0;
     if (s->ev_seal) (void)hipEventDestroy(s->ev_seal);
     if (s->ev_pass) (void)hipEventDestroy(s->ev_pass);
     if (s->pstream) release_stream(s->device, s->prio_pass, s->pstream);
@@ -1425,6 +1431,7 @@ int run_window_graph(dlp_session* s, int64_t chunk) {
     if (!s->gexec || s->graph_chunk != chunk) {
         if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
         if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
+        StageClock clk;
         HIP_TRY(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
         int rc = DLP_OK;
         for (int64_t k = 0; k < chunk && rc == DLP_OK; ++k) rc = enqueue_pivot(s, 0, k == chunk - 1);
@@ -1432,8 +1439,10 @@ int run_window_graph(dlp_session* s, int64_t chunk) {
         hipError_t e = hipStreamEndCapture(s->stream, &gr);
         if (rc != DLP_OK) return rc;
         HIP_TRY(e);
+        clk.mark("run: graph capture");
         s->graph = gr;
         HIP_TRY(hipGraphInstantiate(&s->gexec, s->graph, nullptr, nullptr, 0));
+        clk.mark("run: graph instantiate");
         s->graph_chunk = chunk;
     }
     HIP_TRY(hipGraphLaunch(s->gexec, s->stream));

@@ -25,6 +25,7 @@ st = np.fromfile(path, dtype=np.uint64).reshape(64, 16).astype(np.float64) / 100
 # (stamp 5, the ticket, is not taken when the ratio launch selects for the peer exchange)
 fused = not (st[:, 5] > 0).any()
 ok = (st[:, [0, 1, 2, 3, 4, 6, 8, 9, 10, 11] + ([] if fused else [5])] > 0).all(axis=1)
+full = st.copy()
 st = st[ok]
 names = ["ratio: pricing reduce (start -> q)", "ratio: T0[i][q] + P[l][q] in", "ratio: replay (lane 0)",
          "ratio: block reduce", "ratio: partials + ticket", "ratio: last workgroup select (ticket -> end)",
@@ -48,5 +49,11 @@ elif (st[:, 12:15] > 0).all():   # exchange sessions: the pivot row is pushed, t
     res["pivot period (ratio start -> next ratio start)"] = float(np.median(np.diff(np.sort(st[:, 0]))))
 res["ratio total (start -> end)"] = float(np.median(st[:, 6] - st[:, 0]))
 res["prow total"] = float(np.median(st[:, 11] - st[:, 8]))
+# by position k in the block (slot k = pivot count mod 64): when each pivot starts after the block's
+# first, and its ratio / pivot-row launch durations (-1: stamp missing)
+t0 = full[0, 0]
+by_slot = {"start_after_first": [round(float(full[k, 0] - t0), 1) if ok[k] else -1 for k in range(64)],
+           "ratio": [round(float(full[k, 6] - full[k, 0]), 1) if ok[k] else -1 for k in range(64)],
+           "prow": [round(float(full[k, 11] - full[k, 8]), 1) if ok[k] else -1 for k in range(64)]}
 print(json.dumps({"pivots_sampled": int(ok.sum()), "bench_value": line["value"],
-                  "pass_ms": line["roofline"]["launch_ms"], "median_us": res}, indent=1))
+                  "pass_ms": line["roofline"]["launch_ms"], "median_us": res, "by_slot_us": by_slot}, indent=1))
