@@ -255,15 +255,19 @@ def alt_exchange_window(sess, dist, barrier_sync, args, L, torch):
         return out
     barrier_sync()
     t0 = time.perf_counter()
+    done = 0
     try:
         st, done = sess.run(args.alt_pivots)
     except L.DLPError as e:
         out["error"] = str(e)
-        return out
-    barrier_sync()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    barrier_sync()   # every rank, failed or not, so the collectives below stay matched
+    el = torch.tensor([time.perf_counter() - t0, 1.0 if "error" in out else 0.0], dtype=torch.float64,
+                      device="cuda")
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    out.update({"done": done, "seconds": float(el.item())})
+    if el[1].item() > 0:
+        out.setdefault("error", "failed on another rank")
+        return out
+    out.update({"done": done, "seconds": float(el[0].item())})
     if done == args.alt_pivots:
         out["pivots_per_s"] = done / out["seconds"]
     return out
@@ -304,41 +308,86 @@ def main():
         torch.cuda.synchronize()
 
     prob = dlp.Problem.random(m, n, seed)
-    # K is fixed by the session (auto: 32 on a streaming tableau); the pivot budget
-    # leaves room for the widest window and the extra pivot window
-    sess = dlp.Session(prob, rank=rank, nranks=world, rccl_id=rccl_id, device=local,
-                       check_interval=64 * max(args.steps, args.warmup, 1), timing=args.timing,
-                       nontemporal=args.nontemporal, update_variant=args.variant,
-                       ld_align=args.ld_align, rows_per_block=args.rows_per_block,
-                       max_pivots=64 * (args.warmup + args.steps) + args.steps + args.alt_pivots + 2,
-                       log_pivots=1, defer=args.defer, lookahead=args.lookahead,
-                       exchange=xopt if xsess else 0)
-    if args.occupancy >= 0 or args.form >= 0:
-        if sess.update_stats()[2] > 1:
-            sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 0, args.form)
-    K = sess.update_stats()[2]
-    lookahead_on = sess.lookahead()
+
+    def open_session(x, rid):
+        # K is fixed by the session (auto: 64 on a streaming tableau); the pivot budget
+        # leaves room for the widest window and the extra pivot window
+        return dlp.Session(prob, rank=rank, nranks=world, rccl_id=rid, device=local,
+                           check_interval=64 * max(args.steps, args.warmup, 1), timing=args.timing,
+                           nontemporal=args.nontemporal, update_variant=args.variant,
+                           ld_align=args.ld_align, rows_per_block=args.rows_per_block,
+                           max_pivots=64 * (args.warmup + args.steps) + args.steps + args.alt_pivots + 2,
+                           log_pivots=1, defer=args.defer, lookahead=args.lookahead,
+                           exchange=x if xsess else 0)
+
+    def any_rank(flag):
+        if dist is None:
+            return flag
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item()) != 0
+
+    def guarded_run(sess, pivots, timed):
+        """sess.run on every rank.  A failure (an exchange error or timeout) is held until every
+        rank has passed the same barriers, then agreed, so all ranks take the same next step."""
+        err, st, done, el = None, None, 0, 0.0
+        if timed:
+            barrier_sync()
+            t0 = time.perf_counter()
+        try:
+            st, done = sess.run(pivots)
+        except dlp.DLPError as e:
+            err = e
+        if timed:
+            barrier_sync()
+            el = time.perf_counter() - t0
+        return st, done, el, err, any_rank(err is not None)
+
+    def measure(sess):
+        st, done, _, err, bad = guarded_run(sess, warm, False)
+        if bad:
+            return st, done, 0.0, err, True
+        if done != warm:
+            raise SystemExit(f"warm-up ended early: status {st} after {done} pivots")
+        sess.reset_timings()
+        return guarded_run(sess, timed, True)
+
+    def configure(sess):
+        if args.occupancy >= 0 or args.form >= 0:
+            if sess.update_stats()[2] > 1:
+                sess.set_defer_tuning(args.occupancy if args.occupancy >= 0 else 0, args.form)
+        if xsess:
+            # a dead rank ends the run in bounded time (its peers' waits abort), never a hang
+            sess.set_exchange_timeout(60.0)
+
     XNAMES = {L.XCHG_RCCL: "rccl", L.XCHG_PEER: "peer"}
-    xmode = XNAMES.get(sess.get_exchange(), "none") if xsess else None
-    xreason = sess.exchange_reason() if xsess and hasattr(sess, "exchange_reason") else None
-    if xsess:
-        # a dead rank ends the run in bounded time (its peers' waits abort), never a hang
-        sess.set_exchange_timeout(60.0)
+    sess = open_session(xopt, rccl_id)
+    configure(sess)
+    K = sess.update_stats()[2]
     per_step = K if args.step_unit == "block" else 1
     warm, timed = args.warmup * per_step, args.steps * per_step
+    xmode = XNAMES.get(sess.get_exchange(), "none") if xsess else None
+    xreason = sess.exchange_reason() if xsess and hasattr(sess, "exchange_reason") else None
 
-    st, done = sess.run(warm)
-    if done != warm:
-        raise SystemExit(f"warm-up ended early: status {st} after {done} pivots")
-    sess.reset_timings()
-
-    barrier_sync()
-    t0 = time.perf_counter()
-    st, done = sess.run(timed)
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
+    st, done, elapsed, err, bad = measure(sess)
+    run_fallback = None
+    if bad and world > 1 and xmode == "peer" and args.exchange == "auto":
+        # the owner-rooted exchange failed on some rank during the run (it has never run across
+        # xGMI on this pool's one-GPU boxes): every rank reruns the measurement over RCCL
+        run_fallback = f"peer exchange failed during the run: {err if err else 'on another rank'}"
+        sess.close()
+        obj = [dlp.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        sess = open_session(L.XCHG_RCCL, obj[0])
+        configure(sess)
+        xmode = XNAMES.get(sess.get_exchange(), "none")
+        xreason = run_fallback
+        st, done, elapsed, err, bad = measure(sess)
+    if bad:
+        raise SystemExit(f"run failed: {err if err else 'on another rank'}")
     if done != timed:
         raise SystemExit(f"timed window ended early: status {st} after {done} pivots")
+    lookahead_on = sess.lookahead()
 
     tm, nsamp = sess.timings()
     launches, upd_total_ms, _ = sess.update_stats()
@@ -383,7 +432,7 @@ def main():
     # (RCCL collectives <-> owner-rooted peer stores), timed the same way, so that one
     # scaling run measures both; a failure to switch or to run is reported, not fatal
     alt = None
-    if dist is not None and args.alt_pivots > 0 and K > 1:
+    if dist is not None and args.alt_pivots > 0 and K > 1 and run_fallback is None:
         alt = alt_exchange_window(sess, dist, barrier_sync, args, L, torch)
         if alt.get("pivots_per_s") and rank == 0:
             alt["pivot_log_vs_oracle"] = log_parity(args.workload, sess.result().pivot_log)

@@ -162,6 +162,7 @@ SIGNATURES = [
     ("dlp_session_set_tuning", C.c_int, [_P, C.c_int, C.c_int, C.c_int]),
     ("dlp_session_get_tuning", C.c_int,
      [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("dlp_session_small_lp", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("dlp_session_info", C.c_int,
      [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64)]),
     ("dlp_session_tableau", C.c_int, [_P, _DP]),

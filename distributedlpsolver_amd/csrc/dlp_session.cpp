@@ -229,8 +229,8 @@ void release_stream(int device, int prio, hipStream_t s) {
 // kBufPoolTotal bytes and kBufPoolCount entries cached); a session takes an exact class match.
 // Tableaus and other large buffers are never pooled.  Contents are not cleared: every buffer is
 // initialised by the session before it is read, as a fresh hipMalloc's would have to be.
-constexpr size_t kBufPoolMax = (size_t)16 << 20;
-constexpr size_t kBufPoolTotal = (size_t)256 << 20;
+constexpr size_t kBufPoolMax = (size_t)32 << 20;     // (the default pivot log: 1 M x 32 B)
+constexpr size_t kBufPoolTotal = (size_t)512 << 20;
 constexpr size_t kBufPoolCount = 256;
 struct PooledBuf {
     int device;   // -1: pinned host memory
@@ -270,6 +270,7 @@ hipError_t pool_alloc(dlp_session* s, int device, void** p, size_t bytes) {
 
 // Free p (a session buffer): back to the pool when it came from it and the session is healthy.
 int g_pool_freed = 0;   // DLP_TRACE_CREATE: buffers the last teardown freed instead of pooling
+std::string g_pool_freed_why;
 void pool_release(dlp_session* s, int device, void* p) {
     if (!p) return;
     size_t cls = 0;
@@ -288,6 +289,8 @@ void pool_release(dlp_session* s, int device, void* p) {
         }
     }
     ++g_pool_freed;
+    if (std::getenv("DLP_TRACE_CREATE"))
+        g_pool_freed_why += " " + std::to_string(cls) + (cls == 0 ? "(unpooled)" : s->pool_ok ? "(full)" : "(failed)");
     if (device < 0)
         (void)hipHostFree(p);
     else
@@ -440,8 +443,9 @@ void free_session(dlp_session* s) {
         void* sl[] = {s->dslot[1].C, s->dslot[1].Cc, s->dslot[1].P, s->dslot[1].nzc};
         for (void* p : sl) pool_release(s, s->device, p);
     }
-    clk.mark(g_pool_freed ? "free: pooled buffers (some freed)" : "free: pooled buffers");
+    clk.mark(g_pool_freed ? ("free: pooled buffers, freed:" + g_pool_freed_why).c_str() : "free: pooled buffers");
     g_pool_freed = 0;
+    g_pool_freed_why.clear();
     if (s->ev_seal) (void)hipEventDestroy(s->ev_seal);
     if (s->ev_pass) (void)hipEventDestroy(s->ev_pass);
     if (s->pstream) release_stream(s->device, s->prio_pass, s->pstream);
@@ -561,6 +565,8 @@ int la_enable(dlp_session* s, bool forced) {
 int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int nranks,
                  const void* uid, dlp_session* s, ncclComm_t comm_in = nullptr) {
     const bool rccl = uid != nullptr || comm_in != nullptr;
+    // the caller's choice, before the "auto" values below are resolved into s->opt
+    const bool variant_auto = opt->update_variant < 0;
     s->opt = *opt;
     s->device = opt->device;
     s->rank = rank;
@@ -673,7 +679,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
             cus = 0;
         if (!s->general && nranks == 1 && !rccl && s->m < (1 << 30) && s->N < (1 << 30) &&
             (opt->small_lp == 1 ||
-             (opt->small_lp == 0 && K == 0 && tiny && opt->update_variant < 0))) {
+             (opt->small_lp == 0 && K == 0 && tiny && variant_auto))) {
             s->cl_wg = dlp::cluster_plan(s->m, s->N, cus, &s->cl_cw);
             // tuning only: DLP_CLUSTER_WG=G forces the workgroup count (if the slices fit)
             if (const char* e = std::getenv("DLP_CLUSTER_WG")) {
@@ -2529,6 +2535,12 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
     if (update_variant) *update_variant = s->opt.update_variant;
     if (rows_per_block) *rows_per_block = s->d.K > 1 ? s->defer_rb : s->g.rows_per_block;
     if (nontemporal) *nontemporal = s->opt.nontemporal;
+    return DLP_OK;
+}
+
+int dlp_session_small_lp(dlp_session* s, int* small_lp) {
+    if (!s || !small_lp) return DLP_ERR_ARG;
+    *small_lp = s->cluster ? 1 : 0;
     return DLP_OK;
 }
 

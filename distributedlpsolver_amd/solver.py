@@ -285,6 +285,12 @@ class Session:
                 "dlp_session_get_tuning")
         return v.value, rb.value, nt.value
 
+    def small_lp(self) -> bool:
+        """True when this session solves in the one-launch LDS path (options.small_lp)."""
+        v = C.c_int()
+        L.check(L.lib().dlp_session_small_lp(self._h, C.byref(v)), "dlp_session_small_lp")
+        return bool(v.value)
+
     def update_stats(self) -> tuple[int, float, int]:
         """(timed update launches, their total ms, pivots per tableau pass)."""
         n, ms, k = C.c_int64(), C.c_double(), C.c_int()

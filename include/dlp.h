@@ -302,6 +302,8 @@ int dlp_session_reset_timings(dlp_session* s);
  * rows per workgroup band (0 = auto, <= 256), non-temporal loads/stores. */
 int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_block, int nontemporal);
 int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_block, int* nontemporal);
+/* 1 when the session solves in the one-launch LDS path (options.small_lp), else 0. */
+int dlp_session_small_lp(dlp_session* s, int* small_lp);
 /* Deferred sessions: workgroups per CU allowed for the tableau pass (LDS
  * reservation; 0 = no cap, the default) and its form (-1 = keep):
  *   LDS-staged coefficients: 0 = 2 doubles per lane (K <= 32), 1 / 2 = 1 double

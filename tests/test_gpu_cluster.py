@@ -64,6 +64,15 @@ def test_cluster_auto_policy_and_off_switch():
     ref = O.solve_dense(A, b, c)
     for small in (0, -1):   # auto picks the cluster launch for this size; -1 = multi-kernel
         _check(dlp.solve(dlp.Problem.dense(A, b, c), small_lp=small), ref)
+        # the path really taken (round 4 found auto resolved to multi-kernel since round 3:
+        # the check read the resolved update variant instead of the caller's "auto")
+        with dlp.Session(dlp.Problem.dense(A, b, c), small_lp=small) as s:
+            assert s.small_lp() == (small == 0)
+    # a caller-chosen rank-1 variant keeps the multi-kernel path; a forced small_lp takes it anyway
+    with dlp.Session(dlp.Problem.dense(A, b, c), update_variant=0) as s:
+        assert not s.small_lp()
+    with dlp.Session(dlp.Problem.dense(A, b, c), small_lp=1, update_variant=0) as s:
+        assert s.small_lp()
 
 
 def test_cluster_step_api_continues():

@@ -78,13 +78,13 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0, tableau_digest=None, form=None):
+def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0, tableau_digest=None, form=None, lookahead=-1):
     """k pivots in windows of ci (whole K-blocks, then a tail) through the auto
     geometry of the bench (deferred K, pass form, band rows, ld alignment);
     the whole pivot log, every pivot row, random rows and the objective row
     against the oracle on the same generated LP, byte for byte."""
     rng = np.random.default_rng(seed)
-    with dlp.Session(dlp.Problem.random(m, n, seed), check_interval=ci, defer=defer) as s:
+    with dlp.Session(dlp.Problem.random(m, n, seed), check_interval=ci, defer=defer, lookahead=lookahead) as s:
         if form is not None:
             s.set_defer_tuning(0, form)
         occ, f, K = s.get_defer_tuning()
@@ -94,7 +94,8 @@ def _full_blocks_vs_oracle(m, n, seed, k, ci, want_K, defer=0, tableau_digest=No
             assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
         if K == 32:
             assert f == 4 and s.get_tuning()[1] == 256   # round 2's first default
-            assert s.lookahead()   # auto from 4 GiB: block b+1 selected during pass b
+            # lookahead is auto only at K = 64 since round 4 (profiles/r04l/): forced here
+            assert s.lookahead() == (lookahead == 1)
         done = 0
         while done < k:
             st, d = s.run(min(ci, k - done))
@@ -134,8 +135,8 @@ def test_c3_full_blocks_bit_exact(form):
 
 
 def test_c3_k32_lookahead_full_blocks_bit_exact():
-    """C3 with K = 32 (form 4, lookahead auto-on): 2 full blocks and an 8-pivot tail."""
-    _full_blocks_vs_oracle(32768, 32768, 3, 72, 64, 32, defer=32)
+    """C3 with K = 32 (form 4, lookahead forced on): 2 full blocks and an 8-pivot tail."""
+    _full_blocks_vs_oracle(32768, 32768, 3, 72, 64, 32, defer=32, lookahead=1)
 
 
 def test_c2_full_blocks_bit_exact():
@@ -153,7 +154,7 @@ def test_c3_bench_window_digest(K):
     g = load_golden("digests.json")["c3_k64" if K == 64 else "c3"]
     m, n = g["m"], g["n"]
     with dlp.Session(dlp.Problem.random(m, n, g["seed"]), check_interval=64 * 20, timing=1,
-                     max_pivots=64 * 25 + 22, defer=0 if K == 64 else 32) as s:
+                     max_pivots=64 * 25 + 22, defer=0 if K == 64 else 32, lookahead=1) as s:
         assert s.get_defer_tuning()[2] == K and s.lookahead()
         for k in (5 * K, 20 * K, 20):
             st, d = s.run(k)
