@@ -235,6 +235,61 @@ def log_parity(workload, log):
             "bit_identical": all(got.values()) if got else None}
 
 
+def agree_any(flag, dist, torch, device):
+    """True on every rank when `flag` is true on any rank (MAX all-reduce); the flag itself at N = 1."""
+    if dist is None:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item()) != 0
+
+
+def guarded_run(sess, pivots, timed, barrier_sync, any_rank, errors):
+    """sess.run on every rank.  A failure (an exchange error or timeout: `errors`) is held until
+    every rank has passed the same barriers, then agreed, so all ranks take the same next step
+    and every collective stays matched."""
+    err, st, done, el = None, None, 0, 0.0
+    if timed:
+        barrier_sync()
+        t0 = time.perf_counter()
+    try:
+        st, done = sess.run(pivots)
+    except errors as e:
+        err = e
+    if timed:
+        barrier_sync()
+        el = time.perf_counter() - t0
+    return st, done, el, err, any_rank(err is not None)
+
+
+def measure(sess, warm, timed, barrier_sync, any_rank, errors):
+    """Warm-up window, then the timed window: (status, pivots done, seconds, error, failed on any rank)."""
+    st, done, _, err, bad = guarded_run(sess, warm, False, barrier_sync, any_rank, errors)
+    if bad:
+        return st, done, 0.0, err, True
+    if done != warm:
+        raise SystemExit(f"warm-up ended early: status {st} after {done} pivots")
+    sess.reset_timings()
+    return guarded_run(sess, timed, True, barrier_sync, any_rank, errors)
+
+
+def measure_with_fallback(sess, warm, timed, barrier_sync, any_rank, errors, reopen=None):
+    """measure(); when it failed on any rank and `reopen` is given (N > 1, auto exchange, the peer
+    exchange chosen), every rank closes its session and measures again on reopen()'s (RCCL).
+    The owner-rooted exchange has never run across xGMI on this pool's one-GPU boxes.
+    Returns (session, status, done, seconds, fallback reason or None, the new exchange name)."""
+    st, done, el, err, bad = measure(sess, warm, timed, barrier_sync, any_rank, errors)
+    why, name = None, None
+    if bad and reopen is not None:
+        why = f"peer exchange failed during the run: {err if err else 'on another rank'}"
+        sess.close()
+        sess, name = reopen()
+        st, done, el, err, bad = measure(sess, warm, timed, barrier_sync, any_rank, errors)
+    if bad:
+        raise SystemExit(f"run failed: {err if err else 'on another rank'}")
+    return sess, st, done, el, why, name
+
+
 def alt_exchange_window(sess, dist, barrier_sync, args, L, torch):
     """Switch every rank to the other exchange and time args.alt_pivots pivots.  The switch
     to PEER all-gathers the exchange blocks' IPC handles over the session's communicator;
@@ -321,36 +376,7 @@ def main():
                            exchange=x if xsess else 0)
 
     def any_rank(flag):
-        if dist is None:
-            return flag
-        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return int(t.item()) != 0
-
-    def guarded_run(sess, pivots, timed):
-        """sess.run on every rank.  A failure (an exchange error or timeout) is held until every
-        rank has passed the same barriers, then agreed, so all ranks take the same next step."""
-        err, st, done, el = None, None, 0, 0.0
-        if timed:
-            barrier_sync()
-            t0 = time.perf_counter()
-        try:
-            st, done = sess.run(pivots)
-        except dlp.DLPError as e:
-            err = e
-        if timed:
-            barrier_sync()
-            el = time.perf_counter() - t0
-        return st, done, el, err, any_rank(err is not None)
-
-    def measure(sess):
-        st, done, _, err, bad = guarded_run(sess, warm, False)
-        if bad:
-            return st, done, 0.0, err, True
-        if done != warm:
-            raise SystemExit(f"warm-up ended early: status {st} after {done} pivots")
-        sess.reset_timings()
-        return guarded_run(sess, timed, True)
+        return agree_any(flag, dist, torch, "cuda")
 
     def configure(sess):
         if args.occupancy >= 0 or args.form >= 0:
@@ -369,22 +395,18 @@ def main():
     xmode = XNAMES.get(sess.get_exchange(), "none") if xsess else None
     xreason = sess.exchange_reason() if xsess and hasattr(sess, "exchange_reason") else None
 
-    st, done, elapsed, err, bad = measure(sess)
-    run_fallback = None
-    if bad and world > 1 and xmode == "peer" and args.exchange == "auto":
-        # the owner-rooted exchange failed on some rank during the run (it has never run across
-        # xGMI on this pool's one-GPU boxes): every rank reruns the measurement over RCCL
-        run_fallback = f"peer exchange failed during the run: {err if err else 'on another rank'}"
-        sess.close()
+    def reopen_rccl():
         obj = [dlp.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        sess = open_session(L.XCHG_RCCL, obj[0])
-        configure(sess)
-        xmode = XNAMES.get(sess.get_exchange(), "none")
-        xreason = run_fallback
-        st, done, elapsed, err, bad = measure(sess)
-    if bad:
-        raise SystemExit(f"run failed: {err if err else 'on another rank'}")
+        s2 = open_session(L.XCHG_RCCL, obj[0])
+        configure(s2)
+        return s2, XNAMES.get(s2.get_exchange(), "none")
+
+    fallback_ok = world > 1 and xmode == "peer" and args.exchange == "auto"
+    sess, st, done, elapsed, run_fallback, xmode2 = measure_with_fallback(
+        sess, warm, timed, barrier_sync, any_rank, dlp.DLPError, reopen_rccl if fallback_ok else None)
+    if run_fallback:
+        xmode, xreason = xmode2, run_fallback
     if done != timed:
         raise SystemExit(f"timed window ended early: status {st} after {done} pivots")
     lookahead_on = sess.lookahead()
