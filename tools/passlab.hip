@@ -247,6 +247,33 @@ __global__ __launch_bounds__(256) void copy_kernel(double* __restrict__ T, int64
 }
 
 
+// Out-of-place streaming probe in form 21's shape (T -> To, one double per lane, U = 2 rows per
+// iteration, next group loaded before this one is stored): NTH lanes per workgroup (256 = form 21;
+// 768 = 12 waves, the most that 3 waves/SIMD of a 160-VGPR kernel allow), band of rb rows.
+// Asks whether wider row segments per workgroup (6 KB instead of 2 KB) keep tall bands streaming.
+template <int NTH>
+__global__ __launch_bounds__(NTH) void copyw_kernel(const double* __restrict__ T, double* __restrict__ To,
+                                                    int64_t ld, int64_t rows, int64_t width, int rb) {
+    const int64_t j = (int64_t)blockIdx.x * NTH + threadIdx.x;
+    const bool colok = j < width;
+    const int64_t jc = colok ? j : width - 1;
+    const int64_t i0 = (int64_t)blockIdx.y * rb;
+    const int64_t iend = (i0 + rb < rows) ? i0 + rb : rows;
+    double a0 = __builtin_nontemporal_load(T + i0 * ld + jc);
+    double a1 = i0 + 1 < iend ? __builtin_nontemporal_load(T + (i0 + 1) * ld + jc) : 0.0;
+    for (int64_t i = i0; i < iend; i += 2) {
+        double b0 = 0.0, b1 = 0.0;
+        if (i + 2 < iend) b0 = __builtin_nontemporal_load(T + (i + 2) * ld + jc);
+        if (i + 3 < iend) b1 = __builtin_nontemporal_load(T + (i + 3) * ld + jc);
+        if (colok) {
+            __builtin_nontemporal_store(a0 + 0.0, To + i * ld + j);
+            if (i + 1 < iend) __builtin_nontemporal_store(a1 + 0.0, To + (i + 1) * ld + j);
+        }
+        a0 = b0;
+        a1 = b1;
+    }
+}
+
 // Persistent interleaved probe: G workgroups per 512-column tile, workgroup (x, g) walks
 // bands g, g + G, g + 2G, ... of rb rows; TF: grid x = tile (tile fastest) or band group.
 template <int U>
@@ -1704,6 +1731,39 @@ int main(int argc, char** argv) {
                 const double fl = 2.0 * 64.0 * iters * wg * 256;
                 printf("valu mode %d wgs %d: %.3f ms  %.1f TF/s\n", mode, wg, ms, fl / ms / 1e9);
             }
+        return 0;
+    }
+    if (only && !strcmp(only, "copyw")) {
+        struct C { int nth, rb; };
+        std::vector<C> cs;
+        for (int rb : {8, 32, 256, 768})
+            for (int nth : {256, 512, 768, 1024}) cs.push_back({nth, rb});
+        for (int rep2 = 0; rep2 < 2; ++rep2)
+        for (auto& c : cs) {
+            auto go = [&]() {
+                dim3 grid((unsigned)((L.width + c.nth - 1) / c.nth), (unsigned)((L.rows + c.rb - 1) / c.rb));
+                switch (c.nth) {
+                    case 256: copyw_kernel<256><<<grid, 256>>>(L.T, L.To, L.ld, L.rows, L.width, c.rb); break;
+                    case 512: copyw_kernel<512><<<grid, 512>>>(L.T, L.To, L.ld, L.rows, L.width, c.rb); break;
+                    case 768: copyw_kernel<768><<<grid, 768>>>(L.T, L.To, L.ld, L.rows, L.width, c.rb); break;
+                    default: copyw_kernel<1024><<<grid, 1024>>>(L.T, L.To, L.ld, L.rows, L.width, c.rb); break;
+                }
+            };
+            go();
+            CK(hipDeviceSynchronize());
+            std::vector<float> ms(reps);
+            for (int r = 0; r < reps; ++r) {
+                CK(hipEventRecord(e0, 0));
+                go();
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                CK(hipEventElapsedTime(&ms[r], e0, e1));
+            }
+            std::sort(ms.begin(), ms.end());
+            printf("copyw nth=%4d rb=%4d  median %.3f ms  %6.0f GB/s\n", c.nth, c.rb, ms[reps / 2],
+                   bytes / ms[reps / 2] / 1e6);
+            fflush(stdout);
+        }
         return 0;
     }
     if (only && !strcmp(only, "copyp")) {
