@@ -1,0 +1,91 @@
+"""Every A/B tuning knob of INTEGRATION.md §4 gives the same bits as the default path.
+
+The knobs are read once per process, so each setting runs in a child process (`_knob_run.py`
+below, through the C ABI) and prints digests of what it computed: the pivot log, the objective,
+the basis and — for the deferred sessions — the whole tableau.  The default run of the same
+workload is the reference (it is itself checked against the oracle by the parity tests:
+`test_gpu_large.py`, `test_gpu_lookahead.py`, `test_gpu_cluster.py`, `test_c5_full_batch`)."""
+import functools
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+SCRIPT = r"""
+import hashlib, json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import distributedlpsolver_amd as dlp
+
+def h(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+kind = sys.argv[2]
+out = {}
+if kind == "defer":   # one rank of C3 at P = 8 (2.15 GB): K = 64, lookahead on (form 21) or off (23)
+    la = int(sys.argv[3])
+    with dlp.Session(dlp.Problem.random(4096, 61440, 38), check_interval=64, lookahead=la,
+                     max_pivots=200) as s:
+        out["lookahead"], out["form"] = s.lookahead(), s.defer_form()
+        st, done = s.run(136)   # two full blocks and a partial one
+        r = s.result()
+        out.update(done=done, log=h(r.pivot_log), obj=float(r.objective).hex(), basis=h(r.basis),
+                   tableau=h(s.tableau()))
+elif kind == "batched":
+    r = dlp.batched_solve(512, 64, 128, 5000, want_basis=True, log_cap=256)
+    out.update(obj=h(r.objective), st=h(r.status), np=h(r.num_pivots), basis=h(r.basis), logs=h(r.logs))
+elif kind == "cluster":
+    p = dlp.Problem.random(300, 500, 11)
+    with dlp.Session(p, small_lp=1) as s:
+        out["small_lp"] = s.small_lp()
+        s.run(10 ** 6)
+        r = s.result()
+    out.update(log=h(r.pivot_log), obj=float(r.objective).hex(), x=h(r.x), y=h(r.y))
+print(json.dumps(out))
+"""
+
+
+def _run(kind, args=(), env=None):
+    e = dict(os.environ)
+    for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB"):
+        e.pop(k, None)
+    e.update(env or {})
+    p = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, kind, *map(str, args)], env=e,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@functools.lru_cache(maxsize=None)
+def _ref(kind, *args):
+    return _run(kind, args)
+
+
+@pytest.mark.parametrize("env", [{"DLP_LEAN_LCH": "4"}, {"DLP_LEAN_LCH": "8"}, {"DLP_BAND_PUB": "0"}])
+def test_lookahead_chain_knobs(env):
+    ref = _ref("defer", 1)
+    assert ref["lookahead"] and ref["form"] == 21 and ref["done"] == 136
+    assert _run("defer", [1], env) == ref
+
+
+@pytest.mark.parametrize("depth", ["2", "3"])
+def test_form23_ring_depth(depth):
+    ref = _ref("defer", 0)
+    assert not ref["lookahead"] and ref["form"] == 23
+    assert _run("defer", [0], {"DLP_Q_DEPTH": depth}) == ref
+
+
+def test_batched_lds_kernel_knob():
+    assert _run("batched", env={"DLP_BATCH_LDS": "1"}) == _ref("batched")
+
+
+@pytest.mark.parametrize("wg", ["16", "64"])   # slices of 51 / 13 columns fit the LDS
+def test_cluster_workgroup_knob(wg):
+    ref = _ref("cluster")
+    assert ref["small_lp"]
+    assert _run("cluster", env={"DLP_CLUSTER_WG": wg}) == ref
