@@ -410,6 +410,7 @@ def main():
     if done != timed:
         raise SystemExit(f"timed window ended early: status {st} after {done} pivots")
     lookahead_on = sess.lookahead()
+    chain_cus = sess.chain_cus() if hasattr(sess, "chain_cus") else None
 
     tm, nsamp = sess.timings()
     launches, upd_total_ms, _ = sess.update_stats()
@@ -539,7 +540,9 @@ def main():
             "block": {"ms": 1e3 * elapsed / args.steps * (K / per_step), "pass_ms": upd_ms,
                       "chain_us_per_pivot": ((1e3 * elapsed / args.steps * (K / per_step) - upd_ms) / K * 1e3
                                              if (K > 1 and not lookahead_on and upd_ms > 0) else None),
-                      "lookahead": lookahead_on, "rows_local": rows_local},
+                      "lookahead": lookahead_on, "rows_local": rows_local,
+                      # lookahead: CUs of the chain's stream, the pass on the rest (0 = unmasked)
+                      "chain_cus": chain_cus},
             "alt_exchange_window": alt,
             "objective_after_run": obj_after,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -163,6 +163,7 @@ SIGNATURES = [
     ("dlp_session_get_tuning", C.c_int,
      [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dlp_session_small_lp", C.c_int, [_P, C.POINTER(C.c_int)]),
+    ("dlp_session_chain_cus", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("dlp_session_info", C.c_int,
      [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64)]),
     ("dlp_session_tableau", C.c_int, [_P, _DP]),

@@ -174,6 +174,7 @@ struct dlp_session {
     // allocations from the buffer pool (size class per pointer), returned to it at free
     std::vector<std::pair<void*, size_t>> pooled;
     bool pool_ok = true;   // false once the stream failed: its buffers are freed, not pooled
+    int chain_cus = 0;     // lookahead: CUs of the chain's stream (0 = unmasked; chain_cus_policy)
 };
 
 extern "C" int flush_pending(dlp_session* s);   // defined with the C entry points
@@ -188,6 +189,9 @@ int64_t round16(int64_t v) { return (v + 15) / 16 * 16; }
 // end there (profiles/r03f/).  A freed session's streams (drained without error) go back to a
 // per-(device, priority) pool of at most kStreamPoolMax; a new session takes one from it.
 constexpr size_t kStreamPoolMax = 16;
+// Streams on a CU mask (the lookahead's chain / pass split, chain_cus_policy): a pooled stream key
+// >= kMaskedKey names one, key = kMaskedKey + (first mask bit << 10) + bit count.
+constexpr int kMaskedKey = 1 << 20;
 struct PooledStream {
     int device, prio;
     hipStream_t s;
@@ -204,6 +208,13 @@ hipError_t acquire_stream(int device, int prio, hipStream_t* out) {
                 g_stream_pool.erase(g_stream_pool.begin() + (ptrdiff_t)k);
                 return hipSuccess;
             }
+    }
+    if (prio >= kMaskedKey) {
+        const int first = (prio - kMaskedKey) >> 10, n = (prio - kMaskedKey) & 1023;
+        uint32_t mask[8] = {};
+        for (int b = first; b < first + n && b < 256; ++b) mask[b / 32] |= 1u << (b % 32);
+        (void)hipGetLastError();
+        return hipExtStreamCreateWithCUMask(out, 8, mask);
     }
     return hipStreamCreateWithPriority(out, hipStreamNonBlocking, prio);
 }
@@ -497,6 +508,53 @@ int flush_pending_block(dlp_session* s);
 // between runs (la_policy): a pending block is applied first.  Silently stays off where it does
 // not apply (the form has no out-of-place pass, general LPs, the small-LP launch, per-phase
 // timing, a host-driven rank unless forced, too little free memory).
+// The lookahead's CU split.  Beside the pass, the selection chain of a rank-sized tableau is the
+// longer of the two and runs 2-3x slower than alone, its waves sharing every CU with three pass
+// waves.  On disjoint CU masks (chain on the top n mask bits, the pass on the rest) the block
+// balances: measured on the rank geometries (profiles/r04x/, alternating runs), c3r8 (4,096 rows)
+// n = 128: 24.3-24.5 k vs 22.65 k pivots/s; c3r4 (8,192) n = 80-96: 19.9-20.0 k vs 17.0-17.1 k;
+// c3r2 (16,384) n = 48-64: 12.5-12.6 k vs 11.97 k; C3 (32,768 rows, pass-bound) loses with any
+// split (n = 16 / 32: 6.6 / 7.4 k vs 7.8 k).  Auto: n = 32 (log2(32768 / rows) + 1) for fewer than
+// 32,768 local rows (128 / 96 / 64 at 4,096 / 8,192 / 16,384), at most half the CUs, 0 (no masks)
+// from 32,768; DLP_CHAIN_CUS=n overrides (0 = off).
+int chain_cus_policy(const dlp_session* s) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 64)
+        return 0;
+    if (const char* e = std::getenv("DLP_CHAIN_CUS")) {
+        const int n = std::atoi(e);
+        return n > 0 && n < cus ? n : 0;
+    }
+    if (s->rows >= 32768) return 0;
+    const double lg = std::log2(32768.0 / (double)std::max<int64_t>(s->rows, 1));
+    int n = (int)std::lround(32.0 * (lg + 1.0) / 16.0) * 16;
+    return std::min(std::max(n, 0), cus / 2);
+}
+
+// Put the chain's stream on the top n CU-mask bits (n = 0: an unmasked stream at the chain's
+// priority), and name the pass's stream key accordingly (acquired by the caller).  Results do not
+// depend on where a kernel runs.
+int chain_cus_apply(dlp_session* s, int n) {
+    if (n == s->chain_cus) return DLP_OK;
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess) cus = 256;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->pstream) {
+        HIP_TRY(hipStreamSynchronize(s->pstream));
+        release_stream(s->device, s->prio_pass, s->pstream);
+        s->pstream = nullptr;
+    }
+    release_stream(s->device, s->prio_chain, s->stream);
+    s->stream = nullptr;
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    s->prio_chain = n > 0 ? kMaskedKey + ((cus - n) << 10) + n : hi;
+    s->prio_pass = n > 0 ? kMaskedKey + (cus - n) : lo;
+    HIP_TRY(acquire_stream(s->device, s->prio_chain, &s->stream));
+    s->chain_cus = n;
+    return DLP_OK;
+}
+
 int la_enable(dlp_session* s, bool forced) {
     if (s->la) return DLP_OK;
     const bool host_driven = s->nranks > 1 && !s->use_rccl && s->xmode != dlp_session::X_PEER;
@@ -548,7 +606,10 @@ int la_enable(dlp_session* s, bool forced) {
         HIP_TRY(pool_alloc(s, s->device, (void**)&s->band_cnt, sizeof(uint32_t) * 2 * s->band_stride));
     }
     HIP_TRY(hipMemsetAsync(s->band_cnt, 0, sizeof(uint32_t) * 2 * s->band_stride, s->stream));
-    if (!s->pstream) HIP_TRY(acquire_stream(s->device, s->prio_pass, &s->pstream));
+    if (!s->pstream) {
+        CALL_TRY(chain_cus_apply(s, chain_cus_policy(s)));
+        HIP_TRY(acquire_stream(s->device, s->prio_pass, &s->pstream));
+    }
     if (!s->ev_seal) HIP_TRY(hipEventCreateWithFlags(&s->ev_seal, hipEventDisableTiming));
     if (!s->ev_pass) HIP_TRY(hipEventCreateWithFlags(&s->ev_pass, hipEventDisableTiming));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -959,6 +1020,7 @@ int la_disable(dlp_session* s) {
     s->d.form = form;
     s->la = false;
     s->opt.lookahead = 0;
+    CALL_TRY(chain_cus_apply(s, 0));   // the pass runs on the chain's stream again: every CU
     pick_form(s);
     return DLP_OK;
 }
@@ -2535,6 +2597,12 @@ int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_bl
     if (update_variant) *update_variant = s->opt.update_variant;
     if (rows_per_block) *rows_per_block = s->d.K > 1 ? s->defer_rb : s->g.rows_per_block;
     if (nontemporal) *nontemporal = s->opt.nontemporal;
+    return DLP_OK;
+}
+
+int dlp_session_chain_cus(dlp_session* s, int* cus) {
+    if (!s || !cus) return DLP_ERR_ARG;
+    *cus = s->la ? s->chain_cus : 0;
     return DLP_OK;
 }
 

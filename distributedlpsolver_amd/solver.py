@@ -285,6 +285,12 @@ class Session:
                 "dlp_session_get_tuning")
         return v.value, rb.value, nt.value
 
+    def chain_cus(self) -> int:
+        """Lookahead: CUs the selection chain's stream runs on (the pass on the rest; 0 = unmasked)."""
+        v = C.c_int()
+        L.check(L.lib().dlp_session_chain_cus(self._h, C.byref(v)), "dlp_session_chain_cus")
+        return v.value
+
     def small_lp(self) -> bool:
         """True when this session solves in the one-launch LDS path (options.small_lp)."""
         v = C.c_int()

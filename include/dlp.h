@@ -304,6 +304,9 @@ int dlp_session_set_tuning(dlp_session* s, int update_variant, int rows_per_bloc
 int dlp_session_get_tuning(dlp_session* s, int* update_variant, int* rows_per_block, int* nontemporal);
 /* 1 when the session solves in the one-launch LDS path (options.small_lp), else 0. */
 int dlp_session_small_lp(dlp_session* s, int* small_lp);
+/* Lookahead sessions: the CUs the selection chain runs on, the pass on the others (0 = both
+ * unmasked).  Auto from the rank's rows; DLP_CHAIN_CUS=n overrides. */
+int dlp_session_chain_cus(dlp_session* s, int* cus);
 /* Deferred sessions: workgroups per CU allowed for the tableau pass (LDS
  * reservation; 0 = no cap, the default) and its form (-1 = keep):
  *   LDS-staged coefficients: 0 = 2 doubles per lane (K <= 32), 1 / 2 = 1 double

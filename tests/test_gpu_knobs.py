@@ -31,7 +31,7 @@ if kind == "defer":   # one rank of C3 at P = 8 (2.15 GB): K = 64, lookahead on 
     la = int(sys.argv[3])
     with dlp.Session(dlp.Problem.random(4096, 61440, 38), check_interval=64, lookahead=la,
                      max_pivots=200) as s:
-        out["lookahead"], out["form"] = s.lookahead(), s.defer_form()
+        out["lookahead"], out["form"], out["chain_cus"] = s.lookahead(), s.defer_form(), s.chain_cus()
         st, done = s.run(136)   # two full blocks and a partial one
         r = s.result()
         out.update(done=done, log=h(r.pivot_log), obj=float(r.objective).hex(), basis=h(r.basis),
@@ -52,7 +52,7 @@ print(json.dumps(out))
 
 def _run(kind, args=(), env=None):
     e = dict(os.environ)
-    for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB"):
+    for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB", "DLP_CHAIN_CUS"):
         e.pop(k, None)
     e.update(env or {})
     p = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, kind, *map(str, args)], env=e,
@@ -66,17 +66,23 @@ def _ref(kind, *args):
     return _run(kind, args)
 
 
-@pytest.mark.parametrize("env", [{"DLP_LEAN_LCH": "4"}, {"DLP_LEAN_LCH": "8"}, {"DLP_BAND_PUB": "0"}])
+@pytest.mark.parametrize("env", [{"DLP_LEAN_LCH": "4"}, {"DLP_LEAN_LCH": "8"}, {"DLP_BAND_PUB": "0"},
+                                 {"DLP_CHAIN_CUS": "0"}, {"DLP_CHAIN_CUS": "32"}, {"DLP_CHAIN_CUS": "200"}])
 def test_lookahead_chain_knobs(env):
     ref = _ref("defer", 1)
-    assert ref["lookahead"] and ref["form"] == 21 and ref["done"] == 136
-    assert _run("defer", [1], env) == ref
+    # 4,096 rows: the chain on 128 CUs, the pass on the other 128 (chain_cus_policy)
+    assert ref["lookahead"] and ref["form"] == 21 and ref["done"] == 136 and ref["chain_cus"] == 128
+    got = _run("defer", [1], env)
+    if "DLP_CHAIN_CUS" in env:
+        assert got.pop("chain_cus") == int(env["DLP_CHAIN_CUS"])
+        ref = {k: v for k, v in ref.items() if k != "chain_cus"}
+    assert got == ref
 
 
 @pytest.mark.parametrize("depth", ["2", "3"])
 def test_form23_ring_depth(depth):
     ref = _ref("defer", 0)
-    assert not ref["lookahead"] and ref["form"] == 23
+    assert not ref["lookahead"] and ref["form"] == 23 and ref["chain_cus"] == 0
     assert _run("defer", [0], {"DLP_Q_DEPTH": depth}) == ref
 
 
