@@ -547,8 +547,7 @@ __device__ __forceinline__ void prow_defer_body(
     // LEAN, band publication: row p final in Tn (its band of the sealed block's pass is done):
     // start there and replay this block's steps only
     bool pdone = false;
-    if constexpr (LEAN)
-        if (bcnt && kp > 0 && pl >= 0)
+    if (bcnt && kp > 0 && pl >= 0)
             pdone = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load(&bcnt[pl / brb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == (uint32_t)bnt;
     const int L0 = pdone ? kp : 0;
@@ -635,8 +634,8 @@ __device__ __forceinline__ void prow_defer_body(
                 }
             }
         };
-        if (S > 0) fetch(pa, 0);
-        for (int l0 = 0; l0 < S; l0 += 2 * CH) {
+        if (S > L0) fetch(pa, L0);
+        for (int l0 = L0; l0 < S; l0 += 2 * CH) {
             if (l0 + CH < S) fetch(pb, l0 + CH);
             apply(pa, l0);
             if (l0 + CH >= S) break;
@@ -2303,12 +2302,22 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                              int64_t* prow_bits, PricePart* pp, double tol_dj, dlp_pivot* log,
                              int64_t log_cap, int nranks, hipStream_t s, const Defer* prev,
                              int prev_seal, const XPeers* xp, uint32_t xseq, const BandPub* bp,
-                             bool xfuse) {
+                             bool xfuse, bool own_cus) {
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     const int xc = (xfuse && xp && nranks > 1) ? 1 : 0;
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
-    if (prev_seal >= 0 && d.K > 32) {   // lookahead at K = 64: beside the form-21 pass
+    static const int fat_env = std::getenv("DLP_FAT_PROW") ? std::atoi(std::getenv("DLP_FAT_PROW")) : -1;
+    const bool fat = fat_env >= 0 ? fat_env == 1 : own_cus;
+    if (prev_seal >= 0 && d.K > 32 && fat) {
+        // lookahead with the chain on CUs of its own (no pass waves beside it): the register
+        // kernel, 2 x 16 pivot rows in flight, with band publication
+        prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits,
+                                                 pp, tol_dj, log, log_cap, nranks == 1 ? 1 : 0, prev->C, prev->P,
+                                                 prev_seal, nranks == 1 ? nullptr : xp, xseq,
+                                                 pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1,
+                                                 pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xc);
+    } else if (prev_seal >= 0 && d.K > 32) {   // lookahead at K = 64: beside the form-21 pass
 #define DLP_PROW_LEAN(RS)                                                                                  \
     prow_lean_kernel<RS><<<blocks, 256, prow_ring_bytes(RS), s>>>(                                          \
         g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap,     \

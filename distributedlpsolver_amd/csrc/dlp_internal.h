@@ -266,7 +266,7 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                              int64_t log_cap, int nranks, hipStream_t s,
                              const Defer* prev = nullptr, int prev_seal = -1,
                              const XPeers* xp = nullptr, uint32_t seq = 0, const BandPub* bp = nullptr,
-                             bool xfuse = false);
+                             bool xfuse = false, bool own_cus = false);
 // nranks > 1, after the MAX all-reduce: P[s] from the exchanged bits + objective row + pricing.
 // xp: each workgroup first waits for its chunk's flag (seq), then reads the row region
 // with system-scope loads (prow_bits = this rank's row region).

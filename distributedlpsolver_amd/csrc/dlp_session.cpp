@@ -1132,7 +1132,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         if (xp) s->xseq_r += 1;
         HIP_TRY(dlp::launch_prow_defer(gsel, *dcur, s->st, s->prow_send, s->pp, o.tol_dj, s->log,
                                        s->log_cap, s->exchange ? 2 : 1, s->stream, dprev, pseal, xp,
-                                       s->xseq_r, &bp, xf));
+                                       s->xseq_r, &bp, xf, s->chain_cus > 0));
         if (s->xmode == dlp_session::X_RCCL)
             NCCL_TRY(ncclAllReduce(s->prow_send, s->prow_recv, (size_t)s->ld, ncclInt64, ncclMax,
                                    s->comm, s->stream));
