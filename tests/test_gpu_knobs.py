@@ -52,7 +52,8 @@ print(json.dumps(out))
 
 def _run(kind, args=(), env=None):
     e = dict(os.environ)
-    for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB", "DLP_CHAIN_CUS"):
+    for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB", "DLP_CHAIN_CUS",
+              "DLP_FAT_PROW"):
         e.pop(k, None)
     e.update(env or {})
     p = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, kind, *map(str, args)], env=e,
@@ -67,7 +68,8 @@ def _ref(kind, *args):
 
 
 @pytest.mark.parametrize("env", [{"DLP_LEAN_LCH": "4"}, {"DLP_LEAN_LCH": "8"}, {"DLP_BAND_PUB": "0"},
-                                 {"DLP_CHAIN_CUS": "0"}, {"DLP_CHAIN_CUS": "32"}, {"DLP_CHAIN_CUS": "200"}])
+                                 {"DLP_CHAIN_CUS": "0"}, {"DLP_CHAIN_CUS": "32"}, {"DLP_CHAIN_CUS": "200"},
+                                 {"DLP_FAT_PROW": "0"}])
 def test_lookahead_chain_knobs(env):
     ref = _ref("defer", 1)
     # 4,096 rows: the chain on 128 CUs, the pass on the other 128 (chain_cus_policy)
