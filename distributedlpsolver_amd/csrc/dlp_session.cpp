@@ -550,7 +550,14 @@ int chain_cus_apply(dlp_session* s, int n) {
     HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     s->prio_chain = n > 0 ? kMaskedKey + ((cus - n) << 10) + n : hi;
     s->prio_pass = n > 0 ? kMaskedKey + (cus - n) : lo;
-    HIP_TRY(acquire_stream(s->device, s->prio_chain, &s->stream));
+    if (n > 0 && acquire_stream(s->device, s->prio_chain, &s->stream) != hipSuccess) {
+        (void)hipGetLastError();   // no CU-masked queue here: both streams unmasked, as before round 4
+        s->stream = nullptr;
+        s->prio_chain = hi;
+        s->prio_pass = lo;
+        n = 0;
+    }
+    if (!s->stream) HIP_TRY(acquire_stream(s->device, s->prio_chain, &s->stream));
     s->chain_cus = n;
     return DLP_OK;
 }
@@ -608,7 +615,12 @@ int la_enable(dlp_session* s, bool forced) {
     HIP_TRY(hipMemsetAsync(s->band_cnt, 0, sizeof(uint32_t) * 2 * s->band_stride, s->stream));
     if (!s->pstream) {
         CALL_TRY(chain_cus_apply(s, chain_cus_policy(s)));
-        HIP_TRY(acquire_stream(s->device, s->prio_pass, &s->pstream));
+        if (acquire_stream(s->device, s->prio_pass, &s->pstream) != hipSuccess) {
+            (void)hipGetLastError();   // no CU-masked queue for the pass: back to unmasked streams
+            s->pstream = nullptr;
+            CALL_TRY(chain_cus_apply(s, 0));
+            HIP_TRY(acquire_stream(s->device, s->prio_pass, &s->pstream));
+        }
     }
     if (!s->ev_seal) HIP_TRY(hipEventCreateWithFlags(&s->ev_seal, hipEventDisableTiming));
     if (!s->ev_pass) HIP_TRY(hipEventCreateWithFlags(&s->ev_pass, hipEventDisableTiming));
