@@ -497,7 +497,12 @@ int validate_options(const dlp_options* o) {
 // profiles/r03d/)
 void pick_form(dlp_session* s) {
     if (!s->form_auto || s->d.K != 64 || !s->streaming || (s->d.form != 21 && s->d.form != 23)) return;
-    s->d.form = s->la ? 21 : 23;
+    // lookahead: form 21 beside the chain (its waves fit the 32 VGPRs three form-21 waves leave);
+    // on a CU split of more than 4,096 rows the LDS-ring pass (form 23), which streams faster per
+    // CU and no longer slows a chain on other CUs: c3r2 13.9-14.3 k vs 12.6 k pivots/s, c3r4
+    // 20.6 k (chain on 128 CUs) vs 20.0-20.3 k (form 21 on 96); c3r8 24.4-24.5 k vs 24.7 k, so
+    // form 21 there (profiles/r04ag/, r04ah/)
+    s->d.form = !s->la ? 23 : (s->chain_cus > 0 && s->rows > 4096) ? 23 : 21;
     s->dslot[0].form = s->dslot[1].form = s->d.form;
 }
 
@@ -511,11 +516,13 @@ int flush_pending_block(dlp_session* s);
 // The lookahead's CU split.  Beside the pass, the selection chain of a rank-sized tableau is the
 // longer of the two and runs 2-3x slower than alone, its waves sharing every CU with three pass
 // waves.  On disjoint CU masks (chain on the top n mask bits, the pass on the rest) the block
-// balances: measured on the rank geometries (profiles/r04x/, alternating runs), c3r8 (4,096 rows)
-// n = 128: 24.3-24.5 k vs 22.65 k pivots/s; c3r4 (8,192) n = 80-96: 19.9-20.0 k vs 17.0-17.1 k;
-// c3r2 (16,384) n = 48-64: 12.5-12.6 k vs 11.97 k; C3 (32,768 rows, pass-bound) loses with any
-// split (n = 16 / 32: 6.6 / 7.4 k vs 7.8 k).  Auto: n = 32 (log2(32768 / rows) + 1) for fewer than
-// 32,768 local rows (128 / 96 / 64 at 4,096 / 8,192 / 16,384), at most half the CUs, 0 (no masks)
+// balances: measured on the rank geometries with the form-21 pass (profiles/r04x/, alternating
+// runs), c3r8 (4,096 rows) n = 128: 24.3-24.5 k vs 22.65 k pivots/s; c3r4 (8,192) n = 80-96:
+// 19.9-20.0 k vs 17.0-17.1 k; c3r2 (16,384) n = 48-64: 12.5-12.6 k vs 11.97 k; C3 (32,768 rows,
+// pass-bound) loses with any split (form 21 n = 32: 7.63 k, form 23 n = 32: 8.05 k vs 8.22 k
+// unmasked on one box, profiles/r04ai/).  With the form-23 pass on the split (pick_form) the
+// best n moves: c3r4 128 (20.6 k), c3r2 64 (13.9-14.3 k), c3r8 128 (profiles/r04ah/).  Auto: 128
+// CUs for the chain up to 8,192 local rows, 64 below 32,768, at most half the CUs, 0 (no masks)
 // from 32,768; DLP_CHAIN_CUS=n overrides (0 = off).
 int chain_cus_policy(const dlp_session* s) {
     int cus = 0;
@@ -525,10 +532,10 @@ int chain_cus_policy(const dlp_session* s) {
         const int n = std::atoi(e);
         return n > 0 && n < cus ? n : 0;
     }
+    // (mask bits act in groups of 32: 112 and 128 chain bits, or 144 and 160, give the pass the
+    // same time, profiles/r04ah/)
     if (s->rows >= 32768) return 0;
-    const double lg = std::log2(32768.0 / (double)std::max<int64_t>(s->rows, 1));
-    int n = (int)std::lround(32.0 * (lg + 1.0) / 16.0) * 16;
-    return std::min(std::max(n, 0), cus / 2);
+    return std::min(s->rows > 8192 ? 64 : 128, cus / 2);
 }
 
 // Put the chain's stream on the top n CU-mask bits (n = 0: an unmasked stream at the chain's

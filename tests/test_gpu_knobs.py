@@ -27,9 +27,10 @@ def h(a):
 
 kind = sys.argv[2]
 out = {}
-if kind == "defer":   # one rank of C3 at P = 8 (2.15 GB): K = 64, lookahead on (form 21) or off (23)
+if kind == "defer":   # one rank of C3 at P = 8 (2.15 GB) or P = 4 (4.3 GB): K = 64, lookahead or not
     la = int(sys.argv[3])
-    with dlp.Session(dlp.Problem.random(4096, 61440, 38), check_interval=64, lookahead=la,
+    m, n, seed = (4096, 61440, 38) if len(sys.argv) < 5 else (8192, 57344, 34)
+    with dlp.Session(dlp.Problem.random(m, n, seed), check_interval=64, lookahead=la,
                      max_pivots=200) as s:
         out["lookahead"], out["form"], out["chain_cus"] = s.lookahead(), s.defer_form(), s.chain_cus()
         st, done = s.run(136)   # two full blocks and a partial one
@@ -79,6 +80,16 @@ def test_lookahead_chain_knobs(env):
         assert got.pop("chain_cus") == int(env["DLP_CHAIN_CUS"])
         ref = {k: v for k, v in ref.items() if k != "chain_cus"}
     assert got == ref
+
+
+def test_cu_split_with_the_form23_pass():
+    """8,192 rows (one rank of C3 at P = 4): the chain on 128 CUs and the LDS-ring pass (form 23)
+    on the rest, against both streams unmasked with the form-21 pass: the same bits."""
+    ref = _run("defer", [1, "p4"])
+    assert ref["lookahead"] and ref["form"] == 23 and ref["chain_cus"] == 128
+    got = _run("defer", [1, "p4"], {"DLP_CHAIN_CUS": "0"})
+    assert got.pop("form") == 21 and got.pop("chain_cus") == 0
+    assert got == {k: v for k, v in ref.items() if k not in ("form", "chain_cus")}
 
 
 @pytest.mark.parametrize("depth", ["2", "3"])
