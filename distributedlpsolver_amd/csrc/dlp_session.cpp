@@ -210,6 +210,7 @@ hipError_t acquire_stream(int device, int prio, hipStream_t* out) {
             }
     }
     if (prio >= kMaskedKey) {
+        if (std::getenv("DLP_TEST_MASK_FAIL")) return hipErrorNotSupported;   // tests: no CU-masked queues
         const int first = (prio - kMaskedKey) >> 10, n = (prio - kMaskedKey) & 1023;
         uint32_t mask[8] = {};
         for (int b = first; b < first + n && b < 256; ++b) mask[b / 32] |= 1u << (b % 32);

@@ -309,7 +309,10 @@ def test_lds_forms_on_streaming_k64_geometry(form):
     k = 2 * 64 + 9
     prob = dlp.Problem.random(m, n, 21)
     with dlp.Session(prob, defer=64, check_interval=64) as s:
-        assert s.get_tuning()[1] == 768 and s.defer_form() == (21 if s.lookahead() else 23)
+        # lookahead: form 21 beside the chain, form 23 when the chain has CUs of its own (16,384 rows:
+        # 64 of them); no lookahead: form 23
+        assert s.get_tuning()[1] == 768
+        assert s.defer_form() == (21 if s.lookahead() and s.chain_cus() == 0 else 23)
         s.set_defer_tuning(0, form)
         rb = s.get_tuning()[1]
         assert 64 * rb * 8 + rb * 4 + 64 * 4 <= 160 * 1024 and rb >= 256

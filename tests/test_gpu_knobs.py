@@ -54,7 +54,7 @@ print(json.dumps(out))
 def _run(kind, args=(), env=None):
     e = dict(os.environ)
     for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB", "DLP_CHAIN_CUS",
-              "DLP_FAT_PROW"):
+              "DLP_FAT_PROW", "DLP_TEST_MASK_FAIL"):
         e.pop(k, None)
     e.update(env or {})
     p = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, kind, *map(str, args)], env=e,
@@ -89,6 +89,15 @@ def test_cu_split_with_the_form23_pass():
     assert ref["lookahead"] and ref["form"] == 23 and ref["chain_cus"] == 128
     got = _run("defer", [1, "p4"], {"DLP_CHAIN_CUS": "0"})
     assert got.pop("form") == 21 and got.pop("chain_cus") == 0
+    assert got == {k: v for k, v in ref.items() if k not in ("form", "chain_cus")}
+
+
+def test_cu_split_falls_back_to_unmasked_streams():
+    """Where CU-masked queues cannot be created the lookahead runs on unmasked streams (form 21), the
+    same bits."""
+    ref = _run("defer", [1, "p4"])
+    got = _run("defer", [1, "p4"], {"DLP_TEST_MASK_FAIL": "1"})
+    assert got.pop("chain_cus") == 0 and got.pop("form") == 21 and got["lookahead"]
     assert got == {k: v for k, v in ref.items() if k not in ("form", "chain_cus")}
 
 
