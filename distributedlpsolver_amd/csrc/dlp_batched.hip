@@ -444,9 +444,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     __shared__ int32_t s_p, s_leave, s_bland;
     __shared__ double s_piv;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int W = n + 1, N = n + M;
-    const int sl = tid;              // this lane's slot: < n a variable's column, n the RHS
-    const bool own = sl < W;
+    const int N = n + M;
+    const int sl = tid;              // this lane's slot: < n a variable's column
+    const bool own = sl < n;
     int var = sl < n ? sl : kNoIndex;   // the variable in the slot
     const int64_t lp = blockIdx.x;
     // buffer loads, one lane offset and the row in the scalar offset (a flat load per row
@@ -454,16 +454,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     // read out of range, which returns +0
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Tg + lp * (int64_t)R * ldg), (short)0, (int)((int64_t)R * ldg * 8), 0x00020000);
-    const int voff = own ? (sl < n ? sl : N) * 8 : 0x7fffff00;
+    const int voff = own ? sl * 8 : 0x7fffff00;
     double t[R];
     each<R>([&](auto I) {
         t[I] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (int)(I * ldg * 8), 0));
     });
-    // wave 0, lane i also keeps row i's RHS (the ratio test's), updated with the RHS slot's own
-    // operations below (same bits), so the RHS column is never copied to LDS
-    double rr = 0.0;
-    if (wid == 0)
+    // wave 0, lane i keeps row i's RHS (the ratio test's) and every lane of wave 0 the objective
+    // value T[M][N], each updated with the operations a column slot's elimination applies (same
+    // bits): the RHS column needs no slot of its own, so n columns take ceil(n / 64) waves (round
+    // 4: 64 x 128 in 2 waves instead of 3, 64 x 64 in 1 instead of 2; more LPs per CU)
+    double rr = 0.0, zr = 0.0;
+    if (wid == 0) {
         rr = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(((int64_t)lane * ldg + N) * 8), 0, 0));
+        zr = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(((int64_t)M * ldg + N) * 8), 0, 0));
+    }
     for (int i = tid; i < M; i += blockDim.x) s_basis[i] = n + i;
     if (tid == 0) s_bland = pricing == DLP_PRICING_BLAND ? 1 : 0;
     __syncthreads();
@@ -596,21 +600,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         elim_row(t[M], s_colq[M], pj);   // the objective row
         each<M / 8>([&](auto G) { set8<8 * G>(&t[8 * G], pj, p); });   // row p := the pivot row
         move_if_row<M>(t[M], pj, p);
-        if (wid == 0) {   // the RHS of row `lane`, as the RHS slot updates it
+        if (wid == 0) {   // the RHS of row `lane` and the objective value, as a column slot updates its rows
             const double fr = s_colq[lane];
             const double pjr = __shfl(rr, p) / s_piv;
             const double v = __builtin_fma(-fr, pjr, rr);
             rr = lane == p ? pjr : (fr != 0.0 ? v : rr);
+            const double fz = s_colq[M];
+            if (fz != 0.0) zr = __builtin_fma(-fz, pjr, zr);
         }
         stamp(5);
-        if (sl == n && out.logs && k < out.log_cap) out.logs[lp * out.log_cap + k].objective = t[M];
+        if (tid == 0 && out.logs && k < out.log_cap) out.logs[lp * out.log_cap + k].objective = zr;
     }
-    if (sl == n) {
+    if (tid == 0) {
         int stt = status;
         if (stt == DLP_RUNNING) stt = DLP_PIVOT_LIMIT;
         if (out.status) out.status[lp] = stt;
         if (out.npivots) out.npivots[lp] = k;
-        if (out.objective) out.objective[lp] = t[M];
+        if (out.objective) out.objective[lp] = zr;
     }
     if (out.basis)
         for (int i = tid; i < M; i += blockDim.x) out.basis[lp * M + i] = s_basis[i];
@@ -689,10 +695,10 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
             HIP_BTRY(hipMemsetAsync(dStamps, 0, sizeof(uint64_t) * 64 * 8, s));
             bo.stamps = dStamps;
         }
-        // m = 64 with n + 1 <= 192 slots: the register-resident kernel (DLP_BATCH_LDS=1: the
-        // LDS kernel, for A/B); otherwise the LDS-resident one
+        // m = 64 with n <= 192 columns: the register-resident kernel (DLP_BATCH_LDS=1: the LDS
+        // kernel, for A/B); otherwise the LDS-resident one
         static const bool force_lds = std::getenv("DLP_BATCH_LDS") && std::atoi(std::getenv("DLP_BATCH_LDS")) == 1;
-        const int nw = (int)((n + 1 + 63) / 64);
+        const int nw = (int)((n + 63) / 64);
         const bool reg = !force_lds && m == 64 && nw >= 1 && nw <= 3;
         if (!reg)
             HIP_BTRY(hipFuncSetAttribute((const void*)dlp::batched_solve_kernel,
