@@ -24,7 +24,9 @@ line = json.loads(out.strip().splitlines()[-1])
 st = np.fromfile(path, dtype=np.uint64).reshape(64, 16).astype(np.float64) / 100.0   # µs
 # (stamp 5, the ticket, is not taken when the ratio launch selects for the peer exchange)
 fused = not (st[:, 5] > 0).any()
-ok = (st[:, [0, 1, 2, 3, 4, 6, 8, 9, 10, 11] + ([] if fused else [5])] > 0).all(axis=1)
+# (the register pivot-row kernel, used when the chain has CUs of its own, writes no stamps 8-11)
+prow_stamped = (st[:, [8, 9, 10, 11]] > 0).all(axis=1).any()
+ok = (st[:, [0, 1, 2, 3, 4, 6] + ([8, 9, 10, 11] if prow_stamped else []) + ([] if fused else [5])] > 0).all(axis=1)
 full = st.copy()
 st = st[ok]
 names = ["ratio: pricing reduce (start -> q)", "ratio: T0[i][q] + P[l][q] in", "ratio: replay (lane 0)",
@@ -35,7 +37,8 @@ pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 8), (8, 9), (9, 10)
 if fused:   # every workgroup pushes its candidate; workgroup 0 gathers them all and selects
     names = names[:4] + ["ratio: push + gather + select (wg 0: reduce -> end)"] + names[6:]
     pairs = pairs[:4] + [(4, 6)] + pairs[6:]
-res = {n: float(np.median(st[:, b] - st[:, a])) for n, (a, b) in zip(names, pairs)}
+res = {n: float(np.median(st[:, b] - st[:, a])) for n, (a, b) in zip(names, pairs)
+       if prow_stamped or (a < 8 and b < 8)}
 if (st[:, 13:15] > 0).all() and not (st[:, 12] > 0).any():   # peer, fused: the commit in the prow launch
     res["prow: commit wait (push end -> chunk flag)"] = float(np.median(st[:, 13] - st[:, 11]))
     res["prow: commit (P, objective row, pricing)"] = float(np.median(st[:, 14] - st[:, 13]))
@@ -48,7 +51,9 @@ elif (st[:, 12:15] > 0).all():   # exchange sessions: the pivot row is pushed, t
     res["pivot total (ratio start -> commit end)"] = float(np.median(st[:, 14] - st[:, 0]))
     res["pivot period (ratio start -> next ratio start)"] = float(np.median(np.diff(np.sort(st[:, 0]))))
 res["ratio total (start -> end)"] = float(np.median(st[:, 6] - st[:, 0]))
-res["prow total"] = float(np.median(st[:, 11] - st[:, 8]))
+if prow_stamped:
+    res["prow total"] = float(np.median(st[:, 11] - st[:, 8]))
+res["pivot period (ratio start -> next ratio start)"] = float(np.median(np.diff(np.sort(st[:, 0]))))
 # by position k in the block (slot k = pivot count mod 64): when each pivot starts after the block's
 # first, and its ratio / pivot-row launch durations (-1: stamp missing)
 t0 = full[0, 0]
