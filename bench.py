@@ -59,6 +59,8 @@ WORKLOADS = {
                                "tableau 16385 x 65537 = one rank of the 2-GPU C3 split, 1-rank exchange"),
 }
 RANK_WORKLOADS = ("c3r2", "c3r4", "c3r8")
+# C5 (BASELINE.json configs[4]): 4,096 independent 64 x 128 LPs, one workgroup per LP
+C5 = {"nlp": 4096, "m": 64, "n": 128, "seed": 5000}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP64_PEAK_TFS = 77.3   # measured v_fma_f64 peak on MI355X (tools/passlab.hip valu probe)
 
@@ -70,7 +72,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--step-unit", default="block", choices=("block", "pivot"),
                     help="block: a step is K pivots + one rank-K tableau pass; pivot: one pivot")
-    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS) + ["c5"],
+                    help="c5: the batched small-LP workload (a step = one solve of the whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="CPU baseline: time budget of each oracle window (all CPUs, OMP share, 1)")
@@ -282,6 +285,11 @@ def measure_with_fallback(sess, warm, timed, barrier_sync, any_rank, errors, reo
     why, name = None, None
     if bad and reopen is not None:
         why = f"peer exchange failed during the run: {err if err else 'on another rank'}"
+        # a connected rank's exchange block receives its peers' stores: end every rank's device
+        # waits (abort word), drain this rank's streams, and only after every rank has done so
+        # (barrier) free anything (include/dlp.h, "Freeing connected ranks")
+        sess.abort()
+        barrier_sync()
         sess.close()
         sess, name = reopen()
         st, done, el, err, bad = measure(sess, warm, timed, barrier_sync, any_rank, errors)
@@ -328,8 +336,124 @@ def alt_exchange_window(sess, dist, barrier_sync, args, L, torch):
     return out
 
 
+def c5_cpu_baseline(budget_s):
+    """The oracle (same rule, 1 thread) on consecutive LPs of the C5 batch until budget_s of
+    solve time (generation not timed): LPs/s on one core."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py  # test infrastructure: the CPU comparator only
+    model, nproc, avail = cpu_info()
+    secs, k, piv = 0.0, 0, 0
+    while secs < budget_s and k < C5["nlp"]:
+        A, b, c = oracle_py.gen_dense(C5["m"], C5["n"], C5["seed"] + k)
+        t0 = time.perf_counter()
+        r = oracle_py.solve_dense(A, b, c, nthreads=1, log_cap=0)
+        secs += time.perf_counter() - t0
+        piv += r.num_pivots
+        k += 1
+    return {"value": k / secs, "unit": "LPs/s", "cores": 1, "kind": "port", "cpu_model": model,
+            "sample": f"in-repo C++ oracle (same rule, 1 thread) on LPs 0..{k - 1} of the batch: {k} LPs, "
+                      f"{piv} pivots in {secs:.2f} s of solve time (generation not timed)"}
+
+
+def c5_main(args):
+    """--workload c5: the whole batch solved S times after W warm-ups.  A step = one
+    dlp_batched_solve of the batch (tableaus generated on the device, then ONE solve kernel);
+    `value` = LPs / s of solve-kernel time (HIP events around the kernel: inputs resident in
+    HBM), the wall rate (allocation + generation + read-back included) beside it.  roofline:
+    C5 is bound by per-pivot serial latency x residency, not by HBM or the FMA pipe
+    (DESIGN.md §6): peak = resident LPs (occupancy query) / the single-LP pivot latency
+    (256 LPs, one per CU), achieved = the batch's pivots / kernel time."""
+    import torch
+    import numpy as np
+    import distributedlpsolver_amd as dlp
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # strong split: rank r takes LPs [r nlp / P, (r + 1) nlp / P) of the batch (seeds seed + k)
+    first, last = rank * C5["nlp"] // world, (rank + 1) * C5["nlp"] // world
+    nlp, m, n = last - first, C5["m"], C5["n"]
+    seed = C5["seed"] + first
+
+    def solve():
+        return dlp.batched_solve(nlp, m, n, seed, device=local, log_cap=0)
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        solve()
+    sync()
+    t0 = time.perf_counter()
+    kms, piv, allopt = [], [], True
+    for _ in range(args.steps):
+        br = solve()
+        kms.append(br.kernel_ms)
+        piv.append(int(br.num_pivots.sum()))
+        allopt = allopt and bool((br.status == 0).all())
+    sync()
+    wall = time.perf_counter() - t0
+    kern = sum(kms) * 1e-3
+    if dist is not None:
+        t = torch.tensor([wall, kern], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, kern = float(t[0].item()), float(t[1].item())
+    occ = dlp.batched_occupancy(m, n, local)
+    cus = torch.cuda.get_device_properties(local).multi_processor_count
+    # single-LP serial latency: 256 LPs of the batch, one per CU
+    one = dlp.batched_solve(min(256, nlp), m, n, seed, device=local, log_cap=0)
+    t1 = one.kernel_ms * 1e-3 / max(int(one.num_pivots.max()), 1)
+    resident = min(nlp, occ["lps_per_cu"] * cus)
+    peak = resident / t1   # pivots/s with every resident LP at the single-LP latency
+    achieved = piv[-1] * args.steps / kern
+    pivots_lp = piv[-1] / nlp
+    if rank == 0:
+        total = C5["nlp"] * args.steps
+        bytes_solve = 16.0 * C5["nlp"] * (m + 1) * (m + n + 1)   # one read + one write of every tableau
+        line = {
+            "metric": "batched simplex: LPs/s (C5, 4096 independent 64x128 fp64 LPs, one workgroup per LP)",
+            "value": total / kern, "unit": "LPs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * kern / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (device-generated splitmix64 dense LPs, seeds 5000..9095)",
+            "config": {"workload": f"C5: {C5['nlp']} x ({m} x {n}) dense LPs, seed {C5['seed']} + k",
+                       "parallelism": f"batch split over {world} GPU(s)",
+                       "step": "one dlp_batched_solve of the whole batch",
+                       "residency": ("register-resident: one lane per column slot, the slot's 65 rows in "
+                                     "VGPRs (BASELINE.json says 'tableau held in LDS'; the LDS-resident kernel "
+                                     "is DLP_BATCH_LDS=1, bit-identical, slower: DESIGN.md §6)")
+                       if occ["register_kernel"] else "LDS-resident (one workgroup's LDS holds the tableau)"},
+            "all_optimal": allopt, "pivots_per_solve": piv[-1], "pivots_per_lp": pivots_lp,
+            "wall_lps_per_s": total / wall,
+            "occupancy": dict(occ, cus=cus, resident_lps=resident),
+            "roofline": {"bound": "latency", "unit": "pivots/s", "achieved": achieved, "peak": peak,
+                         "frac": achieved / peak,
+                         "model": ("peak = resident LPs (VGPR/LDS occupancy) / single-LP pivot latency; "
+                                   "single-LP latency from 256 LPs one per CU"),
+                         "single_lp_us_per_pivot": t1 * 1e6,
+                         "batch_us_per_pivot_per_lp": resident / achieved * 1e6,
+                         "hbm_frac": bytes_solve / (kern / args.steps) / 1e9 / HBM_PEAK_GBS,
+                         "fp64_frac": (2.0 * piv[-1] * (m + 1) * (m + n + 1) / (kern / args.steps) / 1e12
+                                       / FP64_PEAK_TFS)},
+            "cpu_baseline": None if (world > 1 or args.no_cpu_baseline) else c5_cpu_baseline(args.cpu_seconds),
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload == "c5":
+        return c5_main(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", "0"))

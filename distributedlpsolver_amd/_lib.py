@@ -185,6 +185,10 @@ SIGNATURES = [
     ("dlp_result_info", C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     ("dlp_result_pivot_log", C.c_int, [_P, C.POINTER(Pivot), _I64, C.POINTER(_I64)]),
     ("dlp_result_timings", C.c_int, [_P, _DP]),
+    ("dlp_result_exchange", C.c_int, [_P, C.POINTER(C.c_int), C.c_char_p, C.c_int64]),
+    ("dlp_release_cached_memory", C.c_int, [C.c_int, C.POINTER(C.c_int64)]),
+    ("dlp_batched_occupancy", C.c_int, [C.c_int64, C.c_int64, C.c_int, C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("dlp_result_free", None, [_P]),
     ("dlp_batched_solve", C.c_int,
      [C.c_int, _I64, _I64, _I64, C.c_uint64, C.POINTER(Options), _DP, C.POINTER(_I32),

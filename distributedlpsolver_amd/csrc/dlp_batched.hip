@@ -635,6 +635,48 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         }                                                                            \
     } while (0)
 
+// The kernel dlp_batched_solve runs for an m x n batch, its lanes per LP and how many LPs one
+// CU holds at once (the occupancy query with its VGPR / LDS footprint): C5's bound is per-pivot
+// serial latency x this residency (bench.py --workload c5).
+extern "C" int dlp_batched_occupancy(int64_t m, int64_t n, int device, int32_t* lps_per_cu,
+                                     int32_t* threads_per_lp, int32_t* register_kernel) {
+    if (m <= 0 || n <= 0) return DLP_ERR_ARG;
+    const size_t lds = sizeof(double) * ((m + 1) * (n + 1) + (m + 1) + (n + 1)) + sizeof(int32_t) * (n + m + 8) +
+                       sizeof(double) * 2 + 16;
+    static const bool force_lds = std::getenv("DLP_BATCH_LDS") && std::atoi(std::getenv("DLP_BATCH_LDS")) == 1;
+    const int nw = (int)((n + 63) / 64);
+    const bool reg = !force_lds && m == 64 && nw >= 1 && nw <= 3;
+    if (!reg && lds > 160 * 1024) return DLP_ERR_UNSUPPORTED;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        dlp::set_error("no HIP device visible (libdlp has no CPU fallback)");
+        return DLP_ERR_NODEVICE;
+    }
+    if (hipSetDevice(device) != hipSuccess) return DLP_ERR_HIP;
+    int nb = 0, threads = 0;
+    hipError_t e;
+    if (reg) {
+        threads = 64 * nw;
+        e = nw == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dlp::batched_reg_kernel<64, 1>, threads, 0)
+          : nw == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dlp::batched_reg_kernel<64, 2>, threads, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dlp::batched_reg_kernel<64, 3>, threads, 0);
+    } else {
+        threads = lds > 40 * 1024 ? 512 : 256;
+        e = hipFuncSetAttribute((const void*)dlp::batched_solve_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dlp::batched_solve_kernel, threads, lds);
+    }
+    if (e != hipSuccess) {
+        dlp::set_error(std::string("dlp_batched_occupancy: ") + hipGetErrorString(e));
+        return DLP_ERR_HIP;
+    }
+    if (lps_per_cu) *lps_per_cu = nb;
+    if (threads_per_lp) *threads_per_lp = threads;
+    if (register_kernel) *register_kernel = reg ? 1 : 0;
+    return DLP_OK;
+}
+
 extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, uint64_t seed,
                                  const dlp_options* opt, double* objective, int32_t* status,
                                  int64_t* npivots, int32_t* basis, dlp_pivot* logs,

@@ -84,4 +84,6 @@ struct dlp_result {
     std::vector<int32_t> basis;
     std::vector<dlp_pivot> log;
     double timings[DLP_NUM_PHASES] = {0, 0, 0, 0};
+    int exchange = DLP_XCHG_DEFAULT;   // dlp_solve(n_gpus): the exchange the result came from
+    std::string exchange_reason;       // why not the peer exchange ("" when it was, or not a solve)
 };

@@ -239,8 +239,11 @@ void release_stream(int device, int prio, hipStream_t s) {
 // teardown and ~0.2 ms in the allocations (DLP_TRACE_CREATE, profiles/r03g/).  Freed buffers of at
 // most kBufPoolMax bytes go to a per-device pool keyed by their power-of-two size class (at most
 // kBufPoolTotal bytes and kBufPoolCount entries cached); a session takes an exact class match.
-// Tableaus and other large buffers are never pooled.  Contents are not cleared: every buffer is
-// initialised by the session before it is read, as a fresh hipMalloc's would have to be.
+// Buffers above kBufPoolMax (the tableau of every streaming LP) are never pooled; a small LP's
+// tableau is.  Contents are not cleared: every buffer is initialised by the session before it
+// is read, as a fresh hipMalloc's would have to be.  When an allocation fails, the device's
+// cached buffers are freed and it is retried (pool_alloc); dlp_release_cached_memory empties
+// the pool explicitly, and pool_bytes lets the free-memory checks count cached bytes as free.
 constexpr size_t kBufPoolMax = (size_t)32 << 20;     // (the default pivot log: 1 M x 32 B)
 constexpr size_t kBufPoolTotal = (size_t)512 << 20;
 constexpr size_t kBufPoolCount = 256;
@@ -259,6 +262,45 @@ size_t size_class(size_t bytes) {
     return c;
 }
 
+// Free every cached buffer of `device` (-1: pinned host memory; kAllDevices: every entry);
+// returns the bytes freed.
+constexpr int kAllDevices = -2;
+size_t pool_drain(int device) {
+    std::vector<PooledBuf> out;
+    {
+        std::lock_guard<std::mutex> lk(g_buf_mu);
+        for (size_t k = g_buf_pool.size(); k-- > 0;)
+            if (device == kAllDevices || g_buf_pool[k].device == device) {
+                out.push_back(g_buf_pool[k]);
+                g_buf_total -= g_buf_pool[k].cls;
+                g_buf_pool.erase(g_buf_pool.begin() + (ptrdiff_t)k);
+            }
+    }
+    size_t freed = 0;
+    for (const auto& b : out) {
+        if (b.device < 0) {
+            (void)hipHostFree(b.p);
+        } else {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(b.device);
+            (void)hipFree(b.p);
+            (void)hipSetDevice(cur);
+        }
+        freed += b.cls;
+    }
+    return freed;
+}
+
+// Device bytes the pool holds for `device` (free memory as far as a session is concerned).
+size_t pool_bytes(int device) {
+    std::lock_guard<std::mutex> lk(g_buf_mu);
+    size_t n = 0;
+    for (const auto& b : g_buf_pool)
+        if (b.device == device) n += b.cls;
+    return n;
+}
+
 // device < 0: pinned host memory (hipHostMallocDefault)
 hipError_t pool_alloc(dlp_session* s, int device, void** p, size_t bytes) {
     const size_t cls = size_class(bytes);
@@ -274,15 +316,24 @@ hipError_t pool_alloc(dlp_session* s, int device, void** p, size_t bytes) {
             }
     }
     const bool pool = cls <= kBufPoolMax;
-    const hipError_t e = device < 0 ? hipHostMalloc(p, pool ? cls : bytes, hipHostMallocDefault)
-                                    : hipMalloc(p, pool ? cls : bytes);
+    auto alloc = [&]() {
+        return device < 0 ? hipHostMalloc(p, pool ? cls : bytes, hipHostMallocDefault)
+                          : hipMalloc(p, pool ? cls : bytes);
+    };
+    hipError_t e = alloc();
+    if (e != hipSuccess && pool_drain(device) > 0) {   // cached buffers of this device hold memory
+        (void)hipGetLastError();
+        e = alloc();
+    }
     if (e == hipSuccess && pool) s->pooled.push_back({*p, cls});
     return e;
 }
 
 // Free p (a session buffer): back to the pool when it came from it and the session is healthy.
-int g_pool_freed = 0;   // DLP_TRACE_CREATE: buffers the last teardown freed instead of pooling
-std::string g_pool_freed_why;
+// DLP_TRACE_CREATE: buffers the calling thread's last teardown freed instead of pooling (per
+// thread: sessions may be freed from several threads at once)
+thread_local int g_pool_freed = 0;
+thread_local std::string g_pool_freed_why;
 void pool_release(dlp_session* s, int device, void* p) {
     if (!p) return;
     size_t cls = 0;
@@ -577,8 +628,10 @@ int la_enable(dlp_session* s, bool forced) {
               !s->general && !s->cluster && (!host_driven || forced) && s->opt.timing < 2;
     const size_t tbytes = (size_t)(s->rows + 1) * s->ld * sizeof(double);
     size_t freeb = 0, totalb = 0;
-    if (ok && hipMemGetInfo(&freeb, &totalb) == hipSuccess)
+    if (ok && hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
+        freeb += pool_bytes(s->device);   // cached by earlier sessions: released on demand (pool_alloc)
         ok = (s->Tb[1] ? freeb + tbytes : freeb) > tbytes + tbytes / 8 + ((size_t)1 << 30);
+    }
     else
         ok = false;
     if (!ok) return DLP_OK;
@@ -1662,7 +1715,11 @@ int merge_result(dlp_session* const* ss, int P, dlp_result* r) {
 // leave a rank waiting), one host thread per device creating, running and
 // reading its rank ("single process, one host thread per
 // device").  The ranks advance in lockstep through the collectives.
-int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_result** out) {
+// One attempt; *used_peer says whether the ranks ran on the peer exchange, *xwhy why the auto
+// exchange did not (set-up).
+int solve_in_process_once(const dlp_problem* prob, const dlp_options& o, int P, dlp_result** out,
+                          bool* used_peer, std::string* xwhy_out) {
+    *used_peer = false;
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (o.device < 0 || o.device + P > ndev) {
@@ -1728,11 +1785,17 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
     std::string xwhy;
     if (res == DLP_OK && (o.exchange == DLP_XCHG_PEER || o.exchange == DLP_XCHG_DEFAULT)) {
         res = dlp_sessions_connect(ss.data(), P);
-        if (res != DLP_OK && o.exchange == DLP_XCHG_DEFAULT) {
+        // only "these devices cannot connect" falls back; a HIP error, OOM or a failure after
+        // some ranks installed their peer tables is returned
+        if (res == DLP_ERR_UNSUPPORTED && o.exchange == DLP_XCHG_DEFAULT) {
             xwhy = dlp_last_error();
             res = DLP_OK;
             for (dlp_session* s : ss) s->xmode = dlp_session::X_RCCL;
         }
+    }
+    if (res == DLP_OK) {
+        *used_peer = ss[0]->xmode == dlp_session::X_PEER;
+        *xwhy_out = xwhy;
     }
     if (res == DLP_OK)
         res = on_ranks([&](int r) {
@@ -1744,6 +1807,8 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
         res = on_ranks([&](int r) {
             if (const char* e = std::getenv("DLP_TEST_FAIL_RANK"))   // tests: fail this rank's 2nd poll
                 if (std::atoi(e) == r) ss[r]->fault_after_polls = 1;
+            if (const char* e = std::getenv("DLP_TEST_FAIL_PEER_RANK"))   // the same, on the peer exchange only
+                if (std::atoi(e) == r && ss[r]->xmode == dlp_session::X_PEER) ss[r]->fault_after_polls = 1;
             int64_t done = 0;
             return dlp_session_run(ss[r], o.max_pivots, &done);
         });
@@ -1754,6 +1819,8 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
             res = DLP_ERR_OOM;
         } else {
             res = merge_result(ss.data(), P, r);
+            r->exchange = *used_peer ? DLP_XCHG_PEER : DLP_XCHG_RCCL;
+            r->exchange_reason = xwhy;
             if (res == DLP_OK)
                 *out = r;
             else
@@ -1777,6 +1844,29 @@ int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_r
     for (auto c : comms)
         if (c) (void)ncclCommDestroy(c);
     return res;
+}
+
+// dlp_solve(n_gpus = P).  With the auto exchange, a solve whose run fails on the peer exchange
+// (a device wait that never completes, a fault in a cross-device store) is rerun from the start
+// over RCCL on fresh sessions, as bench.py's measure_with_fallback does: the peer
+// path's cross-device stores have run only on one-GPU boxes so far.  The result records the
+// exchange that produced it and why (dlp_result_exchange).
+int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_result** out) {
+    bool peer = false;
+    std::string why;
+    const int rc = solve_in_process_once(prob, o, P, out, &peer, &why);
+    if (rc == DLP_OK || !peer || o.exchange != DLP_XCHG_DEFAULT || rc == DLP_ERR_ARG || rc == DLP_ERR_NODEVICE)
+        return rc;
+    const std::string first = dlp_last_error();
+    dlp_options o2 = o;
+    o2.exchange = DLP_XCHG_RCCL;
+    const int rc2 = solve_in_process_once(prob, o2, P, out, &peer, &why);
+    if (rc2 != DLP_OK) {
+        set_error("peer exchange run failed (" + first + "), and the RCCL rerun: " + dlp_last_error());
+        return rc2;
+    }
+    (*out)->exchange_reason = "peer exchange failed during the run: " + first;
+    return DLP_OK;
 }
 
 // ---- peer exchange set-up ------------------------------------
@@ -2684,8 +2774,12 @@ int dlp_sessions_connect(dlp_session* const* ranks, int nranks) {
             }
             HIP_TRY(hipSetDevice(a->device));
             const hipError_t e = hipDeviceEnablePeerAccess(b->device, 0);
-            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_TRY(e);
             (void)hipGetLastError();
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                set_error("hipDeviceEnablePeerAccess(" + std::to_string(a->device) + " -> " +
+                          std::to_string(b->device) + "): " + hipGetErrorString(e));
+                return DLP_ERR_UNSUPPORTED;
+            }
         }
     std::vector<uint64_t*> bases(nranks);
     for (int r = 0; r < nranks; ++r) bases[r] = by[r]->xblk;
@@ -3026,6 +3120,17 @@ int dlp_result_pivot_log(const dlp_result* r, dlp_pivot* log, int64_t cap, int64
 int dlp_result_timings(const dlp_result* r, double* ms_out) {
     if (!r || !ms_out) return DLP_ERR_ARG;
     for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) ms_out[ph] = r->timings[ph];
+    return DLP_OK;
+}
+int dlp_release_cached_memory(int device, int64_t* bytes) {
+    const size_t n = pool_drain(device < 0 ? kAllDevices : device);
+    if (bytes) *bytes = (int64_t)n;
+    return DLP_OK;
+}
+int dlp_result_exchange(const dlp_result* r, int* mode, char* reason, int64_t cap) {
+    if (!r) return DLP_ERR_ARG;
+    if (mode) *mode = r->exchange;
+    if (reason && cap > 0) std::snprintf(reason, (size_t)cap, "%s", r->exchange_reason.c_str());
     return DLP_OK;
 }
 void dlp_result_free(dlp_result* r) { delete r; }

@@ -166,6 +166,8 @@ class Result:
     pivot_log: np.ndarray
     timings_ms: np.ndarray = field(default_factory=lambda: np.zeros(4))
     phase1_pivots: int = 0
+    exchange: int = 0            # dlp_solve(n_gpus): L.XCHG_PEER / L.XCHG_RCCL (0 otherwise)
+    exchange_reason: str = ""    # why not the peer exchange (dlp_result_exchange)
 
     @property
     def status_name(self) -> str:
@@ -192,9 +194,12 @@ def _result_from_handle(h: C.c_void_p, m: int, n: int) -> Result:
                                              C.byref(cnt)), "dlp_result_pivot_log")
         tm = np.zeros(L.NUM_PHASES)
         L.check(lib.dlp_result_timings(h, _dptr(tm)), "dlp_result_timings")
+        xm, xr = C.c_int(), C.create_string_buffer(512)
+        L.check(lib.dlp_result_exchange(h, C.byref(xm), xr, 512), "dlp_result_exchange")
         return Result(status=lib.dlp_result_status(h), objective=lib.dlp_result_objective(h),
                       num_pivots=lib.dlp_result_num_pivots(h), x=x, y=y, basis=basis,
-                      pivot_log=log, timings_ms=tm, phase1_pivots=p1.value)
+                      pivot_log=log, timings_ms=tm, phase1_pivots=p1.value, exchange=xm.value,
+                      exchange_reason=xr.value.decode())
     finally:
         lib.dlp_result_free(h)
 
@@ -468,6 +473,14 @@ def batched_solve(nlp: int, m: int, n: int, seed: int, degenerate: bool = False,
     return BatchResult(obj, st, npv, basis, logs, ms.value)
 
 
+def batched_occupancy(m: int, n: int, device: int = 0) -> dict:
+    """dlp_batched_occupancy: the batch kernel's lanes per LP and LPs resident per CU."""
+    a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
+    L.check(L.lib().dlp_batched_occupancy(m, n, device, C.byref(a), C.byref(b), C.byref(c)),
+            "dlp_batched_occupancy")
+    return {"lps_per_cu": a.value, "threads_per_lp": b.value, "register_kernel": bool(c.value)}
+
+
 MW_ITER_DTYPE = np.dtype([("dual_value", "<f8"), ("max_infeasibility", "<f8"),
                           ("infeasible_advertiser", "<i4"), ("search_levels", "<i4"), ("min_weight", "<f8"),
                           ("max_weight", "<f8"), ("weighted_budget", "<f8")])
@@ -546,6 +559,14 @@ def tableau_ld(m: int, n: int) -> int:
 def device_count() -> int:
     n = C.c_int()
     L.check(L.lib().dlp_device_count(C.byref(n)), "dlp_device_count")
+    return n.value
+
+
+def release_cached_memory(device: int = -1) -> int:
+    """Free the buffers finished sessions left in the per-process cache (-1: every device);
+    returns the bytes freed (dlp_release_cached_memory)."""
+    n = C.c_int64()
+    L.check(L.lib().dlp_release_cached_memory(int(device), C.byref(n)), "dlp_release_cached_memory")
     return n.value
 
 

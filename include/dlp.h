@@ -166,7 +166,10 @@ typedef struct dlp_options {
                                 open, agreed by all ranks), else RCCL (the reason:
                                 dlp_session_exchange_reason); DLP_XCHG_RCCL = RCCL candidate
                                 all-gather + pivot-row MAX all-reduce; DLP_XCHG_PEER = owner-
-                                rooted peer stores, an error when the ranks cannot connect */
+                                rooted peer stores, an error when the ranks cannot connect.
+                                dlp_solve(n_gpus) with DLP_XCHG_DEFAULT: a run that fails on the
+                                peer exchange is rerun from the start over RCCL
+                                (dlp_result_exchange reports it) */
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
  * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;
@@ -183,6 +186,11 @@ int         dlp_rank_rows(int64_t m, int rank, int nranks, int64_t* first, int64
 int         dlp_candidate_select(const dlp_candidate* cands, int n, int* winner);
 int64_t     dlp_tableau_ld(int64_t m, int64_t n);   /* roundup(N+1,16); sessions may pad more */
 int         dlp_update_variants(void);               /* number of rank-1 update variants */
+/* Sessions return their small buffers (<= 32 MiB each, <= 512 MiB in all) and streams to a
+ * per-process cache for the next session.  This frees the cached buffers of `device`
+ * (-1: every device and the pinned host buffers); *bytes (may be NULL) = bytes freed.  An
+ * allocation that fails frees its device's cached buffers and retries by itself. */
+int         dlp_release_cached_memory(int device, int64_t* bytes);
 
 /* ---- problems ------------------------------------------------------------ */
 /* Dense LP: A is m x n row-major; inputs are copied. Requires b >= 0. */
@@ -378,7 +386,8 @@ int dlp_sessions_run(dlp_session* const* ranks, int nranks, int64_t max_pivots, 
  * failure (the session is then unusable; free it).  A device error returns DLP_ERR_HIP.
  * Each peer-exchange wait on the device is bounded by the same timeout + 5 s.
  * dlp_solve(n_gpus = N) aborts every rank's exchange when one rank fails and returns
- * that rank's error.  dlp_session_abort may be called from any thread.
+ * that rank's error (with the auto exchange, after a failed peer run, the error of the
+ * RCCL rerun).  dlp_session_abort may be called from any thread.
  * dlp_session_inject_fault (tests): the (after_polls+1)-th window wait fails as if the
  * exchange had died.
  * Freeing connected ranks: a rank's exchange block receives its peers' stores, so a
@@ -415,6 +424,11 @@ int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, uint64_t seed
                       const dlp_options* opt, double* objective, int32_t* status,
                       int64_t* npivots, int32_t* basis, dlp_pivot* logs, int64_t log_cap,
                       double* kernel_ms);
+/* The batch kernel dlp_batched_solve runs for m x n LPs on `device`: lanes per LP, LPs one CU
+ * holds at once (VGPR / LDS occupancy) and whether it is the register-resident kernel (m = 64,
+ * n <= 192) or the LDS one.  C5 is bound by per-pivot serial latency x this residency. */
+int dlp_batched_occupancy(int64_t m, int64_t n, int device, int32_t* lps_per_cu,
+                          int32_t* threads_per_lp, int32_t* register_kernel);
 
 /* ---- multiplicative-weights path ------------------
  * The reference's own epsilon-approximate MW loop (R/allocation_mw.cpp:271-326,
@@ -470,6 +484,11 @@ int dlp_result_basis(const dlp_result* r, int32_t* basis, int64_t m /* = m_basis
 int dlp_result_info(const dlp_result* r, int64_t* m_basis, int64_t* phase1_pivots);
 int dlp_result_pivot_log(const dlp_result* r, dlp_pivot* log, int64_t cap, int64_t* count);
 int dlp_result_timings(const dlp_result* r, double* ms_out /* DLP_NUM_PHASES */);
+/* dlp_solve(n_gpus >= 1) only: the exchange the result came from (DLP_XCHG_PEER or
+ * DLP_XCHG_RCCL; DLP_XCHG_DEFAULT for every other result) and, into reason (cap bytes, NUL
+ * terminated), why it is not the peer exchange: the auto exchange could not connect the
+ * devices, or the peer run failed and the solve was rerun from the start over RCCL. */
+int dlp_result_exchange(const dlp_result* r, int* mode, char* reason, int64_t cap);
 void dlp_result_free(dlp_result* r);
 
 #ifdef __cplusplus

@@ -21,6 +21,9 @@ for the GPU to reproduce.  Run in the build container (CPU only):
       in row order; plus the log prefix and basis digests at each stop.
   c5  every LP of the C5 batches (4,096 x 64x128 and 4,096 x 64x64, seed 5000): per-field
       digests of status, pivot count, objective bits, basis and the first 64 log entries.
+  rank_split  bench.py's c3r4 LP (8192 x 57344 seed 34) split over 2 processes of
+      4,096 rows (the per-process rank path, tests/test_gpu_ranks.py): per-rank block
+      digests, objective row, log and basis at 136 / 200 / 264 pivots.
 
 The digests hash little-endian fp64 / int32 bytes of the oracle's outputs
 (tests/oracle_py.py), so the GPU side compares bit for bit."""
@@ -95,6 +98,30 @@ def c3_tableau(stops=(136, 160, C3_K64_PIVOTS, C3_K64_PIVOTS + 256)):
     return out
 
 
+def rank_split(m=8192, n=57344, seed=34, P=2, stops=(136, 200, 264)):
+    """The per-process rank path of a scaling run: bench.py's c3r4 LP
+    (8192 x 57344 seed 34) row-partitioned over P = 2 processes, so that each rank holds
+    4,096 x 65,537 — exactly one rank of C3's 8-GPU split.  At each stop: the log and
+    basis digests, the objective bits, and one sha256 per rank's row block (rows
+    [floor(r m / P), floor((r+1) m / P)), each row its first `width` doubles) plus one of
+    the objective row, so every process can check its own block without the others'."""
+    t0 = time.time()
+    w = ((n + m + 1) + 15) // 16 * 16
+    out = {"m": m, "n": n, "seed": seed, "P": P, "width": w, "stops": {}}
+    cuts = [r * m // P for r in range(P + 1)]
+
+    def at(k, T, log, basis):
+        out["stops"][str(k)] = {
+            "log_sha256": sha(log), "basis_sha256": sha(basis),
+            "objective_hex": float(log[-1]["objective"]).hex(),
+            "block_sha256": [tableau_sha(T[cuts[r]:cuts[r + 1]], w) for r in range(P)],
+            "objective_row_sha256": sha(T[m, :w]), "oracle_seconds": time.time() - t0}
+        print(k, out["stops"][str(k)], flush=True)
+
+    O.run_generated_stops(m, n, seed, list(stops), at, nthreads=os.cpu_count() or 8)
+    return out
+
+
 C5_SHAPES = [(64, 64), (64, 128)]
 
 
@@ -143,7 +170,7 @@ def main():
             d = json.load(f)
     for w in which:
         d[w] = {"c2": c2, "c3": c3, "c3_k64": lambda: c3(C3_K64_PIVOTS), "c3_tableau": c3_tableau,
-                "c5": c5}[w]()
+                "c5": c5, "rank_split": rank_split}[w]()
         with open(OUT, "w") as f:
             json.dump(d, f, indent=1)
         print(w, json.dumps(d[w]), flush=True)

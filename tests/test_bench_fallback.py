@@ -35,7 +35,11 @@ class FakeSession:
     def reset_timings(self):
         self.resets += 1
 
+    def abort(self):
+        self.aborted = True
+
     def close(self):
+        assert getattr(self, "aborted", False), "a failed peer session is aborted and drained before close"
         self.closed = True
 
 

@@ -78,3 +78,27 @@ def test_stall_limit():
         with pytest.raises(L.DLPError) as e:
             s.run(4096)
         assert e.value.status == L.ERR_RCCL and "exchange timeout" in str(e.value)
+
+
+@pytest.mark.parametrize("defer", [1, 16])
+def test_n_gpus_peer_run_failure_reruns_over_rccl(defer):
+    """dlp_solve(n_gpus = 1) with the auto exchange: the peer run fails mid-solve
+    (DLP_TEST_FAIL_PEER_RANK injects a failed window wait on the peer exchange only), every
+    rank is drained and freed, and the solve is rerun from the start over RCCL.  The result
+    is bit-exact and says which exchange produced it and why."""
+    A, b, c = O.gen_dense(200, 400, 1)
+    ref = O.solve_dense(A, b, c)
+    clean = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, defer=defer, check_interval=8, small_lp=-1)
+    assert clean.exchange == L.XCHG_PEER and clean.exchange_reason == ""
+    os.environ["DLP_TEST_FAIL_PEER_RANK"] = "0"
+    try:
+        t0 = time.time()
+        res = dlp.solve(dlp.Problem.dense(A, b, c), n_gpus=1, defer=defer, check_interval=8, small_lp=-1)
+        assert time.time() - t0 < 60
+    finally:
+        del os.environ["DLP_TEST_FAIL_PEER_RANK"]
+    assert res.exchange == L.XCHG_RCCL
+    assert "peer exchange failed during the run" in res.exchange_reason and "injected" in res.exchange_reason
+    assert res.status == ref.status and res.num_pivots == ref.num_pivots
+    assert res.pivot_log.tobytes() == ref.pivot_log.tobytes()
+    assert res.x.tobytes() == ref.x.tobytes() and res.y.tobytes() == ref.y.tobytes()

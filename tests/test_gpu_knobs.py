@@ -117,3 +117,4 @@ def test_cluster_workgroup_knob(wg):
     ref = _ref("cluster")
     assert ref["small_lp"]
     assert _run("cluster", env={"DLP_CLUSTER_WG": wg}) == ref
+

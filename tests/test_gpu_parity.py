@@ -289,3 +289,16 @@ def test_retune_mid_solve():
                 break
         res = s.result()
     _check_equal(res, ref)
+
+
+def test_release_cached_memory():
+    """ADVICE r04: finished sessions leave their small buffers in a per-process cache;
+    dlp_release_cached_memory frees them, and a solve afterwards is unaffected."""
+    A, b, c = O.gen_dense(120, 150, 4)
+    ref = O.solve_dense(A, b, c)
+    dlp.release_cached_memory()
+    res = dlp.solve(dlp.Problem.dense(A, b, c), small_lp=-1)
+    assert dlp.release_cached_memory(0) > 0   # that solve's buffers were cached
+    assert dlp.release_cached_memory() == 0
+    res2 = dlp.solve(dlp.Problem.dense(A, b, c), small_lp=-1)
+    assert res.pivot_log.tobytes() == res2.pivot_log.tobytes() == ref.pivot_log.tobytes()

@@ -1,0 +1,151 @@
+"""GPU: the per-process rank path of a scaling run, with a second rank.
+
+`bench.py --gpus N` runs one process per GPU; each is a rank session of a streaming LP
+with the shipped defaults: K = 64, lookahead auto (on once the peer exchange is
+connected), the chain / pass CU split (128 chain CUs at 4,096 local rows), the form-21
+pass with band publication, and the two-launch peer pivot (workgroup 0 of the ratio
+launch and every pivot-row workgroup of a non-owner wait on ANOTHER PROCESS's stores).
+Here two such processes share one MI355X: bench.py's c3r4 LP (8192 x 57344, seed 34) is
+split into 2 x 4,096 rows, so each rank holds 4,096 x 65,537 — exactly one rank of C3's
+8-GPU split.  The exchange blocks are opened through IPC handles gathered over gloo
+(RCCL cannot join two ranks on one device; the RCCL fallback is covered by injection,
+tests/test_gpu_peer.py, tests/test_bench_fallback.py).
+
+Every process checks its own output against the oracle's committed stops
+(tests/golden/make_digests.py rank_split): the pivot log, basis and objective
+(replicated on every rank), its row block's whole-tableau digest and the objective row.
+Reference analog of the split: R/global_problem.cpp:270-274."""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+import distributedlpsolver_amd as dlp
+from distributedlpsolver_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _block_sha(s, width, chunk=512):
+    """sha256 of this rank's constraint rows, first `width` doubles each, in row order
+    (the stream make_digests.tableau_sha hashes for the oracle's row block)."""
+    h = hashlib.sha256()
+    for first in range(0, s.rows, chunk):
+        cnt = min(chunk, s.rows - first)
+        h.update(np.ascontiguousarray(s.read_rows(first, cnt)[:, :width]).tobytes())
+    return h.hexdigest()
+
+
+def _rank_worker(rank, world, port, g, windows, env, q):
+    """One process = one rank session, driven exactly as bench.py drives it (dlp_session_run
+    windows on its own stream), checked against the oracle's stops after each window."""
+    import torch.distributed as dist
+    os.environ.update(env)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {"rank": rank, "checks": {}}
+    s = None
+    try:
+        la = int(env.get("LOOKAHEAD", "-1"))
+        s = dlp.Session(dlp.Problem.random(g["m"], g["n"], g["seed"]), rank=rank, nranks=world,
+                        defer=0, lookahead=la, check_interval=64 * 20, log_pivots=1,
+                        max_pivots=sum(windows) + 2)
+        hs = [None] * world
+        dist.all_gather_object(hs, s.exchange_handle())
+        s.connect_ipc(hs)
+        s.set_exchange_timeout(60.0)
+        out["config"] = {"exchange": s.get_exchange(), "lookahead": s.lookahead(),
+                         "chain_cus": s.chain_cus(), "defer_tuning": s.get_defer_tuning(),
+                         "rows": s.rows, "row_first": s.row_first, "ld": s.ld}
+        dist.barrier()
+        total = 0
+        for w in windows:
+            st, done = s.run(w)
+            total += done
+            out.setdefault("runs", []).append((st, done))
+            want = g["stops"].get(str(total))
+            if want is None:
+                continue
+            res = s.result()
+            got = {"log": _sha(res.pivot_log) == want["log_sha256"],
+                   "basis": _sha(res.basis) == want["basis_sha256"],
+                   "objective": float(res.objective).hex() == want["objective_hex"],
+                   "block": _block_sha(s, g["width"]) == want["block_sha256"][rank],
+                   "objective_row": _sha(s.read_rows(s.rows, 1)[0, :g["width"]]) == want["objective_row_sha256"]}
+            out["checks"][str(total)] = got
+        # no rank frees its exchange block while a peer's kernels may still store into it
+        dist.barrier()
+        s.close()
+        s = None
+    except Exception as e:   # reported to the parent, which fails the test
+        out["error"] = repr(e)
+    finally:
+        q.put(out)
+        if s is not None:
+            s.abort()
+        dist.destroy_process_group()
+
+
+def _run_two(windows, env, timeout=240):
+    import torch.multiprocessing as mp
+    g = load_golden("digests.json")["rank_split"]
+    world = g["P"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, g, windows, env, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted((q.get(timeout=timeout) for _ in procs), key=lambda o: o["rank"])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    for o in out:
+        assert "error" not in o, o
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return g, out
+
+
+@pytest.mark.parametrize("case", ["default", "chain_cus_0", "no_lookahead"])
+def test_two_process_rank_path(case):
+    """default: the shipped auto policy (K = 64, lookahead on with the peer exchange, 128
+    chain CUs, form 21 + band publication, two-launch peer pivot), 136 pivots (two full
+    blocks + 8) then a 64-pivot window that ends inside a block (200), then 64 more (264);
+    chain_cus_0: DLP_CHAIN_CUS=0 (chain and pass unmasked); no_lookahead: lookahead = 0
+    (the form-23 LDS-ring pass in place, what an RCCL rank runs)."""
+    env = {"chain_cus_0": {"DLP_CHAIN_CUS": "0"}, "no_lookahead": {"LOOKAHEAD": "0"}}.get(case, {})
+    windows = [136, 64, 64] if case == "default" else [136]
+    g, out = _run_two(windows, env)
+    for o in out:
+        cfg = o["config"]
+        assert cfg["exchange"] == L.XCHG_PEER
+        assert cfg["rows"] == g["m"] // g["P"] and cfg["row_first"] == o["rank"] * g["m"] // g["P"]
+        assert cfg["defer_tuning"][2] == 64
+        if case == "no_lookahead":
+            assert not cfg["lookahead"] and cfg["defer_tuning"][1] == 23
+        else:
+            assert cfg["lookahead"] and cfg["defer_tuning"][1] == 21
+            assert cfg["chain_cus"] == (0 if case == "chain_cus_0" else 128)
+        assert [d for _, d in o["runs"]] == windows
+        assert set(o["checks"]) == {str(k) for k in np.cumsum(windows)}
+        for k, got in o["checks"].items():
+            assert all(got.values()), (o["rank"], k, got)
