@@ -167,14 +167,15 @@ def cpu_info():
     return model, os.cpu_count() or 1, avail
 
 
-def cpu_baseline(m, n, seed, budget_s):
+def cpu_baseline(m, n, seed, budget_s, K=1):
     """The in-repo C++ oracle (same pivot rule, OpenMP over rows; test
     infrastructure: the CPU comparator only) on the same LP, SURVEY.md §8(d):
     every CPU this process may use (sched_getaffinity, passed to the oracle
     explicitly, not inherited from OMP_NUM_THREADS), then the same LP continued
     on OMP_NUM_THREADS threads (the box's per-GPU CPU share, when set) and on 1
     thread.  `value` is the faster multi-thread run (threads_for_value says
-    which); every run is reported."""
+    which); every run is reported.  With K > 1, `like_for_like` times the GPU's own
+    deferred rank-K algorithm on the host (oracle/oracle_defer.inc) on those threads."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py  # test infrastructure: the CPU comparator only
     model, nproc, avail = cpu_info()
@@ -206,6 +207,22 @@ def cpu_baseline(m, n, seed, budget_s):
     if share:
         out["omp_share"] = {"value": rate[share], "unit": "pivots/s", "cores": share,
                             "pivots": runs[1][1], "seconds": runs[1][0]}
+    if K > 1:
+        # like-for-like: the GPU's own algorithm on the host — the oracle's
+        # deferred rank-K restatement (oracle/oracle_defer.inc: replayed selections, then one
+        # pass per block, bit-identical to eager), same LP, same K, whole blocks only, on the
+        # thread count that gave `value`
+        druns, dgen = oracle_py.bench_windows_defer(m, n, seed, K, [(best, 10 ** 6, budget_s)],
+                                                    gen_threads=avail)
+        dsecs, dk = druns[0]
+        if not (dsecs and dk):
+            raise RuntimeError(f"deferred CPU baseline: {dk} pivots in {dsecs} s (the LP ended inside the sample)")
+        out["like_for_like"] = {
+            "value": dk / dsecs, "unit": "pivots/s", "cores": best, "kind": "port",
+            "algorithm": f"deferred rank-{K} (the GPU's): replayed selections + one pass per {K}-pivot block",
+            "sample": (f"in-repo C++ oracle, oracle/oracle_defer.inc (AVX2 + FMA, OpenMP over row bands), same "
+                       f"LP {m}x{n} seed {seed}: 1 warm-up block, then {dk} pivots = {dk // K} whole blocks "
+                       f"in {dsecs:.2f} s on {best} threads ({where}); generation {dgen:.1f} s not timed")}
     return out
 
 
@@ -623,7 +640,7 @@ def main():
             traffic, traffic_src = None, None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(m, n, seed, args.cpu_seconds)
+            cpu = cpu_baseline(m, n, seed, args.cpu_seconds, K)
         value = timed / elapsed
         line = {
             "metric": ("simplex pivots/s + achieved HBM GB/s (dense fp64 tableau; roofline of the "

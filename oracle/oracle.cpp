@@ -501,3 +501,5 @@ int oracle_bench_windows(int kind, int64_t m, int64_t n, uint64_t seed, int32_t 
 }
 
 }  // extern "C"
+
+#include "oracle_defer.inc"

@@ -235,6 +235,46 @@ def bench_windows(m, n, seed, runs, gen_threads, degenerate=False):
     return [(float(s), int(k)) for s, k in zip(secs, done)], gen.value
 
 
+def bench_windows_defer(m, n, seed, K, runs, gen_threads, degenerate=False):
+    """bench_windows with the deferred rank-K algorithm (oracle/oracle_defer.inc): windows of
+    whole K-pivot blocks, each pass applied.  Returns ([(seconds, pivots), ...], generation s)."""
+    L = lib()
+    if not getattr(L, "_bwd_bound", False):
+        L.oracle_bench_windows_defer.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_uint64, C.c_int32,
+                                                 C.c_int, C.c_int, _I32, _I64, _D, _D, _I64, _D]
+        L._bwd_bound = True
+    thr = np.array([r[0] for r in runs], np.int32)
+    kmax = np.array([r[1] for r in runs], np.int64)
+    bud = np.array([r[2] for r in runs], np.float64)
+    secs = np.zeros(len(runs))
+    done = np.zeros(len(runs), np.int64)
+    gen = C.c_double()
+    rc = L.oracle_bench_windows_defer(1 if degenerate else 0, m, n, seed, gen_threads, K, len(runs),
+                                      thr.ctypes.data_as(_I32), kmax.ctypes.data_as(_I64), _d(bud),
+                                      _d(secs), done.ctypes.data_as(_I64), C.byref(gen))
+    assert rc == 0, f"oracle_bench_windows_defer rc={rc}"
+    return [(float(s), int(k)) for s, k in zip(secs, done)], gen.value
+
+
+def run_generated_defer(m, n, seed, K, k, degenerate=False, nthreads=8):
+    """k pivots of the deferred rank-K restatement on the generated tableau: (log, whole
+    (m+1) x ld tableau after the last pass, basis)."""
+    L = lib()
+    if not getattr(L, "_rgd_bound", False):
+        L.oracle_run_generated_defer.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_uint64, C.c_int,
+                                                 C.c_int64, C.c_int32, C.c_void_p, C.POINTER(C.c_int64),
+                                                 _D, _I32]
+        L._rgd_bound = True
+    log = np.zeros(k, PIVOT_DTYPE)
+    npiv = C.c_int64()
+    T = np.zeros((m + 1, ld(m, n)))
+    basis = np.zeros(m, np.int32)
+    rc = L.oracle_run_generated_defer(1 if degenerate else 0, m, n, seed, K, k, nthreads, log.ctypes.data,
+                                      C.byref(npiv), _d(T), basis.ctypes.data_as(_I32))
+    assert rc == 0, f"oracle_run_generated_defer rc={rc}"
+    return log[:npiv.value], T, basis
+
+
 def mw_scale(epsilon=0.01):
     """R/main.cpp:38 cr_transition_scale = 1 - epsilon * 0.001 in x87 long double, to fp64."""
     return float(np.longdouble(1) - np.longdouble(epsilon) * np.longdouble(0.001))

@@ -18,6 +18,14 @@ def test_cpu_baseline_small():
     assert cb["cpu_model"] and cb["nproc"] >= 1 and cb["cpus_usable"] >= 1
 
 
+def test_cpu_baseline_like_for_like():
+    """The deferred rank-K leg (the GPU's algorithm on the host): whole blocks, labelled."""
+    cb = bench.cpu_baseline(1500, 1500, 3, 0.2, K=16)
+    lf = cb["like_for_like"]
+    assert lf["unit"] == "pivots/s" and lf["value"] > 0 and lf["cores"] == cb["cores"]
+    assert "deferred rank-16" in lf["algorithm"]
+
+
 def test_committed_traffic_unknown_geometry():
     val, src = bench.committed_traffic({"workload": "none", "kernel": "pass", "K": -1})
     assert val is None and src is None

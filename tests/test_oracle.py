@@ -188,3 +188,26 @@ def test_c5_batch_digests_reproduce():
     assert sha(np.asarray(obj, np.float64)) == g["objective_sha256"]
     assert sha(np.asarray(basis, np.int32)) == g["basis_sha256"]
     assert h.hexdigest() == g["log64_sha256"]
+
+
+@pytest.mark.parametrize("m,n,seed,K,k,degen", [(150, 170, 4, 16, 10 ** 6, False), (150, 170, 4, 64, 10 ** 6, False),
+                                                (96, 128, 6, 7, 10 ** 6, True), (300, 420, 11, 64, 200, False),
+                                                (300, 420, 11, 1, 77, False)])
+def test_deferred_oracle_equals_eager(m, n, seed, K, k, degen):
+    """oracle/oracle_defer.inc (the GPU's deferred rank-K algorithm on the CPU, bench.py's
+    like-for-like CPU baseline) against the eager oracle: pivot log, basis and the whole
+    tableau byte for byte, for full solves (optimal inside a block) and windows that end
+    inside a block (the last partial block's pass applied)."""
+    lg_d, T_d, b_d = O.run_generated_defer(m, n, seed, K, k, degenerate=degen, nthreads=4)
+    rows = np.arange(m + 1, dtype=np.int64)
+    lg_e, T_e, b_e = O.run_generated(m, n, seed, k, rows, degenerate=degen, nthreads=4)
+    assert len(lg_d) == len(lg_e) > 0
+    assert np.ascontiguousarray(lg_d).tobytes() == np.ascontiguousarray(lg_e).tobytes()
+    assert b_d.tobytes() == b_e.tobytes()
+    assert T_d.tobytes() == T_e.tobytes()
+
+
+def test_deferred_oracle_bench_windows():
+    """The like-for-like CPU baseline's windows: whole blocks, every one applied."""
+    runs, gen = O.bench_windows_defer(400, 600, 11, 16, [(2, 64, 30.0), (1, 32, 30.0)], gen_threads=2)
+    assert runs[0][1] == 64 and runs[1][1] == 32 and all(s > 0 for s, _ in runs) and gen > 0
