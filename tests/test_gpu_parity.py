@@ -298,7 +298,9 @@ def test_release_cached_memory():
     ref = O.solve_dense(A, b, c)
     dlp.release_cached_memory()
     res = dlp.solve(dlp.Problem.dense(A, b, c), small_lp=-1)
-    assert dlp.release_cached_memory(0) > 0   # that solve's buffers were cached
+    assert dlp.release_cached_memory(0) > 0   # that solve's device buffers were cached
+    assert dlp.release_cached_memory(0) == 0
+    dlp.release_cached_memory()               # + the pinned host buffers
     assert dlp.release_cached_memory() == 0
     res2 = dlp.solve(dlp.Problem.dense(A, b, c), small_lp=-1)
     assert res.pivot_log.tobytes() == res2.pivot_log.tobytes() == ref.pivot_log.tobytes()
