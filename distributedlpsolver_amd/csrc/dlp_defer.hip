@@ -2203,6 +2203,10 @@ __global__ __launch_bounds__(64) void seal_kernel(DevState* st, int slot, uint32
 }  // namespace
 
 int ratio_defer_blocks(const Geometry& g) {
+    return (int)((g.rows + 1 + g.rthreads - 1) / g.rthreads);
+}
+// the fused single-rank pivot and the one-launch peer pivot keep 256-lane ratio workgroups
+static int ratio_blocks_256(const Geometry& g) {
     return (int)((g.rows + 1 + kRatioDeferThreads - 1) / kRatioDeferThreads);
 }
 
@@ -2221,8 +2225,9 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     const double* Ccp = prev_seal >= 0 ? prev->Cc : nullptr;
     const double* Pp = prev_seal >= 0 ? prev->P : nullptr;
     const int steps = prev_seal >= 0 ? 2 * d.K : d.K;   // at most kp + j replayed steps
+    if (g.rthreads != 64 && g.rthreads != 128 && g.rthreads != 256) return hipErrorInvalidValue;
 #define DLP_RATIO_DEFER(KM)                                                                      \
-    ratio_defer_kernel<KM><<<nblocks, kRatioDeferThreads, 0, s>>>(                               \
+    ratio_defer_kernel<KM><<<nblocks, g.rthreads, 0, s>>>(                               \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, \
         d.Cc, d.ldcc, d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing,   \
         log, log_cap, Ccp, Pp, prev_seal, xp, xseq, xfuse ? 1 : 0)
@@ -2238,7 +2243,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     {
         static const int lch = std::getenv("DLP_LEAN_LCH") ? std::atoi(std::getenv("DLP_LEAN_LCH")) : 0;
 #define DLP_RATIO_LEAN(L, DYN)                                                                             \
-    ratio_lean_kernel<128, L><<<nblocks, kRatioDeferThreads, DYN, s>>>(                                       \
+    ratio_lean_kernel<128, L><<<nblocks, g.rthreads, DYN, s>>>(                                       \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
         d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
         xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,   \
@@ -2249,7 +2254,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
         else if (lch == 4)
             DLP_RATIO_LEAN(4, 0);
         else
-            DLP_RATIO_LEAN(0, ratio_ring_bytes(kRatioRingPairs));
+            DLP_RATIO_LEAN(0, ratio_ring_bytes(kRatioRingPairs) / (kRatioDeferThreads / g.rthreads));
 #undef DLP_RATIO_LEAN
     }
 #undef DLP_RATIO_DEFER
@@ -2261,8 +2266,8 @@ hipError_t launch_pivot_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
                               hipStream_t s) {
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
-    if (nblocks < ratio_defer_blocks(g)) return hipErrorInvalidValue;   // partials too small
-    const int nrat = ratio_defer_blocks(g);
+    if (nblocks < ratio_blocks_256(g)) return hipErrorInvalidValue;   // partials too small
+    const int nrat = ratio_blocks_256(g);
     const int nprow = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     // every block resident at once (the pivot-row blocks wait on the ratio blocks): the
     // caller keeps the grid within 2 blocks per CU (fused_pivot_fits); K <= 32
@@ -2283,7 +2288,7 @@ hipError_t launch_pivot_defer(const Geometry& g, const Defer& d, int32_t* basis,
 }
 
 int fused_pivot_blocks(const Geometry& g) {
-    return ratio_defer_blocks(g) + (int)((g.ld + kDeferTile - 1) / kDeferTile);
+    return ratio_blocks_256(g) + (int)((g.ld + kDeferTile - 1) / kDeferTile);
 }
 
 // How many workgroups of the fused pivot kernel (the instance launch_pivot_defer picks for K)
@@ -2339,7 +2344,7 @@ hipError_t launch_pivot_x(const Geometry& g, const Defer& d, int32_t* basis, Pri
                           double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
                           hipStream_t s, const Defer* prev, int prev_seal, const XPeers* xp, uint32_t seq,
                           const BandPub* bp) {
-    if (!xp) return hipErrorInvalidValue;
+    if (!xp || g.rthreads != kRatioDeferThreads) return hipErrorInvalidValue;   // 256-lane ratio blocks
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     const int nrat = ratio_defer_blocks(g);

@@ -180,6 +180,8 @@ struct Geometry {
                           // carried Phase II objective row, when present, is local row rows-1)
     int ntiles;           // ceil(ld / kUpdTile)
     int rows_per_block;   // update kernel
+    int rthreads = kRatioDeferThreads;   // deferred ratio workgroup (64 / 128 / 256 lanes; the
+                                         // session's ratio_threads_policy, fixed at creation)
 };
 
 // Update-kernel variants (tuning): 0 U4/2dbl/scalar-colq (default), 1 U8, 2 U4/LDS-colq,

@@ -576,6 +576,19 @@ int flush_pending_block(dlp_session* s);
 // best n moves: c3r4 128 (20.6 k), c3r2 64 (13.9-14.3 k), c3r8 128 (profiles/r04ah/).  Auto: 128
 // CUs for the chain up to 8,192 local rows, 64 below 32,768, at most half the CUs, 0 (no masks)
 // from 32,768; DLP_CHAIN_CUS=n overrides (0 = off).
+// Lanes per deferred ratio workgroup (one lane per row; the replay's coefficient chain streams
+// through each wave's LDS-DMA ring, whose rate is per CU): fixed at creation, since the peer
+// exchange's candidate slots are one per ratio workgroup of every rank (xslots), identical on
+// every rank.  DLP_RATIO_THREADS=64/128/256 overrides.
+int ratio_threads_policy(const dlp_session* s) {
+    (void)s;
+    if (const char* e = std::getenv("DLP_RATIO_THREADS")) {
+        const int n = std::atoi(e);
+        if (n == 64 || n == 128 || n == 256) return n;
+    }
+    return dlp::kRatioDeferThreads;
+}
+
 int chain_cus_policy(const dlp_session* s) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 64)
@@ -784,6 +797,7 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     g.ncols = s->N;
     g.nprice = s->nprice;
     g.rows_elig = rows_elig;
+    g.rthreads = ratio_threads_policy(s);
     if (opt->update_variant < 0 || opt->update_variant >= dlp::update_variants()) {
         set_error("update_variant out of range");
         return DLP_ERR_ARG;
@@ -1109,13 +1123,19 @@ int flush_pending_block(dlp_session* s) {
 // a streaming tableau), where every per-pivot kernel fits beside the form-21 pass (the LEAN ratio
 // and pivot-row launches, with the selection and the commit inside: <= 32 VGPRs,
 // tests/test_isa.py).  Measured on the C3 rank geometries at P = 8 / 4 / 2 (c3r8 / c3r4 / c3r2):
-// 23,012 vs 21,358, 17,098 vs 15,881, 11,980 vs 10,183 pivots/s (profiles/r04g/).  Off with RCCL,
-// whose collective kernels need more registers than the pass leaves on a CU and would each wait
-// for pass workgroups to drain.  A caller's explicit lookahead setting is kept.
+// 23,012 vs 21,358, 17,098 vs 15,881, 11,980 vs 10,183 pivots/s (profiles/r04g/).  With RCCL only
+// where the chain gets CUs of its own (chain_cus_policy > 0: a rank of up to 32k rows): RCCL's
+// collective kernels need more registers than the pass leaves on a CU and would each wait for pass
+// workgroups to drain, but on a disjoint CU mask they never share a CU with the pass
+// (round 5; profiles/r05*/).  A caller's explicit lookahead setting is kept.
 int la_policy(dlp_session* s) {
     if (!s->la_auto || !s->exchange) return DLP_OK;
-    const bool want = s->xmode == dlp_session::X_PEER && s->d.K == 64 && s->streaming && !s->general;
+    const bool rccl_split = s->xmode == dlp_session::X_RCCL && chain_cus_policy(s) > 0;
+    const bool want = (s->xmode == dlp_session::X_PEER || rccl_split) && s->d.K == 64 && s->streaming &&
+                      !s->general;
     if (want && !s->la) CALL_TRY(la_enable(s, false));
+    // RCCL beside the pass only on a CU split that really exists (a masked queue may be refused)
+    if (s->la && s->xmode == dlp_session::X_RCCL && s->chain_cus == 0) CALL_TRY(la_disable(s));
     if (!want && s->la) CALL_TRY(la_disable(s));
     pick_form(s);
     return DLP_OK;
@@ -1173,7 +1193,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         // selection, the selection record to the pivot-row workgroups, row push, commit).  Bit-exact,
         // but 1-3 % slower than two launches at the C3 rank geometries: the record's hand-off and its
         // ~130 pollers cost what the launch boundary did (profiles/r04i/, r04j/)
-        if (xf && peer_onelaunch()) {
+        if (xf && peer_onelaunch() && s->g.rthreads == dlp::kRatioDeferThreads) {
             s->xseq_c += 1;
             s->xseq_r += 1;   // (equal: every pivot, drive-out and carry step advances both)
             HIP_TRY(dlp::launch_pivot_x(gsel, *dcur, s->basis, s->pp, s->st, o.tol_dj, o.tol_piv, o.pricing, s->log,
@@ -1194,7 +1214,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     }
     if (phase == 1) {
         if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) return DLP_OK;
-        if (xf && peer_onelaunch()) {   // (the whole pivot ran in phase 0's launch)
+        if (xf && peer_onelaunch() && s->g.rthreads == dlp::kRatioDeferThreads) {   // (the whole pivot ran in phase 0's launch)
             if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
             return DLP_OK;
         }
@@ -1880,7 +1900,7 @@ int xslots(const dlp_session* s, dlp::XPeers* x) {
         int64_t first = 0, count = 0;
         (void)dlp_rank_rows(s->m, r, s->nranks, &first, &count);
         if (carry && r == s->nranks - 1) count += 1;
-        const int nrat = (int)((count + 1 + dlp::kRatioDeferThreads - 1) / dlp::kRatioDeferThreads);
+        const int nrat = (int)((count + 1 + s->g.rthreads - 1) / s->g.rthreads);
         x->nrat[r] = nrat;
         nslot = std::max(nslot, nrat);
     }

@@ -125,14 +125,16 @@ def _run_two(windows, env, timeout=240):
     return g, out
 
 
-@pytest.mark.parametrize("case", ["default", "chain_cus_0", "no_lookahead"])
+@pytest.mark.parametrize("case", ["default", "chain_cus_0", "no_lookahead", "ratio64"])
 def test_two_process_rank_path(case):
     """default: the shipped auto policy (K = 64, lookahead on with the peer exchange, 128
     chain CUs, form 21 + band publication, two-launch peer pivot), 136 pivots (two full
     blocks + 8) then a 64-pivot window that ends inside a block (200), then 64 more (264);
     chain_cus_0: DLP_CHAIN_CUS=0 (chain and pass unmasked); no_lookahead: lookahead = 0
-    (the form-23 LDS-ring pass in place, what an RCCL rank runs)."""
-    env = {"chain_cus_0": {"DLP_CHAIN_CUS": "0"}, "no_lookahead": {"LOOKAHEAD": "0"}}.get(case, {})
+    (the form-23 LDS-ring pass in place); ratio64: 64-lane ratio workgroups (65 candidate slots
+    per rank in the peer exchange instead of 17)."""
+    env = {"chain_cus_0": {"DLP_CHAIN_CUS": "0"}, "no_lookahead": {"LOOKAHEAD": "0"},
+           "ratio64": {"DLP_RATIO_THREADS": "64"}}.get(case, {})
     windows = [136, 64, 64] if case == "default" else [136]
     g, out = _run_two(windows, env)
     for o in out:
@@ -149,3 +151,40 @@ def test_two_process_rank_path(case):
         assert set(o["checks"]) == {str(k) for k in np.cumsum(windows)}
         for k, got in o["checks"].items():
             assert all(got.values()), (o["rank"], k, got)
+
+
+def _split_sha(s, width, cut, chunk=512):
+    """Digests of rows [0, cut) and [cut, rows) of a one-session tableau: the two rank blocks of
+    the rank_split stops."""
+    out = []
+    for a, b in ((0, cut), (cut, s.rows)):
+        h = hashlib.sha256()
+        for first in range(a, b, chunk):
+            cnt = min(chunk, b - first)
+            h.update(np.ascontiguousarray(s.read_rows(first, cnt)[:, :width]).tobytes())
+        out.append(h.hexdigest())
+    return out
+
+
+def test_rccl_rank_session_lookahead_on_cu_split():
+    """an RCCL-exchange rank session keeps lookahead when the chain has CUs of its
+    own (the collectives never share a CU with the pass): the rank_split LP as one 1-rank RCCL
+    session (8,192 rows: 128 chain CUs, form 23 on the rest), 136 + 64 pivots against the
+    oracle's stops (both row blocks, objective row, log, basis)."""
+    g = load_golden("digests.json")["rank_split"]
+    with dlp.Session(dlp.Problem.random(g["m"], g["n"], g["seed"]), rank=0, nranks=1,
+                     rccl_id=dlp.comm_unique_id(), exchange=L.XCHG_RCCL, defer=0, check_interval=64 * 20,
+                     max_pivots=300) as s:
+        assert s.get_exchange() == L.XCHG_RCCL
+        assert s.lookahead() and s.chain_cus() == 128 and s.get_defer_tuning()[1:] == (23, 64)
+        total = 0
+        for w in (136, 64):
+            st, done = s.run(w)
+            total += done
+            want = g["stops"][str(total)]
+            res = s.result()
+            assert _sha(res.pivot_log) == want["log_sha256"]
+            assert _sha(res.basis) == want["basis_sha256"]
+            assert float(res.objective).hex() == want["objective_hex"]
+            assert _split_sha(s, g["width"], g["m"] // 2) == want["block_sha256"]
+            assert _sha(s.read_rows(s.rows, 1)[0, :g["width"]]) == want["objective_row_sha256"]

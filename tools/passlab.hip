@@ -1279,8 +1279,8 @@ void launch_mpass3(const Lab& L, int, int rb, hipStream_t s) {
 // linear double 128 q + 2 L, so the source is the (row, column) that position means in the
 // padded layout); A fragment of lane (r, q) at kblock b = -As[r][4 b + q].  Coefficient
 // staging and T tiles one group ahead (register ring of 2), NT 16-column tiles per wave.
-template <int K, int NT>
-__global__ __launch_bounds__(256, 2) void mpass4_kernel(const double* __restrict__ T, double* __restrict__ To,
+template <int K, int NT, int WPE = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void mpass4_kernel(const double* __restrict__ T, double* __restrict__ To,
                                                        int64_t ld, int64_t rows, int64_t width,
                                                        const double* __restrict__ Cr, const double* __restrict__ P,
                                                        int rb) {
@@ -1367,10 +1367,10 @@ __global__ __launch_bounds__(256, 2) void mpass4_kernel(const double* __restrict
         }
     }
 }
-template <int K, int NT>
+template <int K, int NT, int W = 2>
 void launch_mpass4(const Lab& L, int, int rb, hipStream_t s) {
     dim3 grid((unsigned)((L.width + 64 * NT - 1) / (64 * NT)), (unsigned)((L.rows + rb - 1) / rb));
-    mpass4_kernel<K, NT><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
+    mpass4_kernel<K, NT, W><<<grid, 256, 0, s>>>(L.T, L.To, L.ld, L.rows, L.width, L.Cr, L.P, rb);
 }
 
 // ---- f4r: form 21's compute (P[0..64) of one column per lane in VGPRs, 2 rows per
@@ -1577,6 +1577,20 @@ int main(int argc, char** argv) {
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
     const char* only = argc > 4 ? argv[4] : nullptr;
     std::vector<Variant> vs = {
+        // round 5: band counts against the 768 pass slots (257 tiles x 43 / 42 / 48 bands), the
+        // interleaved persistent form on exactly 256 tiles (ncols 65536: G x 256 = 768 slots),
+        // the MFMA pass at 3-4 waves per SIMD
+        {"r5 f4r rb768", 64, 768, launch_f4r<4, 3, 3>, true},
+        {"r5 f4r rb784", 64, 784, launch_f4r<4, 3, 3>, true},
+        {"r5 f4r rb684", 64, 684, launch_f4r<4, 3, 3>, true},
+        {"r5 f4r G3", 64, 768, launch_f4r<4, 3, 3, 0, 3>, true},
+        {"r5 f4r G3 copy", 64, 768, launch_f4r<4, 3, 3, 1, 3>, false},
+        {"r5 f4r G6", 64, 768, launch_f4r<4, 3, 3, 0, 6>, true},
+        {"r5 f4r U2D4 G3", 64, 768, launch_f4r<2, 4, 3, 0, 3>, true},
+        {"r5 mpass4 NT2 w4 rb768", 64, 768, launch_mpass4<64, 2, 4>, true},
+        {"r5 mpass4 NT3 w3 rb768", 64, 768, launch_mpass4<64, 3, 3>, true},
+        {"r5 mpass4 NT4 w2 rb768", 64, 768, launch_mpass4<64, 4, 2>, true},
+        {"r5 mpass4 NT2 w4 rb256", 64, 256, launch_mpass4<64, 2, 4>, true},
         {"f4r K64 U4 D3 w3", 64, 768, launch_f4r<4, 3, 3>, true},
         {"f4r K64 U4 D3 w3 copy", 64, 768, launch_f4r<4, 3, 3, 1>, false},
         {"f4r K64 U4 D3 w3 nnt", 64, 768, launch_f4r<4, 3, 3, 0, 0, false>, true},
