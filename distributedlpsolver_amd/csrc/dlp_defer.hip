@@ -2037,13 +2037,18 @@ __global__ __launch_bounds__(256) void pass_q_kernel(const double* __restrict__ 
 // rows out of place) go through the generic replay afterwards.  Partial blocks run the
 // same code (tails zeroed at block start).
 typedef double d4 __attribute__((ext_vector_type(4)));
-template <bool NT_, int NT>
+// PUB (lookahead, round 5): band publication as form 21's — every output store write-through
+// (sc1, beside nt) through a band buffer resource, every wave drained, then one agent-scope add
+// to the band's count (pass_d_kernel).  The caller keeps rb * ld * 8 < 2^31.
+template <bool NT_, int NT, bool PUB = false>
 __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict__ T, double* __restrict__ Tout,
                                                      int64_t ld, int64_t rows, int64_t width,
                                                      const BlockDesc* __restrict__ bd,
                                                      const double* __restrict__ C, int64_t ldc,
                                                      const double* __restrict__ P,
-                                                     const int32_t* __restrict__ nzc, int rb) {
+                                                     const int32_t* __restrict__ nzc, int rb,
+                                                     uint32_t* bcnt = nullptr) {
+    constexpr int kSt = (NT_ ? 2 : 0) | (PUB ? kAuxSc1 : 0);   // store policy (PUB)
     constexpr int K = 64, KB = K / 4, W = 16 * NT, RS = K + 2;
     constexpr int NPC = (16 * RS + 127) / 128;   // 1 KiB LDS-DMA pieces per group
     // ONE __shared__ object (the coefficient stages, then the row classes): with a second one
@@ -2073,6 +2078,13 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
     const int nr = (int)(iend - i0);
     classify_band(cls, bd, nzc, i0, nr, kb);
     const int ng = (nr + 15) / 16;
+    // PUB: the band's output through one buffer resource (rows at soffset r * ld8; voffset the
+    // column's byte offset)
+    const int ld8 = (int)(ld * 8);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Tout + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
+    (void)ro;
+    (void)ld8;
     auto stage = [&](int g, int buf) {
         const int gg = g < ng ? g : ng - 1;
         for (int pc = w; pc < NPC; pc += 4) {
@@ -2140,22 +2152,27 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
                     for (int i = 0; i < 4; ++i) {
                         const int rl = rl0 + lq + 4 * i;
                         if (rl < nr && cls[rl] == kDense) {
-                            double* q = Tout + (i0 + rl) * ld + col;
-                            if (NT_)
-                                __builtin_nontemporal_store(acc[t][i], q);
-                            else
-                                *q = acc[t][i];
+                            if constexpr (PUB) {
+                                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc[t][i]), ro,
+                                                                      (int)col * 8, rl * ld8, kSt);
+                            } else {
+                                double* q = Tout + (i0 + rl) * ld + col;
+                                if (NT_)
+                                    __builtin_nontemporal_store(acc[t][i], q);
+                                else
+                                    *q = acc[t][i];
+                            }
                         }
                     }
             }
         }
     }
     // everything else, row by row (as pass_s_body's generic replay): the 256 threads as
-    // 2 row halves x the workgroup's 4 W columns
+    // 256 / WC row slices x the workgroup's WC = 4 W columns
     constexpr int WC = 4 * W;
     const int64_t j = cw + (threadIdx.x % WC);
-    if (threadIdx.x >= 2 * WC || j >= width) return;
-    for (int r = threadIdx.x / WC; r < nr; r += 256 / WC) {
+    const bool jok = j < width && threadIdx.x < (256 / WC) * WC;
+    for (int r = threadIdx.x / WC; jok && r < nr; r += 256 / WC) {
         const int cl = cls[r];
         if (cl == kDense || (cl == kUntouched && !outplace)) continue;
         const double* row = T + (i0 + r) * ld;
@@ -2176,7 +2193,15 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
                 if (f != 0.0) t = __builtin_fma(-f, P[(int64_t)l * ld + j], t);
             }
         }
-        Tout[(i0 + r) * ld + j] = t;
+        if constexpr (PUB)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t), ro, (int)j * 8, r * ld8, kSt);
+        else
+            Tout[(i0 + r) * ld + j] = t;
+    }
+    if constexpr (PUB) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 stores are through
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(&bcnt[blockIdx.y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2444,9 +2469,14 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
                 dyn = (size_t)160 * 1024 / occ - stat;
             }
             const dim3 grid((unsigned)((g.width + 127) / 128), (unsigned)((g.rows + rb - 1) / rb));
-            if (g.rows > 0)
-                pass_m_kernel<NT, 2><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc, d.P,
-                                                             d.nzc, rb);
+            if (g.rows > 0) {
+                if (bcnt && (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31))
+                    pass_m_kernel<NT, 2, true><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C,
+                                                                      d.ldc, d.P, d.nzc, rb, bcnt);
+                else
+                    pass_m_kernel<NT, 2><<<grid, 256, dyn, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C, d.ldc,
+                                                                 d.P, d.nzc, rb);
+            }
             if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
             return hipGetLastError();
         }
@@ -2603,9 +2633,14 @@ bool lookahead_form(int form) {
     return form == 3 || form == 4 || form == 5 || form == 20 || form == 21 || form == 22 || form == 23;
 }
 
+// pass workgroups per band of a publishing form: 256-column tiles (21, 23), 128 (22)
+int band_pub_tiles(int form, int64_t width) {
+    return (int)(form == 22 ? (width + 127) / 128 : (width + 255) / 256);
+}
 bool band_pub_ok(const BandPub& bp, const Geometry& g, const Defer& d, int rb) {
-    return (d.form == 21 || d.form == 23) && d.K == 64 && d.ldc == 64 && rb == bp.rb && (g.rows + rb - 1) / rb <= bp.stride &&
-           (int)((g.width + 255) / 256) == bp.ntiles;
+    return (d.form == 21 || d.form == 22 || d.form == 23) && d.K == 64 && d.ldc == 64 && rb == bp.rb &&
+           (g.rows + rb - 1) / rb <= bp.stride && band_pub_tiles(d.form, g.width) == bp.ntiles &&
+           (int64_t)rb * g.ld * 8 < ((int64_t)1 << 31);
 }
 
 hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, bool nontemporal,

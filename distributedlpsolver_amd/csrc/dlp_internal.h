@@ -158,11 +158,12 @@ struct BandPub {
     uint32_t* cnt = nullptr;    // [2][stride]
     int64_t stride = 0;         // >= the pass's bands
     int rb = 0;                 // pass rows per band
-    int ntiles = 0;             // pass workgroups per band (256-column tiles)
+    int ntiles = 0;             // pass workgroups per band (band_pub_tiles)
     const double* Tn = nullptr; // the pass's output buffer (set per pass by the session)
 };
 struct Geometry;
 bool band_pub_ok(const BandPub& bp, const Geometry& g, const struct Defer& d, int rb);
+int band_pub_tiles(int form, int64_t width);
 
 static_assert(offsetof(DevState, pl) - offsetof(DevState, blk) == offsetof(BlockDesc, pl),
               "BlockDesc must alias DevState::blk / pl");

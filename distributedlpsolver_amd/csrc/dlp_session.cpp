@@ -1062,7 +1062,7 @@ dlp::BandPub band_pub(const dlp_session* s) {
     b.cnt = s->band_cnt;
     b.stride = s->band_stride;
     b.rb = s->defer_rb;
-    b.ntiles = (int)((s->g.width + 255) / 256);
+    b.ntiles = dlp::band_pub_tiles(s->d.form, s->g.width);
     b.Tn = s->la_pending ? s->Tb[s->tcur] : nullptr;   // the pass in flight writes Tb[tcur]
     return b;
 }
