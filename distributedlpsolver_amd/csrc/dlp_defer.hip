@@ -34,6 +34,16 @@ namespace {
 
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+// A double's bits as the b64 buffer-store operand, built from scalars: hipcc miscompiles a
+// __builtin_bit_cast of an element of an ext_vector value (tests/test_isa.py source guard).
+__device__ __forceinline__ u2v dbits(double v) {
+    uint64_t u;
+    __builtin_memcpy(&u, &v, sizeof(u));
+    u2v w;
+    w.x = (unsigned)u;
+    w.y = (unsigned)(u >> 32);
+    return w;
+}
 
 template <bool NT>
 __device__ inline d2 ldv(const double* p) {
@@ -2078,8 +2088,8 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
     const int nr = (int)(iend - i0);
     classify_band(cls, bd, nzc, i0, nr, kb);
     const int ng = (nr + 15) / 16;
-    // PUB: the band's output through one buffer resource (rows at soffset r * ld8; voffset the
-    // column's byte offset)
+    // PUB: the band's output through one buffer resource (byte offsets column * 8 + row * ld8;
+    // the caller keeps rb * ld * 8 < 2^31)
     const int ld8 = (int)(ld * 8);
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Tout + i0 * ld), (short)0, (int)((int64_t)nr * ld * 8), 0x00020000);
@@ -2152,9 +2162,11 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
                     for (int i = 0; i < 4; ++i) {
                         const int rl = rl0 + lq + 4 * i;
                         if (rl < nr && cls[rl] == kDense) {
-                            if constexpr (PUB) {
-                                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc[t][i]), ro,
-                                                                      (int)col * 8, rl * ld8, kSt);
+                            if constexpr (PUB) {   // (per-lane row: in the VGPR offset, not the SGPR one)
+                                const double v = acc[t][i];
+                                __builtin_amdgcn_raw_buffer_store_b64(dbits(v), ro,
+                                                                      (int)col * 8 + (lq + 4 * i) * ld8, rl0 * ld8,
+                                                                      kSt);
                             } else {
                                 double* q = Tout + (i0 + rl) * ld + col;
                                 if (NT_)
@@ -2193,8 +2205,8 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
                 if (f != 0.0) t = __builtin_fma(-f, P[(int64_t)l * ld + j], t);
             }
         }
-        if constexpr (PUB)
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t), ro, (int)j * 8, r * ld8, kSt);
+        if constexpr (PUB)   // (r differs between the lanes: VGPR offset)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, t), ro, (int)j * 8 + r * ld8, 0, kSt);
         else
             Tout[(i0 + r) * ld + j] = t;
     }

@@ -71,7 +71,7 @@ def _ref(kind, *args):
 @pytest.mark.parametrize("env", [{"DLP_LEAN_LCH": "4"}, {"DLP_LEAN_LCH": "8"}, {"DLP_BAND_PUB": "0"},
                                  {"DLP_CHAIN_CUS": "0"}, {"DLP_CHAIN_CUS": "32"}, {"DLP_CHAIN_CUS": "200"},
                                  {"DLP_FAT_PROW": "0"}, {"DLP_RATIO_THREADS": "64"},
-                                 {"DLP_RATIO_THREADS": "128"}])
+                                 {"DLP_RATIO_THREADS": "128"}, {"DLP_RATIO_THREADS": "256"}])
 def test_lookahead_chain_knobs(env):
     ref = _ref("defer", 1)
     # 4,096 rows: the chain on 128 CUs, the pass on the other 128 (chain_cus_policy)
@@ -102,7 +102,7 @@ def test_cu_split_falls_back_to_unmasked_streams():
     assert got == {k: v for k, v in ref.items() if k not in ("form", "chain_cus")}
 
 
-@pytest.mark.parametrize("n", ["64", "128"])
+@pytest.mark.parametrize("n", ["64", "128", "256"])
 def test_ratio_threads_without_lookahead(n):
     """Smaller deferred ratio workgroups (more of them, one lane per row) on the non-lookahead path."""
     assert _run("defer", [0], {"DLP_RATIO_THREADS": n}) == _ref("defer", 0)

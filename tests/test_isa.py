@@ -192,8 +192,9 @@ def test_peer_row_push_is_drained():
 
 def test_no_bit_cast_of_a_vector_element_in_kernels():
     """Source guard for the same compiler behaviour: no __builtin_bit_cast of a .x/.y/.z/.w
-    element or a subscripted element of an ext_vector value in the kernel sources."""
-    pat = re.compile(r"__builtin_bit_cast\(\s*\w+\s*,\s*[\w\[\]]+\.[xyzw]\s*\)")
+    element or a subscripted element of an ext_vector value in the kernel sources (round 5: a
+    doubly subscripted operand, acc[t][i] of a d4 array, is caught too; dbits() is the form to use)."""
+    pat = re.compile(r"__builtin_bit_cast\(\s*\w+\s*,\s*([\w\[\]]+\.[xyzw]|\w+\[[^\]]+\]\[[^\]]+\])\s*\)")
     csrc = os.path.join(ROOT, "distributedlpsolver_amd", "csrc")
     for f in sorted(os.listdir(csrc)):
         if f.endswith((".hip", ".h")):

@@ -3,7 +3,7 @@
 # the lookahead + form tests, then C3 alternating: form 21 (default) vs form 22, and 128-lane ratio workgroups
 set -o pipefail
 O=gpurun_out/r05e; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_lookahead.py "tests/test_gpu_defer.py::test_pass_form21_dpp_full_blocks" "tests/test_gpu_defer.py::test_pass_form21_sparse_and_degenerate" -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo FAIL tests; tail -40 $O/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_lookahead.py "tests/test_gpu_defer.py::test_pass_form21_dpp_full_blocks" "tests/test_gpu_defer.py::test_pass_form21_sparse_and_degenerate" tests/test_gpu_ranks.py "tests/test_gpu_knobs.py::test_lookahead_chain_knobs" tests/test_gpu_knobs.py::test_ratio_threads_without_lookahead -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo FAIL tests; tail -40 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
 run() {  # tag args/env...
 timeout -k 10 300 env "${@:3}" python -u bench.py --no-cpu-baseline --no-eager-window --no-pivot-window $2 > $O/c3_$1.json 2> $O/c3_$1.err || { echo FAIL $1; tail -20 $O/c3_$1.err; exit 1; }
