@@ -140,7 +140,7 @@ __device__ int g_chain_stamps_on;
 // (RP = kRatioRingPairs: 16 measured equal at C3, 8,239-8,267 vs 8,262-8,263 pivots/s, profiles/r04c/)
 constexpr int kRatioRingPairs = 8;
 constexpr size_t ratio_ring_bytes(int rp) { return (size_t)(kRatioDeferThreads / 64) * rp * 128 * sizeof(double); }
-template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4, int RP = kRatioRingPairs>
+template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4, int RP = kRatioRingPairs, bool DB = false>
 __device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
@@ -187,7 +187,7 @@ __device__ __forceinline__ void ratio_defer_body(
     // band publication (RING): the wave's 64 rows final in Tn (their bands of the sealed
     // block's pass are done): start there and replay this block's steps only
     bool wdone = false;
-    if constexpr (RING)
+    if constexpr (LEAN)
         if (bcnt && kp > 0 && i0 + 63 < rows) {
             const int64_t b0 = i0 / brb, b1 = (i0 + 63) / brb;
             const uint32_t c0 = __hip_atomic_load(&bcnt[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -287,9 +287,11 @@ __device__ __forceinline__ void ratio_defer_body(
         }
         if (blockIdx.x == 0) CHAIN_STAMP(slot, 3);
     } else if constexpr (LEAN) {
-        // LCH coefficient loads per round trip (the register budget of this kernel)
-        if (i < rows)
-            for (int l0 = 0; l0 < J; l0 += LCH) {
+        // LCH coefficient loads per round trip (the register budget of this kernel), from the
+        // first step not applied to the row's source (L0: a published band starts after the
+        // sealed block); the next chunk's loads are issued before this chunk is applied
+        if (i < rows && J > L0 && !DB) {   // one chunk at a time (LEAN's 32 VGPRs)
+            for (int l0 = L0; l0 < J; l0 += LCH) {
                 double fq[LCH];
 #pragma unroll
                 for (int u = 0; u < LCH; ++u) fq[u] = l0 + u < J ? fld(l0 + u) : 0.0;
@@ -306,6 +308,37 @@ __device__ __forceinline__ void ratio_defer_body(
                     }
                 }
             }
+        } else if (i < rows && J > L0) {   // DB (MID): double-buffered
+            double fa[LCH], fb[LCH];
+            auto fetch = [&](double (&fq)[LCH], int l0) {
+#pragma unroll
+                for (int u = 0; u < LCH; ++u) fq[u] = l0 + u < J ? fld(l0 + u) : 0.0;
+            };
+            auto apply = [&](const double (&fq)[LCH], int l0) {
+#pragma unroll
+                for (int u = 0; u < LCH; ++u) {
+                    const int l = l0 + u;
+                    const double fv = fq[u];
+                    if (l < J) {
+                        if (i == s_pl[l])
+                            a = s_pq[l];
+                        else if (fv != 0.0)
+                            a = __builtin_fma(-fv, s_pq[l], a);
+                        flast = fv;
+                    }
+                }
+            };
+            fetch(fa, L0);
+            for (int l0 = L0; l0 < J; l0 += 2 * LCH) {
+                if (l0 + LCH < J) fetch(fb, l0 + LCH);
+                apply(fa, l0);
+                if (l0 + LCH >= J) break;
+                if (l0 + 2 * LCH < J) fetch(fa, l0 + 2 * LCH);
+                apply(fb, l0 + LCH);
+            }
+        } else if (i < rows && J > 0 && L0 == J) {
+            flast = Ccp[(int64_t)(kp - 1) * ldcc + i];   // nothing replayed: the RHS cache's step
+        }
         if (blockIdx.x == 0) CHAIN_STAMP(slot, 3);
     }
     if (i <= rows) {
@@ -446,6 +479,24 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
                                   xp, xseq, nullptr, 1, 0, nullptr, xsel);
 }
 
+// MID (round 5): beside the MFMA pass (form 22 leaves 104 VGPRs per SIMD), the replay's
+// coefficients in registers, LCH per round trip, double-buffered, no LDS ring.
+template <int KMAX, int LCH>
+__global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(104))) void ratio_mid_kernel(
+    const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
+    int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
+    DevState* st, double* __restrict__ C, int64_t ldc, double* __restrict__ Cc, int64_t ldcc,
+    const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
+    Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
+    dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
+    int prev_seal, const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn,
+    int xsel) {
+    ratio_defer_body<KMAX, false, true, LCH, kRatioRingPairs, true>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
+                                             ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
+                                             tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
+                                             xp, xseq, bcnt, brb, bnt, Tn, xsel);
+}
+
 // The LEAN selection kernel, held to 32 VGPRs (lookahead at K = 64, beside the pass).
 template <int KMAX, int LCH, int RP = kRatioRingPairs>
 __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(32))) void ratio_lean_kernel(
@@ -505,7 +556,7 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
 // other rank INT64_MIN for the int64 MAX exchange.
 constexpr int kProwRingSteps = 8;   // (RS: 16 measured equal, with the ratio ring's 16)
 constexpr size_t prow_ring_bytes(int rs) { return (size_t)4 * rs * 128 * sizeof(double); }
-template <bool LEAN, int RS = kProwRingSteps>
+template <bool LEAN, int RS = kProwRingSteps, int CHR = 16>
 __device__ __forceinline__ void prow_defer_body(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
@@ -621,7 +672,7 @@ __device__ __forceinline__ void prow_defer_body(
         // chunks of CH pivot rows (row index clamped), double-buffered: the next chunk's loads are
         // issued before this chunk is applied, so up to 2 CH rows are in flight (c3r8: the replay
         // was 7 us per pivot with one chunk of 8 in flight, profiles/r04e/)
-        constexpr int CH = 16;
+        constexpr int CH = CHR;
         d2 pa[CH], pb[CH];
         auto fetch = [&](d2 (&pv)[CH], int l0) {
 #pragma unroll
@@ -725,6 +776,12 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(DLP_PROW_ARGS) {
 template <int RS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void prow_lean_kernel(DLP_PROW_ARGS) {
     prow_defer_body<true, RS>(DLP_PROW_PASS);
+}
+// MID (round 5): beside the MFMA pass (form 22: 3 waves x 136 VGPRs per SIMD leave 104), the
+// register replay of the fat kernel with 2 x 8 pivot rows in flight instead of 2 x 16, and no
+// LDS ring (the MFMA pass stages its coefficients through LDS).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(104))) void prow_mid_kernel(DLP_PROW_ARGS) {
+    prow_defer_body<false, kProwRingSteps, 8>(DLP_PROW_PASS);
 }
 #undef DLP_PROW_ARGS
 #undef DLP_PROW_PASS
@@ -2279,6 +2336,15 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     else   // lookahead at K = 64, beside the form-21 pass
     {
         static const int lch = std::getenv("DLP_LEAN_LCH") ? std::atoi(std::getenv("DLP_LEAN_LCH")) : 0;
+        static const int mid_env = std::getenv("DLP_MID_CHAIN") ? std::atoi(std::getenv("DLP_MID_CHAIN")) : -1;
+        if (mid_env >= 0 ? mid_env == 1 : d.form == 22) {   // beside the MFMA pass: registers, no ring
+            ratio_mid_kernel<128, 16><<<nblocks, g.rthreads, 0, s>>>(
+                g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc,
+                d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp,
+                prev_seal, xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1,
+                pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xfuse ? 1 : 0);
+            return hipGetLastError();
+        }
 #define DLP_RATIO_LEAN(L, DYN)                                                                             \
     ratio_lean_kernel<128, L><<<nblocks, g.rthreads, DYN, s>>>(                                       \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
@@ -2351,7 +2417,16 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
     const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
     static const int fat_env = std::getenv("DLP_FAT_PROW") ? std::atoi(std::getenv("DLP_FAT_PROW")) : -1;
     const bool fat = fat_env >= 0 ? fat_env == 1 : own_cus;
-    if (prev_seal >= 0 && d.K > 32 && fat) {
+    static const int mid_env = std::getenv("DLP_MID_CHAIN") ? std::atoi(std::getenv("DLP_MID_CHAIN")) : -1;
+    const bool mid = !fat && (mid_env >= 0 ? mid_env == 1 : d.form == 22);
+    if (prev_seal >= 0 && d.K > 32 && mid) {
+        // beside the MFMA pass (form 22 leaves 104 VGPRs per SIMD): the register replay, 2 x 8 rows
+        prow_mid_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits,
+                                              pp, tol_dj, log, log_cap, nranks == 1 ? 1 : 0, prev->C, prev->P,
+                                              prev_seal, nranks == 1 ? nullptr : xp, xseq,
+                                              pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1,
+                                              pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xc);
+    } else if (prev_seal >= 0 && d.K > 32 && fat) {
         // lookahead with the chain on CUs of its own (no pass waves beside it): the register
         // kernel, 2 x 16 pivot rows in flight, with band publication
         prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits,

@@ -142,6 +142,8 @@ def test_lookahead_kernels_fit_beside_the_form21_pass():
         return max(hits)
     assert one("pass_d_kernel") <= 160, c
     assert one("pass_m_kernel") <= 160, c   # form 22 beside the chain (round 5: publishing)
+    # its chain kernels: 3 form-22 waves (<= 136 allocated VGPRs each) leave 104 per SIMD
+    assert one("ratio_mid_kernel") <= 104 and one("prow_mid_kernel") <= 104, c
     assert one("ratio_lean_kernel") <= 32   # every instance (ring depths 8 / 16, LCH 4 / 8)
     assert one("prow_lean_kernel") <= 32
     assert one("pivot_x_lean_kernel") <= 32   # the one-launch peer pivot beside the pass
