@@ -1747,6 +1747,71 @@ int main(int argc, char** argv) {
             }
         return 0;
     }
+    if (only && !strcmp(only, "hetero")) {
+        // round 5: the VALU (DPP, f4r) and the matrix-core (mpass4) passes side by side on every CU,
+        // each on a share of the columns, as two concurrent launches whose occupancy is held by
+        // dynamic LDS (f4r nw WGs per CU, mpass4 nm per CU): both pipes busy at once
+        hipStream_t sa, sb;
+        CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+        CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+        hipEvent_t a0, a1, b1;
+        CK(hipEventCreate(&a0));
+        CK(hipEventCreate(&a1));
+        CK(hipEventCreate(&b1));
+        const int rb = 768;
+        struct H { double frac; int nw, nm; };
+        for (const H h : {H{0.0, 0, 3}, H{1.0, 3, 0}, H{0.25, 1, 2}, H{0.33, 1, 2}, H{0.4, 1, 2}, H{0.5, 1, 2},
+                          H{0.33, 1, 3}, H{0.5, 2, 1}})
+        for (int rep2 = 0; rep2 < 1; ++rep2) {
+            const int64_t wa = (int64_t)(L.width * h.frac / 256.0 + 0.5) * 256;   // f4r's columns
+            Lab La = L, Lb = L;
+            La.width = wa;
+            Lb.T = L.T + wa;
+            Lb.To = L.To + wa;
+            Lb.P = L.P + wa;
+            Lb.width = L.width - wa;
+            // mpass4 WG = 18 KiB static + 2 KiB dynamic = 20 KiB; f4r takes the rest, nw per CU
+            const size_t dynb = (h.nm && h.nw) ? 2048 : 0;
+            const size_t dyna = h.nw ? (size_t)(163840 - h.nm * 20480 - 1024) / h.nw : 0;
+            auto go = [&]() {
+                if (wa > 0) {
+                    dim3 grid((unsigned)((La.width + 255) / 256), (unsigned)((La.rows + rb - 1) / rb));
+                    f4r_kernel<true, 4, 3, 3><<<grid, 256, std::max(dyna, (size_t)4 * 3 * 1024 * 4), sa>>>(
+                        La.T, La.To, La.ld, La.rows, La.width, La.Cr, La.P, rb);
+                }
+                if (Lb.width > 0) {
+                    dim3 grid((unsigned)((Lb.width + 127) / 128), (unsigned)((Lb.rows + rb - 1) / rb));
+                    mpass4_kernel<64, 2, 3><<<grid, 256, dynb, sb>>>(Lb.T, Lb.To, Lb.ld, Lb.rows, Lb.width, Lb.Cr,
+                                                                     Lb.P, rb);
+                }
+            };
+            go();
+            CK(hipDeviceSynchronize());
+            std::vector<float> ms(reps);
+            for (int r = 0; r < reps; ++r) {
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(a0, 0));
+                CK(hipStreamWaitEvent(sa, a0, 0));
+                CK(hipStreamWaitEvent(sb, a0, 0));
+                go();
+                CK(hipEventRecord(a1, sa));
+                CK(hipEventRecord(b1, sb));
+                CK(hipStreamWaitEvent(0, a1, 0));
+                CK(hipStreamWaitEvent(0, b1, 0));
+                hipEvent_t e2;
+                CK(hipEventCreate(&e2));
+                CK(hipEventRecord(e2, 0));
+                CK(hipEventSynchronize(e2));
+                CK(hipEventElapsedTime(&ms[r], a0, e2));
+                CK(hipEventDestroy(e2));
+            }
+            std::sort(ms.begin(), ms.end());
+            printf("hetero f4r share %.2f (%ld cols, %d WG/CU, dyn %zu) + mpass4 (%d WG/CU, dyn %zu): median %.3f ms  %6.0f GB/s\n",
+                   h.frac, (long)wa, h.nw, dyna, h.nm, dynb, ms[reps / 2], bytes / ms[reps / 2] / 1e6);
+            fflush(stdout);
+        }
+        return 0;
+    }
     if (only && !strcmp(only, "copyw")) {
         struct C { int nth, rb; };
         std::vector<C> cs;

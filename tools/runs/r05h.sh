@@ -16,5 +16,5 @@ for r in a b; do
 run c3 f21$r "" X=0 && run c3 f22mid$r "--form 22" X=0 && run c3 f22lean$r "--form 22" DLP_MID_CHAIN=0 || exit 1
 done
 for r in a b; do
-run c3r8 def$r "" X=0 && run c3r8 f22$r "--form 22" X=0 && run c3r8 cus160$r "" DLP_CHAIN_CUS=160 && run c3r8 cus192$r "" DLP_CHAIN_CUS=192 && run c3r4 def$r "" X=0 && run c3r4 f22$r "--form 22" X=0 || exit 1
+run c3r8 def$r "" X=0 && run c3r8 f22$r "--form 22" X=0 && run c3r8 cus160$r "" DLP_CHAIN_CUS=160 && run c3r8 cus192$r "" DLP_CHAIN_CUS=192 && run c3r8 mid$r "" DLP_MID_CHAIN=1 && run c3r4 def$r "" X=0 && run c3r4 f22$r "--form 22" X=0 || exit 1
 done
