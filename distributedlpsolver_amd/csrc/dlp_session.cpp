@@ -560,22 +560,6 @@ void pick_form(dlp_session* s) {
 
 int flush_pending_block(dlp_session* s);
 
-// Lookahead on (DESIGN.md §13): a second tableau buffer holding the same bytes, a second set of
-// block arrays (rhs shared), band counters, the pass stream.  Called at session creation or
-// between runs (la_policy): a pending block is applied first.  Silently stays off where it does
-// not apply (the form has no out-of-place pass, general LPs, the small-LP launch, per-phase
-// timing, a host-driven rank unless forced, too little free memory).
-// The lookahead's CU split.  Beside the pass, the selection chain of a rank-sized tableau is the
-// longer of the two and runs 2-3x slower than alone, its waves sharing every CU with three pass
-// waves.  On disjoint CU masks (chain on the top n mask bits, the pass on the rest) the block
-// balances: measured on the rank geometries with the form-21 pass (profiles/r04x/, alternating
-// runs), c3r8 (4,096 rows) n = 128: 24.3-24.5 k vs 22.65 k pivots/s; c3r4 (8,192) n = 80-96:
-// 19.9-20.0 k vs 17.0-17.1 k; c3r2 (16,384) n = 48-64: 12.5-12.6 k vs 11.97 k; C3 (32,768 rows,
-// pass-bound) loses with any split (form 21 n = 32: 7.63 k, form 23 n = 32: 8.05 k vs 8.22 k
-// unmasked on one box, profiles/r04ai/).  With the form-23 pass on the split (pick_form) the
-// best n moves: c3r4 128 (20.6 k), c3r2 64 (13.9-14.3 k), c3r8 128 (profiles/r04ah/).  Auto: 128
-// CUs for the chain up to 8,192 local rows, 64 below 32,768, at most half the CUs, 0 (no masks)
-// from 32,768; DLP_CHAIN_CUS=n overrides (0 = off).
 // Lanes per deferred ratio workgroup (one lane per row; the replay's coefficient chain streams
 // through each wave's LDS-DMA ring, whose rate is per CU): fixed at creation, since the peer
 // exchange's candidate slots are one per ratio workgroup of every rank (xslots), identical on
@@ -593,6 +577,22 @@ int ratio_threads_policy(const dlp_session* s) {
     return streaming && per_rank <= 8192 ? 128 : dlp::kRatioDeferThreads;
 }
 
+// Lookahead on (DESIGN.md §13): a second tableau buffer holding the same bytes, a second set of
+// block arrays (rhs shared), band counters, the pass stream.  Called at session creation or
+// between runs (la_policy): a pending block is applied first.  Silently stays off where it does
+// not apply (the form has no out-of-place pass, general LPs, the small-LP launch, per-phase
+// timing, a host-driven rank unless forced, too little free memory).
+// The lookahead's CU split.  Beside the pass, the selection chain of a rank-sized tableau is the
+// longer of the two and runs 2-3x slower than alone, its waves sharing every CU with three pass
+// waves.  On disjoint CU masks (chain on the top n mask bits, the pass on the rest) the block
+// balances: measured on the rank geometries with the form-21 pass (profiles/r04x/, alternating
+// runs), c3r8 (4,096 rows) n = 128: 24.3-24.5 k vs 22.65 k pivots/s; c3r4 (8,192) n = 80-96:
+// 19.9-20.0 k vs 17.0-17.1 k; c3r2 (16,384) n = 48-64: 12.5-12.6 k vs 11.97 k; C3 (32,768 rows,
+// pass-bound) loses with any split (form 21 n = 32: 7.63 k, form 23 n = 32: 8.05 k vs 8.22 k
+// unmasked on one box, profiles/r04ai/).  With the form-23 pass on the split (pick_form) the
+// best n moves: c3r4 128 (20.6 k), c3r2 64 (13.9-14.3 k), c3r8 128 (profiles/r04ah/).  Auto: 128
+// CUs for the chain up to 8,192 local rows, 64 below 32,768, at most half the CUs, 0 (no masks)
+// from 32,768; DLP_CHAIN_CUS=n overrides (0 = off).
 int chain_cus_policy(const dlp_session* s) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 64)
