@@ -188,3 +188,72 @@ def test_rccl_rank_session_lookahead_on_cu_split():
             assert float(res.objective).hex() == want["objective_hex"]
             assert _split_sha(s, g["width"], g["m"] // 2) == want["block_sha256"]
             assert _sha(s.read_rows(s.rows, 1)[0, :g["width"]]) == want["objective_row_sha256"]
+
+
+def _stall_worker(rank, world, port, g, q):
+    """Rank 0 runs two windows; rank 1 runs only the first and then stops taking part (it stays
+    alive, so its exchange block stays mapped).  Rank 0's device waits in the second window end at
+    its exchange timeout + 5 s through the abort word; the run returns DLP_ERR_RCCL."""
+    import time as _t
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {"rank": rank}
+    s = None
+    try:
+        s = dlp.Session(dlp.Problem.random(g["m"], g["n"], g["seed"]), rank=rank, nranks=world, defer=0,
+                        check_interval=64, max_pivots=400)
+        hs = [None] * world
+        dist.all_gather_object(hs, s.exchange_handle())
+        s.connect_ipc(hs)
+        s.set_exchange_timeout(3.0)
+        dist.barrier()
+        out["first"] = s.run(136)
+        if rank == 0:
+            t0 = _t.time()
+            try:
+                s.run(64)
+                out["second"] = "completed"
+            except L.DLPError as e:
+                out["second"] = (e.status, str(e))
+            out["seconds"] = _t.time() - t0
+        s.abort()                 # every rank: no device wait outlives the test
+        import torch
+        torch.cuda.synchronize()
+        dist.barrier()            # both streams drained before either block is freed
+        s.close()
+        s = None
+    except Exception as e:   # reported to the parent
+        out["error"] = repr(e)
+    finally:
+        q.put(out)
+        dist.destroy_process_group()
+
+
+def test_two_process_rank_stall_is_bounded():
+    """Failure containment across processes at the shipped geometry: a rank
+    that stops taking part mid-solve ends its peer's run with DLP_ERR_RCCL in bounded time, not a
+    hang; both processes then abort, drain and free their blocks cleanly."""
+    import torch.multiprocessing as mp
+    g = load_golden("digests.json")["rank_split"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_worker, args=(r, 2, port, g, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted((q.get(timeout=240) for _ in procs), key=lambda o: o["rank"])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    for o in out:
+        assert "error" not in o, o
+        assert o["first"] == (L.RUNNING, 136) or o["first"][1] == 136, o
+    st, msg = out[0]["second"]
+    assert st == L.ERR_RCCL, out[0]
+    assert out[0]["seconds"] < 60, out[0]
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
