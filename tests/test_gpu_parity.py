@@ -304,3 +304,14 @@ def test_release_cached_memory():
     assert dlp.release_cached_memory() == 0
     res2 = dlp.solve(dlp.Problem.dense(A, b, c), small_lp=-1)
     assert res.pivot_log.tobytes() == res2.pivot_log.tobytes() == ref.pivot_log.tobytes()
+
+
+def test_batched_occupancy_query():
+    """dlp_batched_occupancy (bench.py --workload c5's roofline): the register-resident kernel at
+    m = 64 (ceil(n / 64) waves per LP), the LDS-resident one otherwise; at least one LP per CU."""
+    o = dlp.batched_occupancy(64, 128)
+    assert o["register_kernel"] and o["threads_per_lp"] == 128 and o["lps_per_cu"] >= 1
+    o = dlp.batched_occupancy(64, 64)
+    assert o["register_kernel"] and o["threads_per_lp"] == 64 and o["lps_per_cu"] >= o["lps_per_cu"]
+    o = dlp.batched_occupancy(40, 60)
+    assert not o["register_kernel"] and o["threads_per_lp"] in (256, 512) and o["lps_per_cu"] >= 1
