@@ -309,9 +309,9 @@ def test_release_cached_memory():
 def test_batched_occupancy_query():
     """dlp_batched_occupancy (bench.py --workload c5's roofline): the register-resident kernel at
     m = 64 (ceil(n / 64) waves per LP), the LDS-resident one otherwise; at least one LP per CU."""
-    o = dlp.batched_occupancy(64, 128)
-    assert o["register_kernel"] and o["threads_per_lp"] == 128 and o["lps_per_cu"] >= 1
-    o = dlp.batched_occupancy(64, 64)
-    assert o["register_kernel"] and o["threads_per_lp"] == 64 and o["lps_per_cu"] >= o["lps_per_cu"]
+    o128 = dlp.batched_occupancy(64, 128)
+    assert o128["register_kernel"] and o128["threads_per_lp"] == 128 and o128["lps_per_cu"] >= 1
+    o = dlp.batched_occupancy(64, 64)   # one wave per LP: at least as many LPs per CU
+    assert o["register_kernel"] and o["threads_per_lp"] == 64 and o["lps_per_cu"] >= o128["lps_per_cu"]
     o = dlp.batched_occupancy(40, 60)
     assert not o["register_kernel"] and o["threads_per_lp"] in (256, 512) and o["lps_per_cu"] >= 1
