@@ -2509,6 +2509,13 @@ static void launch_pass_r(const Geometry& g, const Defer& d, DevState* st, int r
         g.T, g.ld, g.rows, g.width, st, d.C, d.ldc, d.P, d.nzc, rb, ntiles, nbands, order);
 }
 
+// DLP_PASS_LDS=<bytes> (tuning only): the dynamic LDS of the forms-21/23 pass workgroups, which caps
+// how many share a CU while leaving the rest of the 160 KiB to the chain kernels beside them
+static size_t pass_lds_env() {
+    static const long v = std::getenv("DLP_PASS_LDS") ? std::atol(std::getenv("DLP_PASS_LDS")) : 0;
+    return v > 0 && v <= 150 * 1024 ? (size_t)v : 0;
+}
+
 template <bool NT, int K>
 static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, int occ,
                        hipStream_t s, double* Tout, int seal, uint32_t* bcnt) {
@@ -2573,7 +2580,7 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
         (int64_t)rb * d.ldc * 8 < ((int64_t)1 << 31)) {
         // DPP-coefficient pass (K = 64 blocks; 1 double per lane: 256-column tiles)
         if constexpr (K == 64) {
-            size_t dyn = 0;
+            size_t dyn = pass_lds_env();
             if (occ > 0) dyn = (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t);
             const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
             if (g.rows > 0) {
@@ -2597,8 +2604,8 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
             // ring depth D: 4 groups in flight (DLP_Q_DEPTH = 2 or 3: tuning only)
             static const int qd = std::getenv("DLP_Q_DEPTH") ? std::atoi(std::getenv("DLP_Q_DEPTH")) : 4;
             constexpr int U = 2;
-            const int D = qd == 2 || qd == 3 ? qd : 4;
-            size_t dyn = (size_t)4 * D * 128 * U * sizeof(double);
+            const int D = qd == 2 || qd == 3 || qd == 6 || qd == 8 ? qd : 4;
+            size_t dyn = std::max((size_t)4 * D * 128 * U * sizeof(double), pass_lds_env());
             if (occ > 0) dyn = std::max(dyn, (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t));
             const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
 #define DLP_PASS_Q(DD)                                                                                     \
@@ -2615,6 +2622,10 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
                     DLP_PASS_Q(2);
                 else if (D == 3)
                     DLP_PASS_Q(3);
+                else if (D == 6)
+                    DLP_PASS_Q(6);
+                else if (D == 8)
+                    DLP_PASS_Q(8);
                 else
                     DLP_PASS_Q(4);
             }

@@ -108,11 +108,19 @@ def test_ratio_threads_without_lookahead(n):
     assert _run("defer", [0], {"DLP_RATIO_THREADS": n}) == _ref("defer", 0)
 
 
-@pytest.mark.parametrize("depth", ["2", "3"])
+@pytest.mark.parametrize("depth", ["2", "3", "6", "8"])
 def test_form23_ring_depth(depth):
     ref = _ref("defer", 0)
     assert not ref["lookahead"] and ref["form"] == 23 and ref["chain_cus"] == 0
     assert _run("defer", [0], {"DLP_Q_DEPTH": depth}) == ref
+
+
+@pytest.mark.parametrize("env", [{"DLP_PASS_LDS": "57344"}, {"DLP_PASS_LDS": "57344", "DLP_Q_DEPTH": "6"}])
+def test_pass_lds_cap(env):
+    """Pass workgroups held to 2 per CU by their LDS (the chain beside them keeps the rest): same bits,
+    without lookahead (form 23) and with it (form 21 beside the chain)."""
+    assert _run("defer", [0], env) == _ref("defer", 0)
+    assert _run("defer", [1], env) == _ref("defer", 1)
 
 
 def test_batched_lds_kernel_knob():
