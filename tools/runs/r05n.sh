@@ -13,5 +13,5 @@ d=json.loads(open('$O/c3_$1.json').read().strip().splitlines()[-1]); b=d['block'
 print('$1', round(d['value']), 'block', round(b['ms'],3), 'pass', round(b['pass_ms'],3), 'form', d['geometry']['form'])"
 }
 for r in a b; do
-run def$r "" X=0 && run f23$r "--form 23" X=0 && run f23l56$r "--form 23" DLP_PASS_LDS=57344 && run f23d6l56$r "--form 23" DLP_PASS_LDS=57344 DLP_Q_DEPTH=6 && run f23d8$r "--form 23" DLP_Q_DEPTH=8 && run f21l56$r "" DLP_PASS_LDS=57344 || exit 1
+run def$r "" X=0 && run f23$r "--form 23" X=0 && run f23l56$r "--form 23" DLP_PASS_LDS=57344 && run f23d6l56$r "--form 23" DLP_PASS_LDS=57344 DLP_Q_DEPTH=6 && run f23d8$r "--form 23" DLP_Q_DEPTH=8 && run f21l56$r "" DLP_PASS_LDS=57344 && run c32$r "" DLP_CHAIN_CUS=32 || exit 1
 done
