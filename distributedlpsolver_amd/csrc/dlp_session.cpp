@@ -564,17 +564,17 @@ int flush_pending_block(dlp_session* s);
 // through each wave's LDS-DMA ring, whose rate is per CU): fixed at creation, since the peer
 // exchange's candidate slots are one per ratio workgroup of every rank (xslots), identical on
 // every rank — so the rule reads the global m and the rank count, not the local rows.  128 lanes
-// on a streaming rank tableau of at most 8,192 rows (the chain on CUs of its own: c3r8 25.3-25.4 k
-// vs 24.8-25.0 k pivots/s, c3r4 21.0 k vs 20.7-20.9 k; 64 lanes lose it again, profiles/r05d/),
-// else 256.  DLP_RATIO_THREADS=64/128/256 overrides.
+// up to 8,192 rows per rank: twice the workgroups spread the replay over more CUs (c3r8 25.3-25.4 k
+// vs 24.8-25.0 k pivots/s, c3r4 21.0 k vs 20.7-20.9 k, profiles/r05d/; C2 44.7 k vs 42.7 k,
+// profiles/r05o/; 64 lanes gain nothing more), else 256 (C3 at P = 1: no difference,
+// profiles/r05e/).  DLP_RATIO_THREADS=64/128/256 overrides.
 int ratio_threads_policy(const dlp_session* s) {
     if (const char* e = std::getenv("DLP_RATIO_THREADS")) {
         const int n = std::atoi(e);
         if (n == 64 || n == 128 || n == 256) return n;
     }
     const int64_t per_rank = s->m / std::max(s->nranks, 1);
-    const bool streaming = (double)(per_rank + 1) * (double)s->ld * 8.0 > (double)((size_t)1 << 30);
-    return streaming && per_rank <= 8192 ? 128 : dlp::kRatioDeferThreads;
+    return per_rank <= 8192 ? 128 : dlp::kRatioDeferThreads;
 }
 
 // Lookahead on: a second tableau buffer holding the same bytes, a second set of
