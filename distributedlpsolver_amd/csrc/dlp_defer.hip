@@ -2345,8 +2345,9 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                 pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xfuse ? 1 : 0);
             return hipGetLastError();
         }
-#define DLP_RATIO_LEAN(L, DYN)                                                                             \
-    ratio_lean_kernel<128, L><<<nblocks, g.rthreads, DYN, s>>>(                                       \
+        static const int ring_env = std::getenv("DLP_CHAIN_RING") ? std::atoi(std::getenv("DLP_CHAIN_RING")) : 0;
+#define DLP_RATIO_LEAN(L, DYN, ...)                                                                        \
+    ratio_lean_kernel<128, L, ##__VA_ARGS__><<<nblocks, g.rthreads, DYN, s>>>(                         \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
         d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
         xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,   \
@@ -2356,6 +2357,8 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
             DLP_RATIO_LEAN(8, 0);
         else if (lch == 4)
             DLP_RATIO_LEAN(4, 0);
+        else if (ring_env == 16)   // (tuning: DLP_CHAIN_RING=16, 16 ring DMAs in flight per wave)
+            DLP_RATIO_LEAN(0, ratio_ring_bytes(16) / (kRatioDeferThreads / g.rthreads), 16);
         else
             DLP_RATIO_LEAN(0, ratio_ring_bytes(kRatioRingPairs) / (kRatioDeferThreads / g.rthreads));
 #undef DLP_RATIO_LEAN
@@ -2441,7 +2444,11 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
         nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal, nranks == 1 ? nullptr : xp, xseq,                \
         pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,           \
         pub ? bp->Tn : nullptr, xc)
-        DLP_PROW_LEAN(kProwRingSteps);
+        static const int ring_env = std::getenv("DLP_CHAIN_RING") ? std::atoi(std::getenv("DLP_CHAIN_RING")) : 0;
+        if (ring_env == 16)
+            DLP_PROW_LEAN(16);
+        else
+            DLP_PROW_LEAN(kProwRingSteps);
 #undef DLP_PROW_LEAN
     } else
         prow_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc,

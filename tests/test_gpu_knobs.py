@@ -71,7 +71,8 @@ def _ref(kind, *args):
 @pytest.mark.parametrize("env", [{"DLP_LEAN_LCH": "4"}, {"DLP_LEAN_LCH": "8"}, {"DLP_BAND_PUB": "0"},
                                  {"DLP_CHAIN_CUS": "0"}, {"DLP_CHAIN_CUS": "32"}, {"DLP_CHAIN_CUS": "200"},
                                  {"DLP_FAT_PROW": "0"}, {"DLP_RATIO_THREADS": "64"},
-                                 {"DLP_RATIO_THREADS": "128"}, {"DLP_RATIO_THREADS": "256"}])
+                                 {"DLP_RATIO_THREADS": "128"}, {"DLP_RATIO_THREADS": "256"},
+                                 {"DLP_CHAIN_RING": "16"}, {"DLP_CHAIN_RING": "16", "DLP_FAT_PROW": "0"}])
 def test_lookahead_chain_knobs(env):
     ref = _ref("defer", 1)
     # 4,096 rows: the chain on 128 CUs, the pass on the other 128 (chain_cus_policy)
