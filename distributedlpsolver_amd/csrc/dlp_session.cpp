@@ -624,7 +624,11 @@ int chain_cus_apply(dlp_session* s, int n) {
     s->stream = nullptr;
     int lo = 0, hi = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    s->prio_chain = n > 0 ? kMaskedKey + ((cus - n) << 10) + n : hi;
+    // (tests: DLP_TEST_CHAIN_CU_FIRST puts the chain's n CUs at another first bit, so that rank
+    // processes sharing one GPU get disjoint chain CUs: tests/test_gpu_ranks.py)
+    int first = cus - n;
+    if (const char* e = std::getenv("DLP_TEST_CHAIN_CU_FIRST")) first = std::max(0, std::min(std::atoi(e), cus - n));
+    s->prio_chain = n > 0 ? kMaskedKey + (first << 10) + n : hi;
     s->prio_pass = n > 0 ? kMaskedKey + (cus - n) : lo;
     if (n > 0 && acquire_stream(s->device, s->prio_chain, &s->stream) != hipSuccess) {
         (void)hipGetLastError();   // no CU-masked queue here: both streams unmasked, as before round 4
