@@ -24,6 +24,9 @@ for the GPU to reproduce.  Run in the build container (CPU only):
   rank_split  bench.py's c3r4 LP (8192 x 57344 seed 34) split over 2 processes of
       4,096 rows (the per-process rank path, tests/test_gpu_ranks.py): per-rank block
       digests, objective row, log and basis at 136 / 200 / 264 pivots.
+  rank_split_c3  C3 itself (32768 x 32768 seed 3) split over 2, 4 and 8 processes (the
+      rank geometries of the N = 2, 4, 8 scaling runs): the same digests at 136 / 200
+      pivots, with the block digests of each split ("blocks": {"2": [...], "4": [...], "8": [...]}).
 
 The digests hash little-endian fp64 / int32 bytes of the oracle's outputs
 (tests/oracle_py.py), so the GPU side compares bit for bit."""
@@ -98,25 +101,34 @@ def c3_tableau(stops=(136, 160, C3_K64_PIVOTS, C3_K64_PIVOTS + 256)):
     return out
 
 
-def rank_split(m=8192, n=57344, seed=34, P=2, stops=(136, 200, 264)):
+def rank_split(m=8192, n=57344, seed=34, P=2, stops=(136, 200, 264), Ps=None):
     """The per-process rank path of a scaling run: bench.py's c3r4 LP
     (8192 x 57344 seed 34) row-partitioned over P = 2 processes, so that each rank holds
     4,096 x 65,537 — exactly one rank of C3's 8-GPU split.  At each stop: the log and
     basis digests, the objective bits, and one sha256 per rank's row block (rows
     [floor(r m / P), floor((r+1) m / P)), each row its first `width` doubles) plus one of
-    the objective row, so every process can check its own block without the others'."""
+    the objective row, so every process can check its own block without the others'.
+    Ps: several splits of the same run, their block digests under "blocks" keyed by P."""
     t0 = time.time()
     w = ((n + m + 1) + 15) // 16 * 16
     out = {"m": m, "n": n, "seed": seed, "P": P, "width": w, "stops": {}}
-    cuts = [r * m // P for r in range(P + 1)]
+    if Ps:
+        out["Ps"] = list(Ps)
+
+    def blocks(T, p):
+        cuts = [r * m // p for r in range(p + 1)]
+        return [tableau_sha(T[cuts[r]:cuts[r + 1]], w) for r in range(p)]
 
     def at(k, T, log, basis):
-        out["stops"][str(k)] = {
-            "log_sha256": sha(log), "basis_sha256": sha(basis),
-            "objective_hex": float(log[-1]["objective"]).hex(),
-            "block_sha256": [tableau_sha(T[cuts[r]:cuts[r + 1]], w) for r in range(P)],
-            "objective_row_sha256": sha(T[m, :w]), "oracle_seconds": time.time() - t0}
-        print(k, out["stops"][str(k)], flush=True)
+        rec = {"log_sha256": sha(log), "basis_sha256": sha(basis),
+               "objective_hex": float(log[-1]["objective"]).hex(),
+               "objective_row_sha256": sha(T[m, :w]), "oracle_seconds": time.time() - t0}
+        if Ps:
+            rec["blocks"] = {str(p): blocks(T, p) for p in Ps}
+        else:
+            rec["block_sha256"] = blocks(T, P)
+        out["stops"][str(k)] = rec
+        print(k, rec, flush=True)
 
     O.run_generated_stops(m, n, seed, list(stops), at, nthreads=os.cpu_count() or 8)
     return out
@@ -170,7 +182,8 @@ def main():
             d = json.load(f)
     for w in which:
         d[w] = {"c2": c2, "c3": c3, "c3_k64": lambda: c3(C3_K64_PIVOTS), "c3_tableau": c3_tableau,
-                "c5": c5, "rank_split": rank_split}[w]()
+                "c5": c5, "rank_split": rank_split,
+                "rank_split_c3": lambda: rank_split(32768, 32768, 3, P=2, stops=(136, 200), Ps=(2, 4, 8))}[w]()
         with open(OUT, "w") as f:
             json.dump(d, f, indent=1)
         print(w, json.dumps(d[w]), flush=True)

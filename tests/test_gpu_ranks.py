@@ -50,11 +50,21 @@ def _block_sha(s, width, chunk=512):
     return h.hexdigest()
 
 
+def _want_block(want, world, rank):
+    """The oracle's digest of this rank's row block at one stop (entries with several splits keep
+    them under "blocks", keyed by the rank count)."""
+    return want["blocks"][str(world)][rank] if "blocks" in want else want["block_sha256"][rank]
+
+
 def _rank_worker(rank, world, port, g, windows, env, q):
     """One process = one rank session, driven exactly as bench.py drives it (dlp_session_run
     windows on its own stream), checked against the oracle's stops after each window."""
     import torch.distributed as dist
     os.environ.update(env)
+    if "CHAIN_SLICE" in env:   # this rank's chain on CUs no other rank process's chain uses
+        n = int(env["CHAIN_SLICE"])
+        os.environ["DLP_CHAIN_CUS"] = str(n)
+        os.environ["DLP_TEST_CHAIN_CU_FIRST"] = str(256 - n * (rank + 1))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -85,7 +95,7 @@ def _rank_worker(rank, world, port, g, windows, env, q):
             got = {"log": _sha(res.pivot_log) == want["log_sha256"],
                    "basis": _sha(res.basis) == want["basis_sha256"],
                    "objective": float(res.objective).hex() == want["objective_hex"],
-                   "block": _block_sha(s, g["width"]) == want["block_sha256"][rank],
+                   "block": _block_sha(s, g["width"]) == _want_block(want, world, rank),
                    "objective_row": _sha(s.read_rows(s.rows, 1)[0, :g["width"]]) == want["objective_row_sha256"]}
             out["checks"][str(total)] = got
         # no rank frees its exchange block while a peer's kernels may still store into it
@@ -101,10 +111,10 @@ def _rank_worker(rank, world, port, g, windows, env, q):
         dist.destroy_process_group()
 
 
-def _run_two(windows, env, timeout=240):
+def _run_two(windows, env, timeout=240, key="rank_split", world=None):
     import torch.multiprocessing as mp
-    g = load_golden("digests.json")["rank_split"]
-    world = g["P"]
+    g = load_golden("digests.json")[key]
+    world = world or g["P"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -147,6 +157,35 @@ def test_two_process_rank_path(case):
         else:
             assert cfg["lookahead"] and cfg["defer_tuning"][1] == 21
             assert cfg["chain_cus"] == (0 if case == "chain_cus_0" else 128)
+        assert [d for _, d in o["runs"]] == windows
+        assert set(o["checks"]) == {str(k) for k in np.cumsum(windows)}
+        for k, got in o["checks"].items():
+            assert all(got.values()), (o["rank"], k, got)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_c3_rank_processes(world):
+    """The rank geometries of the N = 2, 4 and 8 scaling runs, each rank its own process on this
+    one GPU: C3 itself (32,768 x 32,768 seed 3, bench.py's default LP) split into 2 x 16,384 rows
+    (the auto policy: 64 chain CUs, 256-lane ratio workgroups, the form-23 pass on the other CUs),
+    4 x 8,192 (128-lane ratio workgroups, form 23, the register pivot-row kernel of a chain on CUs
+    of its own) or 8 x 4,096 (the same with the form-21 pass), with lookahead and the two-launch
+    peer pivot; 136 pivots (two full blocks + 8; N = 2: then 64 more, ending inside a block)
+    against the oracle's stops (tests/golden/make_digests.py rank_split_c3).
+    Four or eight processes on one GPU: each rank's chain on 32 CUs of its own
+    (DLP_TEST_CHAIN_CU_FIRST) instead of all on the same top 128 — with the shared mask their
+    spinning chain workgroups fill those CUs and starve the owner's (3+ processes,
+    profiles/r05w/; on N GPUs each chain has its GPU's CUs to itself)."""
+    windows = [136, 64] if world == 2 else [136]
+    env = {} if world == 2 else {"CHAIN_SLICE": "32"}
+    g, out = _run_two(windows, env, timeout=420, key="rank_split_c3", world=world)
+    rows = g["m"] // world
+    for o in out:
+        cfg = o["config"]
+        assert cfg["exchange"] == L.XCHG_PEER and cfg["lookahead"]
+        assert cfg["rows"] == rows and cfg["row_first"] == o["rank"] * rows
+        assert cfg["defer_tuning"][1:] == (23 if rows > 4096 else 21, 64)
+        assert cfg["chain_cus"] == (64 if world == 2 else 32)
         assert [d for _, d in o["runs"]] == windows
         assert set(o["checks"]) == {str(k) for k in np.cumsum(windows)}
         for k, got in o["checks"].items():
