@@ -92,6 +92,33 @@ def test_peer_exchange_degenerate_bland(P, K):
             s.close()
 
 
+@pytest.mark.parametrize("P,K", [(2, 1), (3, 16), (4, 16), (2, 64)])
+def test_peer_exchange_unbounded(P, K):
+    """An unbounded LP through the peer exchange: column 5 of A small and non-positive with
+    c_5 = 0.5, so x_5 enters after 96 pivots, no row bounds it, and every rank's selection ends
+    the solve DLP_UNBOUNDED at the same pivot as the oracle (every rank's candidates empty).
+    K = 64: with lookahead forced on, the end comes in the second block's selection while the
+    first block's pass runs."""
+    A, b, c = O.gen_dense(60, 80, 9)
+    A[:, 5] = -np.abs(A[:, 5]) * 0.01
+    c[5] = 0.5
+    ref = O.solve_dense(A, b, c)
+    assert ref.status == L.UNBOUNDED and ref.num_pivots == 96
+    sess = _peer_ranks(dlp.Problem.dense(A, b, c), P, defer=K, check_interval=29,
+                       lookahead=1 if K == 64 else -1)
+    try:
+        assert all(s.lookahead() for s in sess) == (K == 64)
+        st, done = dlp.Session.run_ranks(sess, 10 ** 6)
+        assert st == L.UNBOUNDED and done == ref.num_pivots
+        for s in sess:
+            r = s.result()
+            assert r.status == L.UNBOUNDED
+            _same_log(r.pivot_log, ref.pivot_log)
+    finally:
+        for s in sess:
+            s.close()
+
+
 def test_peer_exchange_lookahead_and_windows():
     """Lookahead forced on (selection of block b+1 beside pass b) and windows that end
     inside blocks, resumed: the peer sequence numbers continue across runs."""
