@@ -335,33 +335,31 @@ __device__ __forceinline__ int wave_min_i32(int v) {
 
 // Rows of the register-resident elimination in inline asm.  The entering column's entry f
 // and the pivot row index are the same for every lane of the LP, so each test is a uniform
-// exec mask (all lanes or none) set by SALU, with no branch: a row costs one compare and one
-// fma on the VALU.  (hipcc, left to itself, turned the 2 x 65 tests into live vector masks
+// exec mask (all lanes or none) set by SALU, with no branch.  (hipcc, left to itself, turned the 2 x 65 tests into live vector masks
 // and spilled them, or moved the register rows to scratch.)
 // t := fma(-f, pj, t) unless f == +-0 (the eager rule leaves the row untouched).
-// 8 rows: the 8 tests first, then per row one exec select (from the saved exec) and the fma
-__device__ __forceinline__ void elim8(double* t, const double* f, double pj) {
-    uint64_t m0, m1, m2, m3, m4, m5, m6, m7, sv;
+// 8 rows, their masks from zm (bit r set: the entering column's row r is +-0, the row is skipped;
+// the ratio test ballots it once per pivot), so a row costs two SALU instructions and its fma
+// (round 5; round 3-4 compared every row on the VALU first, a VALU -> SALU dependency per row)
+template <int R0>
+__device__ __forceinline__ void elim8z(double* t, const double* f, double pj, uint64_t zm) {
+    uint64_t sv;
     asm volatile(
-        "v_cmp_neq_f64_e64 %[m0], 0, %[f0]\n\tv_cmp_neq_f64_e64 %[m1], 0, %[f1]\n\t"
-        "v_cmp_neq_f64_e64 %[m2], 0, %[f2]\n\tv_cmp_neq_f64_e64 %[m3], 0, %[f3]\n\t"
-        "v_cmp_neq_f64_e64 %[m4], 0, %[f4]\n\tv_cmp_neq_f64_e64 %[m5], 0, %[f5]\n\t"
-        "v_cmp_neq_f64_e64 %[m6], 0, %[f6]\n\tv_cmp_neq_f64_e64 %[m7], 0, %[f7]\n\t"
         "s_mov_b64 %[sv], exec\n\t"
-        "s_and_b64 exec, %[sv], %[m0]\n\tv_fma_f64 %[t0], -%[f0], %[pj], %[t0]\n\t"
-        "s_and_b64 exec, %[sv], %[m1]\n\tv_fma_f64 %[t1], -%[f1], %[pj], %[t1]\n\t"
-        "s_and_b64 exec, %[sv], %[m2]\n\tv_fma_f64 %[t2], -%[f2], %[pj], %[t2]\n\t"
-        "s_and_b64 exec, %[sv], %[m3]\n\tv_fma_f64 %[t3], -%[f3], %[pj], %[t3]\n\t"
-        "s_and_b64 exec, %[sv], %[m4]\n\tv_fma_f64 %[t4], -%[f4], %[pj], %[t4]\n\t"
-        "s_and_b64 exec, %[sv], %[m5]\n\tv_fma_f64 %[t5], -%[f5], %[pj], %[t5]\n\t"
-        "s_and_b64 exec, %[sv], %[m6]\n\tv_fma_f64 %[t6], -%[f6], %[pj], %[t6]\n\t"
-        "s_and_b64 exec, %[sv], %[m7]\n\tv_fma_f64 %[t7], -%[f7], %[pj], %[t7]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r0]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t0], -%[f0], %[pj], %[t0]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r1]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t1], -%[f1], %[pj], %[t1]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r2]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t2], -%[f2], %[pj], %[t2]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r3]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t3], -%[f3], %[pj], %[t3]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r4]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t4], -%[f4], %[pj], %[t4]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r5]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t5], -%[f5], %[pj], %[t5]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r6]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t6], -%[f6], %[pj], %[t6]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r7]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t7], -%[f7], %[pj], %[t7]\n\t"
         "s_mov_b64 exec, %[sv]"
         : [t0] "+v"(t[0]), [t1] "+v"(t[1]), [t2] "+v"(t[2]), [t3] "+v"(t[3]), [t4] "+v"(t[4]), [t5] "+v"(t[5]),
-          [t6] "+v"(t[6]), [t7] "+v"(t[7]), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3),
-          [m4] "=&s"(m4), [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7), [sv] "=&s"(sv)
+          [t6] "+v"(t[6]), [t7] "+v"(t[7]), [sv] "=&s"(sv)
         : [f0] "v"(f[0]), [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [f4] "v"(f[4]), [f5] "v"(f[5]),
-          [f6] "v"(f[6]), [f7] "v"(f[7]), [pj] "v"(pj)
+          [f6] "v"(f[6]), [f7] "v"(f[7]), [pj] "v"(pj), [zm] "s"(zm), [r0] "n"(R0), [r1] "n"(R0 + 1),
+          [r2] "n"(R0 + 2), [r3] "n"(R0 + 3), [r4] "n"(R0 + 4), [r5] "n"(R0 + 5), [r6] "n"(R0 + 6), [r7] "n"(R0 + 7)
         : "scc");
 }
 __device__ __forceinline__ void elim_row(double& t, double f, double pj) {
@@ -443,6 +441,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     __shared__ int32_t s_basis[M];
     __shared__ int32_t s_p, s_leave, s_bland;
     __shared__ double s_piv;
+    __shared__ uint64_t s_zm;   // rows 0..63 of the entering column that are +-0 (the elimination's skip rule)
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int N = n + M;
     const int sl = tid;              // this lane's slot: < n a variable's column
@@ -531,6 +530,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             // min ratio over the valid rows, then the smallest basis variable among the rows
             // holding it (cand_better's order), field by field
             const double a = s_colq[lane];
+            const uint64_t zm = __ballot(a == 0.0);   // (-0 == 0: both skipped, as the eager rule)
+            if (lane == 0) s_zm = zm;
             const bool valid = a > tol_piv;
             double ratio = __builtin_inf();
             if (valid) {
@@ -592,10 +593,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         const double pj = (ent ? 1.0 : tp) / s_piv;
         stamp(4);
         if (ent) each<R>([&](auto I) { t[I] = 0.0; });   // e_p before the pivot (see the LDS kernel)
+        // the skip rule's row masks from the entering column's zero mask (SALU, no VALU compare
+        // and no VALU -> SALU dependency per row; elim8z)
+        const uint64_t zm = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_zm >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)s_zm);
         double fq[8];   // a group's column entries, read together
         each<M / 8>([&](auto G) {
             each<8>([&](auto J) { fq[J] = s_colq[8 * G + J]; });
-            elim8(&t[8 * G], fq, pj);
+            elim8z<8 * G>(&t[8 * G], fq, pj, zm);
         });
         elim_row(t[M], s_colq[M], pj);   // the objective row
         each<M / 8>([&](auto G) { set8<8 * G>(&t[8 * G], pj, p); });   // row p := the pivot row

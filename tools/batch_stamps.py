@@ -15,12 +15,13 @@ os.environ["DLP_BATCH_STAMPS"] = path
 import distributedlpsolver_amd as dlp  # noqa: E402
 
 m, n = (int(a) for a in (sys.argv[1:3] if len(sys.argv) > 2 else (64, 128)))
-br = dlp.batched_solve(4096, m, n, 5000, log_cap=0)
+nlp = int(sys.argv[3]) if len(sys.argv) > 3 else 4096   # (256: one LP per CU, no co-resident LPs)
+br = dlp.batched_solve(nlp, m, n, 5000, log_cap=0)
 st = np.fromfile(path, dtype=np.uint64).reshape(64, 8).astype(np.float64) / 100.0   # us (100 MHz)
 ok = (st[:, :6] > 0).all(axis=1)
 st = st[ok]
 names = ["pricing", "column q + RHS to LDS", "ratio test + select", "row p + division", "elimination"]
 res = {nm: float(np.median(st[:, i + 1] - st[:, i])) for i, nm in enumerate(names)}
 res["pivot total"] = float(np.median(st[:, 5] - st[:, 0]))
-print(json.dumps({"m": m, "n": n, "pivots_sampled": int(ok.sum()), "kernel_ms": br.kernel_ms,
+print(json.dumps({"m": m, "n": n, "nlp": nlp, "pivots_sampled": int(ok.sum()), "kernel_ms": br.kernel_ms,
                   "median_us": res}, indent=1))
