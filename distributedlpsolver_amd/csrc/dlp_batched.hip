@@ -340,26 +340,33 @@ __device__ __forceinline__ int wave_min_i32(int v) {
 // t := fma(-f, pj, t) unless f == +-0 (the eager rule leaves the row untouched).
 // 8 rows, their masks from zm (bit r set: the entering column's row r is +-0, the row is skipped;
 // the ratio test ballots it once per pivot), so a row costs two SALU instructions and its fma
-// (round 5; round 3-4 compared every row on the VALU first, a VALU -> SALU dependency per row)
+// (round 5; rounds 3-4 compared every row on the VALU first, a VALU -> SALU dependency per row),
+// with the entering column's entries taken from another lane's register by DPP:
+// lane k of every 16-lane row holds entry 16 g + k (cq = colq[16 g + (lane & 15)], g = R0 / 16), and
+// v_fmac_f64_dpp ... row_newbcast:k reads it for the whole row (neg modifier: fma(-f, pj, t), the
+// eager operation), so the elimination waits for one LDS read per 16 rows instead of one per 8.
+// cq is written only by an LDS load (no VALU write within two instructions of a DPP read:
+// tests/test_isa.py); an SALU write of exec before a DPP op needs no wait state.
 template <int R0>
-__device__ __forceinline__ void elim8z(double* t, const double* f, double pj, uint64_t zm) {
+__device__ __forceinline__ void elim8dpp(double* t, double cq, double pj, uint64_t zm) {
     uint64_t sv;
     asm volatile(
         "s_mov_b64 %[sv], exec\n\t"
-        "s_bitcmp1_b64 %[zm], %[r0]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t0], -%[f0], %[pj], %[t0]\n\t"
-        "s_bitcmp1_b64 %[zm], %[r1]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t1], -%[f1], %[pj], %[t1]\n\t"
-        "s_bitcmp1_b64 %[zm], %[r2]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t2], -%[f2], %[pj], %[t2]\n\t"
-        "s_bitcmp1_b64 %[zm], %[r3]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t3], -%[f3], %[pj], %[t3]\n\t"
-        "s_bitcmp1_b64 %[zm], %[r4]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t4], -%[f4], %[pj], %[t4]\n\t"
-        "s_bitcmp1_b64 %[zm], %[r5]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t5], -%[f5], %[pj], %[t5]\n\t"
-        "s_bitcmp1_b64 %[zm], %[r6]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t6], -%[f6], %[pj], %[t6]\n\t"
-        "s_bitcmp1_b64 %[zm], %[r7]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fma_f64 %[t7], -%[f7], %[pj], %[t7]\n\t"
+        "s_bitcmp1_b64 %[zm], %[r0]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t0], -%[c], %[pj] row_newbcast:%[k0] row_mask:0xf bank_mask:0xf\n\t"
+        "s_bitcmp1_b64 %[zm], %[r1]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t1], -%[c], %[pj] row_newbcast:%[k1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_bitcmp1_b64 %[zm], %[r2]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t2], -%[c], %[pj] row_newbcast:%[k2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_bitcmp1_b64 %[zm], %[r3]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t3], -%[c], %[pj] row_newbcast:%[k3] row_mask:0xf bank_mask:0xf\n\t"
+        "s_bitcmp1_b64 %[zm], %[r4]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t4], -%[c], %[pj] row_newbcast:%[k4] row_mask:0xf bank_mask:0xf\n\t"
+        "s_bitcmp1_b64 %[zm], %[r5]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t5], -%[c], %[pj] row_newbcast:%[k5] row_mask:0xf bank_mask:0xf\n\t"
+        "s_bitcmp1_b64 %[zm], %[r6]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t6], -%[c], %[pj] row_newbcast:%[k6] row_mask:0xf bank_mask:0xf\n\t"
+        "s_bitcmp1_b64 %[zm], %[r7]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t7], -%[c], %[pj] row_newbcast:%[k7] row_mask:0xf bank_mask:0xf\n\t"
         "s_mov_b64 exec, %[sv]"
         : [t0] "+v"(t[0]), [t1] "+v"(t[1]), [t2] "+v"(t[2]), [t3] "+v"(t[3]), [t4] "+v"(t[4]), [t5] "+v"(t[5]),
           [t6] "+v"(t[6]), [t7] "+v"(t[7]), [sv] "=&s"(sv)
-        : [f0] "v"(f[0]), [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [f4] "v"(f[4]), [f5] "v"(f[5]),
-          [f6] "v"(f[6]), [f7] "v"(f[7]), [pj] "v"(pj), [zm] "s"(zm), [r0] "n"(R0), [r1] "n"(R0 + 1),
-          [r2] "n"(R0 + 2), [r3] "n"(R0 + 3), [r4] "n"(R0 + 4), [r5] "n"(R0 + 5), [r6] "n"(R0 + 6), [r7] "n"(R0 + 7)
+        : [c] "v"(cq), [pj] "v"(pj), [zm] "s"(zm), [r0] "n"(R0), [r1] "n"(R0 + 1), [r2] "n"(R0 + 2),
+          [r3] "n"(R0 + 3), [r4] "n"(R0 + 4), [r5] "n"(R0 + 5), [r6] "n"(R0 + 6), [r7] "n"(R0 + 7),
+          [k0] "n"(R0 % 16), [k1] "n"(R0 % 16 + 1), [k2] "n"(R0 % 16 + 2), [k3] "n"(R0 % 16 + 3),
+          [k4] "n"(R0 % 16 + 4), [k5] "n"(R0 % 16 + 5), [k6] "n"(R0 % 16 + 6), [k7] "n"(R0 % 16 + 7)
         : "scc");
 }
 __device__ __forceinline__ void elim_row(double& t, double f, double pj) {
@@ -588,22 +595,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         const bool ent = sl == sq;
         if (ent) var = s_leave;
         double tp = 0.0;
-        each<M / 8>([&](auto G) { pick8<8 * G>(tp, &t[8 * G], p); });   // tp = t[p]
+        // tp = t[p]: only the group of 8 rows holding p (a uniform branch per group)
+        each<M / 8>([&](auto G) { if ((p >> 3) == (int)G) pick8<8 * G>(tp, &t[8 * G], p); });
         move_if_row<M>(tp, t[M], p);
         const double pj = (ent ? 1.0 : tp) / s_piv;
         stamp(4);
         if (ent) each<R>([&](auto I) { t[I] = 0.0; });   // e_p before the pivot (see the LDS kernel)
         // the skip rule's row masks from the entering column's zero mask (SALU, no VALU compare
-        // and no VALU -> SALU dependency per row; elim8z)
+        // per row), the entries by DPP from 4 LDS reads per lane (elim8dpp)
         const uint64_t zm = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_zm >> 32)) << 32) |
                             __builtin_amdgcn_readfirstlane((uint32_t)s_zm);
-        double fq[8];   // a group's column entries, read together
-        each<M / 8>([&](auto G) {
-            each<8>([&](auto J) { fq[J] = s_colq[8 * G + J]; });
-            elim8z<8 * G>(&t[8 * G], fq, pj, zm);
-        });
+        double cq[M / 16];
+        each<M / 16>([&](auto G) { cq[G] = s_colq[16 * G + (lane & 15)]; });
+        each<M / 8>([&](auto G) { elim8dpp<8 * G>(&t[8 * G], cq[G / 2], pj, zm); });
         elim_row(t[M], s_colq[M], pj);   // the objective row
-        each<M / 8>([&](auto G) { set8<8 * G>(&t[8 * G], pj, p); });   // row p := the pivot row
+        each<M / 8>([&](auto G) { if ((p >> 3) == (int)G) set8<8 * G>(&t[8 * G], pj, p); });   // row p := the pivot row
         move_if_row<M>(t[M], pj, p);
         if (wid == 0) {   // the RHS of row `lane` and the objective value, as a column slot updates its rows
             const double fr = s_colq[lane];
