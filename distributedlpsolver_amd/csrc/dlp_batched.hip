@@ -323,6 +323,12 @@ template <int CTRL, int RMASK>
 __device__ __forceinline__ int dpp_i32(int v) {
     return __builtin_amdgcn_update_dpp(kNoIndex, v, CTRL, RMASK, 0xf, false);
 }
+// lane `l`'s value (l uniform, in an SGPR): two v_readlane_b32
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ int wave_min_i32(int v) {
     v = min(v, dpp_i32<0xB1, 0xf>(v));
     v = min(v, dpp_i32<0x4E, 0xf>(v));
@@ -559,9 +565,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             Cand best;
             best.valid = anyv != 0 ? 1 : 0;
             best.row = wl;
-            best.basis_var = anyv != 0 ? __shfl(bv, wl) : kNoIndex;
-            best.ratio = anyv != 0 ? __shfl(ratio, wl) : 0.0;
-            best.pivot = anyv != 0 ? __shfl(a, wl) : 0.0;
+            // (wl is uniform: v_readlane, no LDS round trip as __shfl's ds_bpermute)
+            const int wls = __builtin_amdgcn_readfirstlane(wl < 0 ? 0 : wl);
+            best.basis_var = anyv != 0 ? __builtin_amdgcn_readlane(bv, wls) : kNoIndex;
+            best.ratio = anyv != 0 ? readlane_f64(ratio, wls) : 0.0;
+            best.pivot = anyv != 0 ? readlane_f64(a, wls) : 0.0;
             best.pad0 = 0;
             if (lane == 0) {
                 if (!best.valid) {
@@ -613,7 +621,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         move_if_row<M>(t[M], pj, p);
         if (wid == 0) {   // the RHS of row `lane` and the objective value, as a column slot updates its rows
             const double fr = s_colq[lane];
-            const double pjr = __shfl(rr, p) / s_piv;
+            const double pjr = readlane_f64(rr, p) / s_piv;   // (p uniform)
             const double v = __builtin_fma(-fr, pjr, rr);
             rr = lane == p ? pjr : (fr != 0.0 ? v : rr);
             const double fz = s_colq[M];
