@@ -356,7 +356,21 @@ __device__ __forceinline__ int wave_min_i32(int v) {
 template <int R0>
 __device__ __forceinline__ void elim8dpp(double* t, double cq, double pj, uint64_t zm) {
     uint64_t sv;
+    // (a group with no +-0 entry, the common case on a dense LP, branches to the 8 fmas back to
+    // back; the branch is inside the asm so the register allocator sees one block)
     asm volatile(
+        "s_bfe_u64 %[sv], %[zm], %[bfe]\n\t"
+        "s_cbranch_scc1 1f\n\t"
+        "v_fmac_f64_dpp %[t0], -%[c], %[pj] row_newbcast:%[k0] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[t1], -%[c], %[pj] row_newbcast:%[k1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[t2], -%[c], %[pj] row_newbcast:%[k2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[t3], -%[c], %[pj] row_newbcast:%[k3] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[t4], -%[c], %[pj] row_newbcast:%[k4] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[t5], -%[c], %[pj] row_newbcast:%[k5] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[t6], -%[c], %[pj] row_newbcast:%[k6] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[t7], -%[c], %[pj] row_newbcast:%[k7] row_mask:0xf bank_mask:0xf\n\t"
+        "s_branch 2f\n"
+        "1:\n\t"
         "s_mov_b64 %[sv], exec\n\t"
         "s_bitcmp1_b64 %[zm], %[r0]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t0], -%[c], %[pj] row_newbcast:%[k0] row_mask:0xf bank_mask:0xf\n\t"
         "s_bitcmp1_b64 %[zm], %[r1]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t1], -%[c], %[pj] row_newbcast:%[k1] row_mask:0xf bank_mask:0xf\n\t"
@@ -366,10 +380,11 @@ __device__ __forceinline__ void elim8dpp(double* t, double cq, double pj, uint64
         "s_bitcmp1_b64 %[zm], %[r5]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t5], -%[c], %[pj] row_newbcast:%[k5] row_mask:0xf bank_mask:0xf\n\t"
         "s_bitcmp1_b64 %[zm], %[r6]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t6], -%[c], %[pj] row_newbcast:%[k6] row_mask:0xf bank_mask:0xf\n\t"
         "s_bitcmp1_b64 %[zm], %[r7]\n\ts_cselect_b64 exec, 0, %[sv]\n\tv_fmac_f64_dpp %[t7], -%[c], %[pj] row_newbcast:%[k7] row_mask:0xf bank_mask:0xf\n\t"
-        "s_mov_b64 exec, %[sv]"
+        "s_mov_b64 exec, %[sv]\n"
+        "2:"
         : [t0] "+v"(t[0]), [t1] "+v"(t[1]), [t2] "+v"(t[2]), [t3] "+v"(t[3]), [t4] "+v"(t[4]), [t5] "+v"(t[5]),
           [t6] "+v"(t[6]), [t7] "+v"(t[7]), [sv] "=&s"(sv)
-        : [c] "v"(cq), [pj] "v"(pj), [zm] "s"(zm), [r0] "n"(R0), [r1] "n"(R0 + 1), [r2] "n"(R0 + 2),
+        : [c] "v"(cq), [pj] "v"(pj), [zm] "s"(zm), [bfe] "n"(R0 | (8 << 16)), [r0] "n"(R0), [r1] "n"(R0 + 1), [r2] "n"(R0 + 2),
           [r3] "n"(R0 + 3), [r4] "n"(R0 + 4), [r5] "n"(R0 + 5), [r6] "n"(R0 + 6), [r7] "n"(R0 + 7),
           [k0] "n"(R0 % 16), [k1] "n"(R0 % 16 + 1), [k2] "n"(R0 % 16 + 2), [k3] "n"(R0 % 16 + 3),
           [k4] "n"(R0 % 16 + 4), [k5] "n"(R0 % 16 + 5), [k6] "n"(R0 % 16 + 6), [k7] "n"(R0 % 16 + 7)
