@@ -609,6 +609,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         __syncthreads();
         stamp(3);
         const int p = __builtin_amdgcn_readfirstlane(s_p);   // (uniform: an SGPR operand below)
+        // the elimination's inputs, requested with p's (their LDS latency overlaps the pivot-row
+        // division): the skip rule's row masks from the entering column's zero mask (SALU, no VALU
+        // compare per row) and the entries for the DPP broadcast, 4 LDS reads per lane (elim8dpp)
+        const uint64_t zm = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_zm >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)s_zm);
+        double cq[M / 16];
+        each<M / 16>([&](auto G) { cq[G] = s_colq[16 * G + (lane & 15)]; });
         if (p < 0) {
             status = DLP_UNBOUNDED;
             break;
@@ -624,12 +631,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         const double pj = (ent ? 1.0 : tp) / s_piv;
         stamp(4);
         if (ent) each<R>([&](auto I) { t[I] = 0.0; });   // e_p before the pivot (see the LDS kernel)
-        // the skip rule's row masks from the entering column's zero mask (SALU, no VALU compare
-        // per row), the entries by DPP from 4 LDS reads per lane (elim8dpp)
-        const uint64_t zm = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_zm >> 32)) << 32) |
-                            __builtin_amdgcn_readfirstlane((uint32_t)s_zm);
-        double cq[M / 16];
-        each<M / 16>([&](auto G) { cq[G] = s_colq[16 * G + (lane & 15)]; });
         each<M / 8>([&](auto G) { elim8dpp<8 * G>(&t[8 * G], cq[G / 2], pj, zm); });
         elim_row(t[M], s_colq[M], pj);   // the objective row
         each<M / 8>([&](auto G) { if ((p >> 3) == (int)G) set8<8 * G>(&t[8 * G], pj, p); });   // row p := the pivot row
