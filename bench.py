@@ -146,7 +146,12 @@ def committed_traffic(key: dict):
             hits.append((os.path.relpath(path, ROOT), d["traffic_bytes_per_launch"]))
     if not hits:
         return None, None
-    src, val = sorted(hits)[-1]
+
+    def order(h):   # the latest run: profiles/rRRxx in the order the runs were named (r05z < r05aa)
+        import re
+        m = re.search(r"profiles/r(\d+)([a-z]*)", h[0].replace(os.sep, "/"))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (0, 0, "")
+    src, val = max(hits, key=order)
     return val, src
 
 
