@@ -210,17 +210,38 @@ __device__ __forceinline__ void ratio_defer_body(
     const int64_t ic = i < rows ? i : rows;   // clamped: loads need no guard
     double f[LEAN ? 1 : KMAX];
     if constexpr (!LEAN) {
+        // every step's load issued unconditionally from a selected row (clamped into the K rows of
+        // the arrays) and the unused ones dropped after: with the loads under `l < J` / `l < kp`
+        // branches hipcc waited for each load before the next (vmcnt(0) at every join), 16 round
+        // trips in a row at K = 16 (round 5)
 #pragma unroll
-        for (int l = 0; l < KMAX; ++l)
-            f[l] = (l < J) ? (l < kp ? Ccp[(int64_t)l * ldcc + ic] : Cc[(int64_t)(l - kp) * ldcc + ic]) : 0.0;
+        for (int l = 0; l < KMAX; ++l) {
+            const int lc = l - kp < (int)ldc - 1 ? l - kp : (int)ldc - 1;
+            const double* row = l < kp ? Ccp + (int64_t)l * ldcc : Cc + (int64_t)lc * ldcc;
+            const double v = row[ic];
+            f[l] = l < J ? v : 0.0;
+        }
     }
     auto fld = [&](int l) { return l < kp ? Ccp[(int64_t)l * ldcc + ic] : Cc[(int64_t)(l - kp) * ldcc + ic]; };
     double r_in = 0.0;
     int32_t nz_in = 0, bvar = 0;
-    if (i < rows && j > 0) nz_in = nzc[i];
-    if (i < rows_elig) {
-        r_in = J == 0 ? T[i * ld + ncols] : rhs[i];
-        bvar = basis[row_first + i];
+    if constexpr (!LEAN) {
+        // (as the coefficients above: unconditional loads from clamped rows, dropped where unused,
+        // so the three are in flight together instead of one round trip each)
+        const int64_t ir = i < rows ? i : (rows > 0 ? rows - 1 : 0);
+        const int64_t ie = i < rows_elig ? i : (rows_elig > 0 ? rows_elig - 1 : 0);
+        const int32_t nzv = nzc[ir];
+        const double rv = J == 0 ? T[ie * ld + ncols] : rhs[ie];
+        const int32_t bv = basis[rows_elig > 0 ? row_first + ie : 0];
+        nz_in = (i < rows && j > 0) ? nzv : 0;
+        r_in = i < rows_elig ? rv : 0.0;
+        bvar = i < rows_elig ? bv : 0;
+    } else {
+        if (i < rows && j > 0) nz_in = nzc[i];
+        if (i < rows_elig) {
+            r_in = J == 0 ? T[i * ld + ncols] : rhs[i];
+            bvar = basis[row_first + i];
+        }
     }
 
     PricePart acc = pp_empty();
