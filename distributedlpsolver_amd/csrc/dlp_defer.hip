@@ -210,38 +210,17 @@ __device__ __forceinline__ void ratio_defer_body(
     const int64_t ic = i < rows ? i : rows;   // clamped: loads need no guard
     double f[LEAN ? 1 : KMAX];
     if constexpr (!LEAN) {
-        // every step's load issued unconditionally from a selected row (clamped into the K rows of
-        // the arrays) and the unused ones dropped after: with the loads under `l < J` / `l < kp`
-        // branches hipcc waited for each load before the next (vmcnt(0) at every join), 16 round
-        // trips in a row at K = 16 (round 5)
 #pragma unroll
-        for (int l = 0; l < KMAX; ++l) {
-            const int lc = l - kp < (int)ldc - 1 ? l - kp : (int)ldc - 1;
-            const double* row = l < kp ? Ccp + (int64_t)l * ldcc : Cc + (int64_t)lc * ldcc;
-            const double v = row[ic];
-            f[l] = l < J ? v : 0.0;
-        }
+        for (int l = 0; l < KMAX; ++l)
+            f[l] = (l < J) ? (l < kp ? Ccp[(int64_t)l * ldcc + ic] : Cc[(int64_t)(l - kp) * ldcc + ic]) : 0.0;
     }
     auto fld = [&](int l) { return l < kp ? Ccp[(int64_t)l * ldcc + ic] : Cc[(int64_t)(l - kp) * ldcc + ic]; };
     double r_in = 0.0;
     int32_t nz_in = 0, bvar = 0;
-    if constexpr (!LEAN) {
-        // (as the coefficients above: unconditional loads from clamped rows, dropped where unused,
-        // so the three are in flight together instead of one round trip each)
-        const int64_t ir = i < rows ? i : (rows > 0 ? rows - 1 : 0);
-        const int64_t ie = i < rows_elig ? i : (rows_elig > 0 ? rows_elig - 1 : 0);
-        const int32_t nzv = nzc[ir];
-        const double rv = J == 0 ? T[ie * ld + ncols] : rhs[ie];
-        const int32_t bv = basis[rows_elig > 0 ? row_first + ie : 0];
-        nz_in = (i < rows && j > 0) ? nzv : 0;
-        r_in = i < rows_elig ? rv : 0.0;
-        bvar = i < rows_elig ? bv : 0;
-    } else {
-        if (i < rows && j > 0) nz_in = nzc[i];
-        if (i < rows_elig) {
-            r_in = J == 0 ? T[i * ld + ncols] : rhs[i];
-            bvar = basis[row_first + i];
-        }
+    if (i < rows && j > 0) nz_in = nzc[i];
+    if (i < rows_elig) {
+        r_in = J == 0 ? T[i * ld + ncols] : rhs[i];
+        bvar = basis[row_first + i];
     }
 
     PricePart acc = pp_empty();
@@ -599,26 +578,23 @@ __device__ __forceinline__ void prow_defer_body(
     constexpr int RING = RS;
     extern __shared__ double s_dyn[];
     auto s_ring = reinterpret_cast<double(*)[RING][128]>(s_dyn);
+    if (st->status != DLP_RUNNING) return;   // an earlier launch ended the solve
     // the selection: from the state (a launch of its own), or, in a one-launch pivot (peer
     // exchange), from the record the ratio workgroups of this launch publish (DevState::SelRec)
     SelView sv;
     if (onelaunch) {
-        if (st->status != DLP_RUNNING) return;   // an earlier launch ended the solve
         if (!sel_wait(xp, st, xseq, &sv, &s_sel, &s_selok)) {
             if (threadIdx.x == 0) const_cast<DevState*>(st)->status = kStatusXFail;   // (writable memory)
             return;
         }
         if (sv.status != DLP_RUNNING) return;
     } else {
-        // (the state's fields requested with its status, one scalar round trip)
-        const int32_t status0 = st->status;
         sv.status = DLP_RUNNING;
         sv.p_local = st->p_local;
         sv.blk = st->blk;
         sv.piv = st->piv;
         sv.zq = 0.0;
         sv.npivots = st->npivots;
-        if (status0 != DLP_RUNNING) return;   // an earlier launch ended the solve
     }
     const int64_t slot = sv.npivots - 1;
     if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 8);
@@ -647,20 +623,6 @@ __device__ __forceinline__ void prow_defer_body(
         if (owner_lane && S > L0)
 #pragma unroll
             for (int r = 0; r < RING; ++r) glds16(psrc(L0 + r), lds_addr(&s_ring[wv][(L0 + r) % RING][0]));
-    // the register replay (non-LEAN): chunks of CH pivot rows (row index clamped), double-buffered;
-    // the first chunk is requested here, before T0[p] and the step-table barrier (round 5: it was
-    // requested after them, one more round trip per pivot)
-    constexpr int CH = CHR;
-    d2 pa[LEAN ? 1 : CH], pb[LEAN ? 1 : CH];
-    auto fetch = [&](d2 (&pv)[LEAN ? 1 : CH], int l0) {
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int l = min(l0 + u, S - 1);
-            pv[u] = *(const d2*)((l < kp ? Pp + (int64_t)l * ld : P + (int64_t)(l - kp) * ld) + j);
-        }
-    };
-    if constexpr (!LEAN)
-        if (owner_lane && S > L0) fetch(pa, L0);
     // everything that depends only on (p, s) is requested before the step-table barrier:
     // T0[p][j..j+1] and, for the fused commit, the objective row and z_q
     d2 t0 = d2{0.0, 0.0}, zpre = d2{0.0, 0.0};
@@ -707,9 +669,19 @@ __device__ __forceinline__ void prow_defer_body(
         pr.y = t.y / piv;
     } else if (owner_lane) {
         d2 t = t0;
-        // the next chunk's loads are issued before this chunk is applied, so up to 2 CH rows are in
-        // flight (c3r8: the replay was 7 us per pivot with one chunk of 8 in flight, profiles/r04e/)
-        auto apply = [&](const d2 (&pv)[LEAN ? 1 : CH], int l0) {
+        // chunks of CH pivot rows (row index clamped), double-buffered: the next chunk's loads are
+        // issued before this chunk is applied, so up to 2 CH rows are in flight (c3r8: the replay
+        // was 7 us per pivot with one chunk of 8 in flight, profiles/r04e/)
+        constexpr int CH = CHR;
+        d2 pa[CH], pb[CH];
+        auto fetch = [&](d2 (&pv)[CH], int l0) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int l = min(l0 + u, S - 1);
+                pv[u] = *(const d2*)((l < kp ? Pp + (int64_t)l * ld : P + (int64_t)(l - kp) * ld) + j);
+            }
+        };
+        auto apply = [&](const d2 (&pv)[CH], int l0) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 const int l = l0 + u;
@@ -723,6 +695,7 @@ __device__ __forceinline__ void prow_defer_body(
                 }
             }
         };
+        if (S > L0) fetch(pa, L0);
         for (int l0 = L0; l0 < S; l0 += 2 * CH) {
             if (l0 + CH < S) fetch(pb, l0 + CH);
             apply(pa, l0);
