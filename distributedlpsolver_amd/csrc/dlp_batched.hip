@@ -616,6 +616,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
                             __builtin_amdgcn_readfirstlane((uint32_t)s_zm);
         double cq[M / 16];
         each<M / 16>([&](auto G) { cq[G] = s_colq[16 * G + (lane & 15)]; });
+        // (with them: the pivot, the objective row's entry and wave 0's row entry for its RHS update)
+        const double piv = s_piv, fM = s_colq[M];
+        const double fr = wid == 0 ? s_colq[lane] : 0.0;
         if (p < 0) {
             status = DLP_UNBOUNDED;
             break;
@@ -628,19 +631,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         // tp = t[p]: only the group of 8 rows holding p (a uniform branch per group)
         each<M / 8>([&](auto G) { if ((p >> 3) == (int)G) pick8<8 * G>(tp, &t[8 * G], p); });
         move_if_row<M>(tp, t[M], p);
-        const double pj = (ent ? 1.0 : tp) / s_piv;
+        const double pj = (ent ? 1.0 : tp) / piv;
         stamp(4);
         if (ent) each<R>([&](auto I) { t[I] = 0.0; });   // e_p before the pivot (see the LDS kernel)
         each<M / 8>([&](auto G) { elim8dpp<8 * G>(&t[8 * G], cq[G / 2], pj, zm); });
-        elim_row(t[M], s_colq[M], pj);   // the objective row
+        elim_row(t[M], fM, pj);   // the objective row
         each<M / 8>([&](auto G) { if ((p >> 3) == (int)G) set8<8 * G>(&t[8 * G], pj, p); });   // row p := the pivot row
         move_if_row<M>(t[M], pj, p);
         if (wid == 0) {   // the RHS of row `lane` and the objective value, as a column slot updates its rows
-            const double fr = s_colq[lane];
-            const double pjr = readlane_f64(rr, p) / s_piv;   // (p uniform)
+            const double pjr = readlane_f64(rr, p) / piv;   // (p uniform)
             const double v = __builtin_fma(-fr, pjr, rr);
             rr = lane == p ? pjr : (fr != 0.0 ? v : rr);
-            const double fz = s_colq[M];
+            const double fz = fM;
             if (fz != 0.0) zr = __builtin_fma(-fz, pjr, zr);
         }
         stamp(5);
