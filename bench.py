@@ -6,8 +6,10 @@ dense fp64 tableau (BASELINE.json metric), 1/2/4/8 MI355X.
                     [--step-unit block|pivot]
 
 What is timed: pivots of ONE LP whose tableau is resident in HBM, row-block
-partitioned over the N ranks (launched by torch.distributed.run for N > 1, one
-process per GPU, exchange over RCCL inside libdlp).  The LP is fixed as N
+partitioned over the N ranks (one process per GPU, exchange inside libdlp).  For
+N > 1 run it either under torch.distributed.run (WORLD_SIZE set) or plainly as
+`python3 bench.py --gpus N`: then bench.py starts its own N rank processes
+(launch_ranks) and relays rank 0's line.  The LP is fixed as N
 grows, so scaling is strong.  Default workload C3: m = n = 32768 (N = 65536,
 17.2 GB tableau), generated on the device (synthetic, seed 3 = config id).
 
@@ -102,7 +104,167 @@ def parse():
                     help="select block b+1 during the pass of block b: 1 on, 0 off, -1 auto")
     ap.add_argument("--pmc-dir", default=None,
                     help="rocprofv3 --pmc output dir (FETCH_SIZE / WRITE_SIZE) to fill roofline.traffic")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="--gpus N > 1 without a launcher: seconds the N rank processes may take in all "
+                         "before every one is killed and bench.py exits 124")
+    ap.add_argument("--launch-grace", type=float, default=30.0,
+                    help="--gpus N > 1 without a launcher: seconds the other ranks get to end on their own "
+                         "after one rank fails")
+    ap.add_argument("--stub-worker", default=None, choices=("ok", "fail1", "hang1"),
+                    help=argparse.SUPPRESS)   # tests/test_bench_launcher.py: a rank that does no GPU work
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------------------------
+# rank launcher: `python3 bench.py --gpus N` with no WORLD_SIZE in the environment starts its
+# own N rank processes (one per GPU), so the driver's scaling run works whether or not it goes
+# through torch.distributed.run.  The parent never touches the GPU (no torch.cuda, no libdlp):
+# it only spawns children (never an exec), relays rank 0's JSON line and reports failures.
+# ---------------------------------------------------------------------------------------------
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _die_with_parent():
+    """preexec_fn of a rank child: SIGKILL when the launcher dies (Linux PR_SET_PDEATHSIG), so a
+    killed launcher never leaves ranks on the GPUs.  Runs between fork and exec in the child; the
+    launcher has made no GPU call."""
+    try:
+        import ctypes
+        import signal
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGKILL))
+    except Exception:  # noqa: BLE001 - best effort: without it the launcher's own kill still runs
+        pass
+
+
+def launch_ranks(n, argv, timeout_s, grace_s=30.0, out=None, err=None):
+    """Start N rank processes of this script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT (127.0.0.1, a free port), wait for all of them, and return the exit code:
+    0 when every rank exited 0 and rank 0 printed a JSON line (relayed once to `out`), else the
+    first failing rank's code, 124 when the ranks outlived `timeout_s`, 1 when rank 0 printed no
+    line.  When one rank fails the others get `grace_s` to end on their own (an exchange timeout
+    ends a healthy rank in bounded time), then are terminated and killed by PID."""
+    import subprocess
+    import threading
+    out = out or sys.stdout
+    err = err or sys.stderr
+    port = _free_port()
+    script = os.path.abspath(__file__)
+    procs, lines, lock = [], [], threading.Lock()
+
+    def pump(r, stream):
+        for raw in stream:
+            s = raw.rstrip("\n")
+            parsed = None
+            if r == 0 and s.startswith("{"):
+                try:
+                    parsed = json.loads(s)
+                except ValueError:
+                    parsed = None
+            with lock:
+                if isinstance(parsed, dict) and "metric" in parsed:
+                    lines.append(s)
+                else:
+                    print(f"[rank {r}] {s}", file=err, flush=True)
+
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", NODE_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   DLP_BENCH_LAUNCHER="1")
+        p = subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env, stdout=subprocess.PIPE,
+                             stderr=None, text=True, preexec_fn=_die_with_parent)
+        procs.append(p)
+    pumps = [threading.Thread(target=pump, args=(r, p.stdout), daemon=True) for r, p in enumerate(procs)]
+    for t in pumps:
+        t.start()
+
+    def stop_all(why):
+        print(f"bench launcher: {why}; stopping ranks "
+              f"{[r for r, p in enumerate(procs) if p.poll() is None]}", file=err, flush=True)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.monotonic() + 10.0
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    import signal
+
+    def on_signal(signum, _frame):
+        stop_all(f"launcher got signal {signum}")
+        raise SystemExit(128 + signum)
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        deadline = time.monotonic() + timeout_s
+        first_fail, code = None, 0
+        while True:
+            codes = [p.poll() for p in procs]
+            if all(c is not None for c in codes):
+                break
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad and first_fail is None:
+                first_fail = time.monotonic()
+                code = bad[0][1]
+                print(f"bench launcher: rank {bad[0][0]} exited with {bad[0][1]}", file=err, flush=True)
+            if first_fail is not None and time.monotonic() - first_fail > grace_s:
+                stop_all(f"{grace_s:g} s after the first rank failure")
+                break
+            if time.monotonic() > deadline:
+                stop_all(f"ranks still running after {timeout_s:g} s (--launch-timeout)")
+                code = code or 124
+                break
+            time.sleep(0.1)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    for t in pumps:
+        t.join(timeout=5.0)
+    codes = [p.returncode for p in procs]
+    if code == 0:
+        code = next((c for c in codes if c != 0), 0)
+        if code < 0:   # killed by a signal
+            code = 128 - code
+    if code == 0 and not lines:
+        print("bench launcher: rank 0 printed no JSON line", file=err, flush=True)
+        code = 1
+    if code == 0:
+        print(lines[-1], file=out, flush=True)
+    else:
+        print(f"bench launcher: exit codes by rank {codes}", file=err, flush=True)
+    return code
+
+
+def stub_worker(args):
+    """--stub-worker (tests only): a rank that checks its launcher environment, joins a gloo
+    group over MASTER_ADDR:MASTER_PORT and all-gathers its rank, with no GPU work.  fail1: rank 1
+    exits 3 before the rendezvous; hang1: rank 1 sleeps."""
+    import torch
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    assert int(os.environ["LOCAL_RANK"]) == rank and world == args.gpus
+    if rank == 1 and args.stub_worker == "fail1":
+        raise SystemExit(3)
+    if rank == 1 and args.stub_worker == "hang1":
+        time.sleep(3600)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.zeros(world, dtype=torch.int64)
+    t[rank] = rank + 1000 * os.getpid()
+    dist.all_reduce(t)
+    if rank == 0:
+        print("stub rank 0 starting", flush=True)   # non-JSON output is relayed to stderr
+        print(json.dumps({"metric": "stub", "value": world, "ranks": [int(v) % 1000 for v in t],
+                          "pids": [int(v) // 1000 for v in t],
+                          "master": [os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"]]}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def pmc_traffic(pmc_dir: str, kernel_substr: str):
@@ -427,6 +589,13 @@ def c5_main(args):
         t = torch.tensor([wall, kern], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, kern = float(t[0].item()), float(t[1].item())
+        # the whole batch's outcome, not rank 0's slice: every rank optimal, pivots summed
+        a = torch.tensor([1 if allopt else 0], dtype=torch.int64, device="cuda")
+        dist.all_reduce(a, op=dist.ReduceOp.MIN)
+        allopt = bool(a.item())
+        pv = torch.tensor(piv, dtype=torch.int64, device="cuda")
+        dist.all_reduce(pv, op=dist.ReduceOp.SUM)
+        piv = [int(v) for v in pv.tolist()]
     occ = dlp.batched_occupancy(m, n, local)
     cus = torch.cuda.get_device_properties(local).multi_processor_count
     # single-LP serial latency: 256 LPs of the batch, one per CU
@@ -434,8 +603,8 @@ def c5_main(args):
     t1 = one.kernel_ms * 1e-3 / max(int(one.num_pivots.max()), 1)
     resident = min(nlp, occ["lps_per_cu"] * cus)
     peak = resident / t1   # pivots/s with every resident LP at the single-LP latency
-    achieved = piv[-1] * args.steps / kern
-    pivots_lp = piv[-1] / nlp
+    achieved = piv[-1] * args.steps / kern     # pivots of the whole batch (all ranks) per second
+    pivots_lp = piv[-1] / C5["nlp"]
     if rank == 0:
         total = C5["nlp"] * args.steps
         bytes_solve = 16.0 * C5["nlp"] * (m + 1) * (m + n + 1)   # one read + one write of every tableau
@@ -474,6 +643,11 @@ def c5_main(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here (before anything touches a GPU) and relay rank 0
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout, args.launch_grace))
+    if args.stub_worker:
+        return stub_worker(args)
     if args.workload == "c5":
         return c5_main(args)
     rank = int(os.environ.get("RANK", "0"))
