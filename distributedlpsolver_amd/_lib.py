@@ -153,6 +153,9 @@ SIGNATURES = [
     ("dlp_sessions_connect", C.c_int, [C.POINTER(_P), C.c_int]),
     ("dlp_session_exchange_handle", C.c_int, [_P, C.c_void_p]),
     ("dlp_session_connect_ipc", C.c_int, [_P, C.c_void_p]),
+    ("dlp_session_exchange_record", C.c_int, [_P, C.c_void_p]),
+    ("dlp_session_connect_records", C.c_int, [_P, C.c_void_p]),
+    ("dlp_session_colocated", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dlp_session_set_exchange", C.c_int, [_P, C.c_int]),
     ("dlp_session_get_exchange", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("dlp_session_exchange_reason", C.c_int, [_P, C.c_char_p, C.c_size_t]),

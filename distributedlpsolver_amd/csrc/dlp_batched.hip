@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -662,6 +664,76 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
 }  // namespace
 }  // namespace dlp
 
+// A device's batch context, reused across dlp_batched_solve calls: the stream,
+// the two timing events, the tableau buffer, one packed output buffer (objective | pivot count |
+// status per LP, read back in ONE copy through a pinned staging buffer), basis and log buffers,
+// each grown on demand and kept.  A fresh stream costs ~2 ms and the 7 allocations + frees ~1 ms
+// on MI355X, more than the 64 x 128 batch's 0.8 ms kernel.  One context per device, taken for the
+// whole call; a concurrent call on the same device builds and frees a private one as before.
+// dlp_release_cached_memory frees them (dlp::batched_release).
+namespace {
+struct BatchCtx {
+    int device = -1;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    void* dT = nullptr;   size_t capT = 0;
+    void* dOut = nullptr; size_t capOut = 0;
+    void* dB = nullptr;   size_t capB = 0;
+    void* dL = nullptr;   size_t capL = 0;
+    void* hOut = nullptr; size_t capH = 0;   // pinned
+    void free_all() {
+        if (device >= 0) (void)hipSetDevice(device);
+        if (s) (void)hipStreamSynchronize(s);
+        for (void* p : {dT, dOut, dB, dL})
+            if (p) (void)hipFree(p);
+        if (hOut) (void)hipHostFree(hOut);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (s) (void)hipStreamDestroy(s);
+        (void)hipGetLastError();
+        *this = BatchCtx{};
+    }
+};
+constexpr int kBatchDevs = 64;
+std::mutex g_batch_mu[kBatchDevs];
+BatchCtx g_batch[kBatchDevs];
+
+// grow *p to at least `bytes` (contents not kept)
+hipError_t ensure_buf(void** p, size_t* cap, size_t bytes, bool pinned = false) {
+    if (*cap >= bytes && *p) return hipSuccess;
+    if (*p) (void)(pinned ? hipHostFree(*p) : hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    const hipError_t e = pinned ? hipHostMalloc(p, bytes, hipHostMallocDefault) : hipMalloc(p, bytes);
+    if (e == hipSuccess) *cap = bytes;
+    return e;
+}
+
+// restores the caller's current device on every return path
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() { if (hipGetDevice(&dev) != hipSuccess) dev = -1; }
+    ~DeviceGuard() { if (dev >= 0) (void)hipSetDevice(dev); }
+};
+}  // namespace
+
+namespace dlp {
+// Free the cached batch contexts of `device` (-1: all); returns the device bytes freed.
+size_t batched_release(int device) {
+    size_t n = 0;
+    DeviceGuard g;
+    for (int d = 0; d < kBatchDevs; ++d) {
+        if (device >= 0 && d != device) continue;
+        std::lock_guard<std::mutex> lk(g_batch_mu[d]);
+        if (g_batch[d].device >= 0) {
+            n += g_batch[d].capT + g_batch[d].capOut + g_batch[d].capB + g_batch[d].capL;
+            g_batch[d].free_all();
+        }
+    }
+    return n;
+}
+}  // namespace dlp
+
 #define HIP_BTRY(expr)                                                               \
     do {                                                                             \
         hipError_t e_ = (expr);                                                      \
@@ -689,6 +761,7 @@ extern "C" int dlp_batched_occupancy(int64_t m, int64_t n, int device, int32_t* 
         dlp::set_error("no HIP device visible (libdlp has no CPU fallback)");
         return DLP_ERR_NODEVICE;
     }
+    DeviceGuard guard;   // the caller's current device is restored
     if (hipSetDevice(device) != hipSuccess) return DLP_ERR_HIP;
     int nb = 0, threads = 0;
     hipError_t e;
@@ -734,40 +807,54 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
         dlp::set_error("no HIP device visible (libdlp has no CPU fallback)");
         return DLP_ERR_NODEVICE;
     }
+    if (o.device < 0 || o.device >= ndev) {
+        dlp::set_error("dlp_batched_solve: no such device");
+        return DLP_ERR_ARG;
+    }
     if (lds > 160 * 1024) {
         dlp::set_error("dlp_batched_solve: tableau does not fit in 160 KiB of LDS");
         return DLP_ERR_UNSUPPORTED;
     }
-    double* dT = nullptr;
-    double* dObj = nullptr;
-    int32_t* dSt = nullptr;
-    int64_t* dNp = nullptr;
-    int32_t* dBasis = nullptr;
-    dlp_pivot* dLog = nullptr;
+    DeviceGuard guard;
+    BatchCtx priv;
+    BatchCtx* c = &priv;
+    std::unique_lock<std::mutex> lk;
+    if (o.device < kBatchDevs) {
+        lk = std::unique_lock<std::mutex>(g_batch_mu[o.device], std::try_to_lock);
+        if (lk.owns_lock()) c = &g_batch[o.device];
+    }
     uint64_t* dStamps = nullptr;
-    hipStream_t s = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
     dlp::BatchOut bo{};
+    const size_t bOut = (sizeof(double) + sizeof(int64_t) + sizeof(int32_t)) * (size_t)nlp;
+    double* dObj = nullptr;
+    int64_t* dNp = nullptr;
+    int32_t* dSt = nullptr;
+    const bool want_log = logs && log_cap > 0;
     HIP_BTRY(hipSetDevice(o.device));
-    HIP_BTRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    HIP_BTRY(hipMalloc(&dT, sizeof(double) * nlp * (m + 1) * ldg));
-    HIP_BTRY(hipMalloc(&dObj, sizeof(double) * nlp));
-    HIP_BTRY(hipMalloc(&dSt, sizeof(int32_t) * nlp));
-    HIP_BTRY(hipMalloc(&dNp, sizeof(int64_t) * nlp));
-    if (basis) HIP_BTRY(hipMalloc(&dBasis, sizeof(int32_t) * nlp * m));
-    if (logs && log_cap > 0) HIP_BTRY(hipMalloc(&dLog, sizeof(dlp_pivot) * nlp * log_cap));
-    HIP_BTRY(hipEventCreate(&e0));
-    HIP_BTRY(hipEventCreate(&e1));
+    c->device = o.device;
+    if (!c->s) HIP_BTRY(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
+    if (!c->e0) HIP_BTRY(hipEventCreate(&c->e0));
+    if (!c->e1) HIP_BTRY(hipEventCreate(&c->e1));
+    HIP_BTRY(ensure_buf(&c->dT, &c->capT, sizeof(double) * nlp * (m + 1) * ldg));
+    HIP_BTRY(ensure_buf(&c->dOut, &c->capOut, bOut));
+    HIP_BTRY(ensure_buf(&c->hOut, &c->capH, bOut, true));
+    if (basis) HIP_BTRY(ensure_buf(&c->dB, &c->capB, sizeof(int32_t) * nlp * m));
+    if (want_log) HIP_BTRY(ensure_buf(&c->dL, &c->capL, sizeof(dlp_pivot) * nlp * log_cap));
+    dObj = (double*)c->dOut;
+    dNp = (int64_t*)(dObj + nlp);
+    dSt = (int32_t*)(dNp + nlp);
     {
+        hipStream_t s = c->s;
+        double* dT = (double*)c->dT;
         dim3 gg((unsigned)((m + 1 + 3) / 4), (unsigned)nlp);
         dlp::batched_generate_kernel<<<gg, 256, 0, s>>>(dT, ldg, m, n, kind, seed);
         HIP_BTRY(hipGetLastError());
         bo.objective = dObj;
         bo.status = dSt;
         bo.npivots = dNp;
-        bo.basis = dBasis;
-        bo.logs = dLog;
-        bo.log_cap = dLog ? log_cap : 0;
+        bo.basis = basis ? (int32_t*)c->dB : nullptr;
+        bo.logs = want_log ? (dlp_pivot*)c->dL : nullptr;
+        bo.log_cap = want_log ? log_cap : 0;
         static const char* stamp_file = std::getenv("DLP_BATCH_STAMPS");
         if (stamp_file) {
             HIP_BTRY(hipMalloc(&dStamps, sizeof(uint64_t) * 64 * 8));
@@ -782,7 +869,7 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
         if (!reg)
             HIP_BTRY(hipFuncSetAttribute((const void*)dlp::batched_solve_kernel,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        HIP_BTRY(hipEventRecord(e0, s));
+        HIP_BTRY(hipEventRecord(c->e0, s));
         if (reg) {
             if (nw == 1)
                 dlp::batched_reg_kernel<64, 1><<<(unsigned)nlp, 64, 0, s>>>(dT, ldg, (int)n, o.max_pivots, o.pricing,
@@ -800,19 +887,28 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
                 dT, ldg, (int)m, (int)n, o.max_pivots, o.pricing, o.tol_dj, o.tol_piv, bo);
         }
         HIP_BTRY(hipGetLastError());
-        HIP_BTRY(hipEventRecord(e1, s));
+        HIP_BTRY(hipEventRecord(c->e1, s));
+        // read back only what the caller asked for: the packed outputs it wants in one copy
+        // (objective | pivot counts | status are contiguous), basis and logs when requested
+        const bool wo = objective != nullptr, wn = npivots != nullptr, ws = status != nullptr;
+        if (wo || wn || ws) {
+            const size_t from = wo ? 0 : wn ? sizeof(double) * nlp : (sizeof(double) + sizeof(int64_t)) * nlp;
+            const size_t to = ws ? bOut : wn ? (sizeof(double) + sizeof(int64_t)) * nlp : sizeof(double) * nlp;
+            HIP_BTRY(hipMemcpyAsync((char*)c->hOut + from, (char*)c->dOut + from, to - from,
+                                    hipMemcpyDeviceToHost, s));
+        }
+        if (basis) HIP_BTRY(hipMemcpyAsync(basis, c->dB, sizeof(int32_t) * nlp * m, hipMemcpyDeviceToHost, s));
+        if (want_log)
+            HIP_BTRY(hipMemcpyAsync(logs, c->dL, sizeof(dlp_pivot) * nlp * log_cap, hipMemcpyDeviceToHost, s));
         HIP_BTRY(hipStreamSynchronize(s));
         if (kernel_ms) {
             float ms = 0.f;
-            HIP_BTRY(hipEventElapsedTime(&ms, e0, e1));
+            HIP_BTRY(hipEventElapsedTime(&ms, c->e0, c->e1));
             *kernel_ms = ms;
         }
-        if (objective) HIP_BTRY(hipMemcpy(objective, dObj, sizeof(double) * nlp, hipMemcpyDeviceToHost));
-        if (status) HIP_BTRY(hipMemcpy(status, dSt, sizeof(int32_t) * nlp, hipMemcpyDeviceToHost));
-        if (npivots) HIP_BTRY(hipMemcpy(npivots, dNp, sizeof(int64_t) * nlp, hipMemcpyDeviceToHost));
-        if (basis) HIP_BTRY(hipMemcpy(basis, dBasis, sizeof(int32_t) * nlp * m, hipMemcpyDeviceToHost));
-        if (dLog)
-            HIP_BTRY(hipMemcpy(logs, dLog, sizeof(dlp_pivot) * nlp * log_cap, hipMemcpyDeviceToHost));
+        if (wo) std::memcpy(objective, c->hOut, sizeof(double) * nlp);
+        if (wn) std::memcpy(npivots, (char*)c->hOut + sizeof(double) * nlp, sizeof(int64_t) * nlp);
+        if (ws) std::memcpy(status, (char*)c->hOut + (sizeof(double) + sizeof(int64_t)) * nlp, sizeof(int32_t) * nlp);
         if (dStamps) {   // diagnostics only
             std::vector<uint64_t> h(64 * 8);
             HIP_BTRY(hipMemcpy(h.data(), dStamps, sizeof(uint64_t) * 64 * 8, hipMemcpyDeviceToHost));
@@ -823,10 +919,7 @@ extern "C" int dlp_batched_solve(int kind, int64_t nlp, int64_t m, int64_t n, ui
         }
     }
 done:
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-    for (void* p : {(void*)dT, (void*)dObj, (void*)dSt, (void*)dNp, (void*)dBasis, (void*)dLog, (void*)dStamps})
-        if (p) (void)hipFree(p);
-    if (s) (void)hipStreamDestroy(s);
+    if (dStamps) (void)hipFree(dStamps);
+    if (rc != DLP_OK || c == &priv) c->free_all();   // a failed context is rebuilt next call
     return rc;
 }

@@ -313,4 +313,7 @@ hipError_t launch_generate(const Geometry& g, int kind, int64_t m, int64_t n, ui
 hipError_t launch_gather_column(const double* T, int64_t ld, int64_t nrows, int64_t col,
                                 double* out, hipStream_t s);
 
+// dlp_batched.hip: free the cached dlp_batched_solve contexts of `device` (-1: all); bytes freed
+size_t batched_release(int device);
+
 }  // namespace dlp

@@ -175,6 +175,9 @@ struct dlp_session {
     std::vector<std::pair<void*, size_t>> pooled;
     bool pool_ok = true;   // false once the stream failed: its buffers are freed, not pooled
     int chain_cus = 0;     // lookahead: CUs of the chain's stream (0 = unmasked; chain_cus_policy)
+    // ranks of this session's exchange on its device (itself included) and this rank's index among
+    // them, from the device of every rank the peer connect saw (install_peers); 1 / 0 otherwise
+    int coloc_n = 1, coloc_i = 0;
 };
 
 extern "C" int flush_pending(dlp_session* s);   // defined with the C entry points
@@ -593,27 +596,43 @@ int ratio_threads_policy(const dlp_session* s) {
 // best n moves: c3r4 128 (20.6 k), c3r2 64 (13.9-14.3 k), c3r8 128 (profiles/r04ah/).  Auto: 128
 // CUs for the chain up to 8,192 local rows, 64 below 32,768, at most half the CUs, 0 (no masks)
 // from 32,768; DLP_CHAIN_CUS=n overrides (0 = off).
+// Ranks that share a device (several rank processes or rank sessions on one GPU: install_peers
+// learns it from the devices of the connected ranks) split that budget into disjoint slices, one
+// per rank, the pass of each on the CUs no chain uses: with one shared mask the spinning chain
+// workgroups of the waiting ranks filled those CUs and the owner's could not be placed (3+ rank
+// processes on one GPU hit the exchange timeout, profiles/r05w/).  A slice under 32 CUs (mask
+// bits act in groups of 32) turns the masks off for those ranks.  Returns this rank's slice.
 int chain_cus_policy(const dlp_session* s) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 64)
         return 0;
+    int n = 0;
     if (const char* e = std::getenv("DLP_CHAIN_CUS")) {
-        const int n = std::atoi(e);
-        return n > 0 && n < cus ? n : 0;
+        n = std::atoi(e);
+        n = n > 0 && n < cus ? n : 0;
+    } else if (s->rows < 32768) {
+        // (mask bits act in groups of 32: 112 and 128 chain bits, or 144 and 160, give the pass the
+        // same time, profiles/r04ah/)
+        n = std::min(s->rows > 8192 ? 64 : 128, cus / 2);
     }
-    // (mask bits act in groups of 32: 112 and 128 chain bits, or 144 and 160, give the pass the
-    // same time, profiles/r04ah/)
-    if (s->rows >= 32768) return 0;
-    return std::min(s->rows > 8192 ? 64 : 128, cus / 2);
+    const int nco = std::max(1, s->coloc_n);
+    if (n <= 0 || nco == 1) return n;
+    const int slice = n / nco / 32 * 32;
+    return slice >= 32 ? slice : 0;
 }
 
-// Put the chain's stream on the top n CU-mask bits (n = 0: an unmasked stream at the chain's
-// priority), and name the pass's stream key accordingly (acquired by the caller).  Results do not
-// depend on where a kernel runs.
+// Put the chain's stream on n CU-mask bits (n = 0: an unmasked stream at the chain's priority) —
+// the top n, or with ranks sharing the device this rank's slice of the top coloc_n x n — and name
+// the pass's stream key accordingly (the bits below every chain slice; acquired by the caller).
+// Results do not depend on where a kernel runs.
 int chain_cus_apply(dlp_session* s, int n) {
-    if (n == s->chain_cus) return DLP_OK;
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess) cus = 256;
+    const int nco = std::max(1, s->coloc_n);
+    if (n > 0 && n * nco > cus) n = 0;   // (chain_cus_policy never asks for more)
+    const int first = cus - n * (s->coloc_i + 1);
+    if (n == s->chain_cus && s->stream && (n == 0 || s->prio_chain == kMaskedKey + (first << 10) + n))
+        return DLP_OK;
     HIP_TRY(hipStreamSynchronize(s->stream));
     if (s->pstream) {
         HIP_TRY(hipStreamSynchronize(s->pstream));
@@ -624,12 +643,8 @@ int chain_cus_apply(dlp_session* s, int n) {
     s->stream = nullptr;
     int lo = 0, hi = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    // (tests: DLP_TEST_CHAIN_CU_FIRST puts the chain's n CUs at another first bit, so that rank
-    // processes sharing one GPU get disjoint chain CUs: tests/test_gpu_ranks.py)
-    int first = cus - n;
-    if (const char* e = std::getenv("DLP_TEST_CHAIN_CU_FIRST")) first = std::max(0, std::min(std::atoi(e), cus - n));
     s->prio_chain = n > 0 ? kMaskedKey + (first << 10) + n : hi;
-    s->prio_pass = n > 0 ? kMaskedKey + (cus - n) : lo;
+    s->prio_pass = n > 0 ? kMaskedKey + (cus - n * nco) : lo;
     if (n > 0 && acquire_stream(s->device, s->prio_chain, &s->stream) != hipSuccess) {
         (void)hipGetLastError();   // no CU-masked queue here: both streams unmasked, as before round 4
         s->stream = nullptr;
@@ -639,6 +654,19 @@ int chain_cus_apply(dlp_session* s, int n) {
     }
     if (!s->stream) HIP_TRY(acquire_stream(s->device, s->prio_chain, &s->stream));
     s->chain_cus = n;
+    return DLP_OK;
+}
+
+// The lookahead's two streams on the split chain_cus_policy asks for (re-applied when the exchange
+// changes what it asks for: a peer connect that finds ranks sharing the device).
+int la_streams(dlp_session* s) {
+    CALL_TRY(chain_cus_apply(s, chain_cus_policy(s)));   // releases the pass stream when the split changes
+    if (!s->pstream && acquire_stream(s->device, s->prio_pass, &s->pstream) != hipSuccess) {
+        (void)hipGetLastError();   // no CU-masked queue for the pass: back to unmasked streams
+        s->pstream = nullptr;
+        CALL_TRY(chain_cus_apply(s, 0));
+        HIP_TRY(acquire_stream(s->device, s->prio_pass, &s->pstream));
+    }
     return DLP_OK;
 }
 
@@ -695,15 +723,7 @@ int la_enable(dlp_session* s, bool forced) {
         HIP_TRY(pool_alloc(s, s->device, (void**)&s->band_cnt, sizeof(uint32_t) * 2 * s->band_stride));
     }
     HIP_TRY(hipMemsetAsync(s->band_cnt, 0, sizeof(uint32_t) * 2 * s->band_stride, s->stream));
-    if (!s->pstream) {
-        CALL_TRY(chain_cus_apply(s, chain_cus_policy(s)));
-        if (acquire_stream(s->device, s->prio_pass, &s->pstream) != hipSuccess) {
-            (void)hipGetLastError();   // no CU-masked queue for the pass: back to unmasked streams
-            s->pstream = nullptr;
-            CALL_TRY(chain_cus_apply(s, 0));
-            HIP_TRY(acquire_stream(s->device, s->prio_pass, &s->pstream));
-        }
-    }
+    CALL_TRY(la_streams(s));
     if (!s->ev_seal) HIP_TRY(hipEventCreateWithFlags(&s->ev_seal, hipEventDisableTiming));
     if (!s->ev_pass) HIP_TRY(hipEventCreateWithFlags(&s->ev_pass, hipEventDisableTiming));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1135,13 +1155,24 @@ int flush_pending_block(dlp_session* s) {
 // where the chain gets CUs of its own (chain_cus_policy > 0: a rank of up to 32k rows): RCCL's
 // collective kernels need more registers than the pass leaves on a CU and would each wait for pass
 // workgroups to drain, but on a disjoint CU mask they never share a CU with the pass
-// (round 5; profiles/r05*/).  A caller's explicit lookahead setting is kept.
+// (round 5; profiles/r05*/).  That RCCL case is measured and tested only on a
+// 1-rank communicator (bench.py --workload c3r8, test_rccl_rank_session_lookahead_on_cu_split):
+// RCCL collectives on a CU-masked chain stream beside the pass across real ranks have never run,
+// and RCCL is the path a multi-GPU run falls back to, so with nranks > 1 it is opt-in
+// (DLP_RCCL_LOOKAHEAD=1).  A caller's explicit lookahead setting is kept.
+bool rccl_lookahead_ok(const dlp_session* s) {
+    if (s->nranks == 1) return true;
+    const char* e = std::getenv("DLP_RCCL_LOOKAHEAD");
+    return e && std::atoi(e) == 1;
+}
+
 int la_policy(dlp_session* s) {
     if (!s->la_auto || !s->exchange) return DLP_OK;
-    const bool rccl_split = s->xmode == dlp_session::X_RCCL && chain_cus_policy(s) > 0;
+    const bool rccl_split = s->xmode == dlp_session::X_RCCL && rccl_lookahead_ok(s) && chain_cus_policy(s) > 0;
     const bool want = (s->xmode == dlp_session::X_PEER || rccl_split) && s->d.K == 64 && s->streaming &&
                       !s->general;
     if (want && !s->la) CALL_TRY(la_enable(s, false));
+    if (s->la && s->pstream) CALL_TRY(la_streams(s));   // (the split may have changed with the exchange)
     // RCCL beside the pass only on a CU split that really exists (a masked queue may be refused)
     if (s->la && s->xmode == dlp_session::X_RCCL && s->chain_cus == 0) CALL_TRY(la_disable(s));
     if (!want && s->la) CALL_TRY(la_disable(s));
@@ -1878,12 +1909,15 @@ int solve_in_process_once(const dlp_problem* prob, const dlp_options& o, int P, 
 // (a device wait that never completes, a fault in a cross-device store) is rerun from the start
 // over RCCL on fresh sessions, as bench.py's measure_with_fallback does: the peer
 // path's cross-device stores have run only on one-GPU boxes so far.  The result records the
-// exchange that produced it and why (dlp_result_exchange).
+// exchange that produced it and why (dlp_result_exchange).  Only an exchange failure is rerun
+// (DLP_ERR_RCCL: a peer wait that timed out or was aborted, kStatusXFail, or the window limit);
+// OOM, state, HIP and argument errors are deterministic or fatal and are returned unchanged
+// (ADVICE r05).
 int solve_in_process(const dlp_problem* prob, const dlp_options& o, int P, dlp_result** out) {
     bool peer = false;
     std::string why;
     const int rc = solve_in_process_once(prob, o, P, out, &peer, &why);
-    if (rc == DLP_OK || !peer || o.exchange != DLP_XCHG_DEFAULT || rc == DLP_ERR_ARG || rc == DLP_ERR_NODEVICE)
+    if (rc != DLP_ERR_RCCL || !peer || o.exchange != DLP_XCHG_DEFAULT)
         return rc;
     const std::string first = dlp_last_error();
     dlp_options o2 = o;
@@ -1952,8 +1986,17 @@ uint64_t xwait_ticks(double stall_limit_s) {
     return stall_limit_s > 0 ? (uint64_t)((stall_limit_s + 5.0) * 1e8) : 0;
 }
 
-// Install the peer table (bases[r] = rank r's block as this device addresses it).
-int install_peers(dlp_session* s, const std::vector<uint64_t*>& bases) {
+// Install the peer table (bases[r] = rank r's block as this device addresses it).  devs[r]: the
+// device ordinal (in this process) of rank r, -1 where unknown (dlp_session_connect_ipc's bare
+// handles): ranks on this session's device share its CUs (coloc_n / coloc_i, chain_cus_policy).
+int install_peers(dlp_session* s, const std::vector<uint64_t*>& bases, const std::vector<int>& devs) {
+    s->coloc_n = 0;
+    s->coloc_i = 0;
+    for (int r = 0; r < s->nranks; ++r)
+        if (r == s->rank || (r < (int)devs.size() && devs[r] == s->device)) {
+            ++s->coloc_n;
+            if (r < s->rank) ++s->coloc_i;
+        }
     dlp::XPeers& x = s->xpeers_host;
     (void)dlp::xblock_layout(s->nranks, s->ld, xslots(s, &x), &x);
     for (int r = 0; r < dlp::kMaxRanks; ++r) x.base[r] = r < (int)bases.size() ? bases[r] : nullptr;
@@ -1987,7 +2030,7 @@ int connect_ipc(dlp_session* s, const uint8_t* handles) {
         s->ipc_open.push_back(p);
         bases[r] = (uint64_t*)p;
     }
-    CALL_TRY(install_peers(s, bases));
+    CALL_TRY(install_peers(s, bases, {}));
     return la_policy(s);
 }
 
@@ -2030,6 +2073,84 @@ int comm_allgather(dlp_session* s, const void* mine, void* all, size_t bytes) {
     return rc;
 }
 
+// This rank's half of a peer connect from every rank's record: each other rank's device (by its
+// PCI bus id, mapped to this process's ordinals), peer access to it, its block opened.  On a
+// failure out->ok = 0 with the reason in out->why and nothing left open.
+void open_peer_blocks(dlp_session* s, XRec* all, XRec* out, std::vector<void*>* opened,
+                      std::vector<uint64_t*>* bases, std::vector<int>* devs) {
+    bases->assign(s->nranks, nullptr);
+    devs->assign(s->nranks, -1);
+    (*devs)[s->rank] = s->device;
+    for (int r = 0; r < s->nranks && out->ok; ++r) {
+        if (r == s->rank) {
+            (*bases)[r] = s->xblk;
+            continue;
+        }
+        int dev = -1, can = 0;
+        all[r].bus[sizeof(all[r].bus) - 1] = 0;
+        if (hipDeviceGetByPCIBusId(&dev, all[r].bus) != hipSuccess || dev < 0) {
+            (void)hipGetLastError();
+            std::snprintf(out->why, sizeof(out->why), "rank %d's device %s is not visible to this process",
+                          r, all[r].bus);
+            out->ok = 0;
+            break;
+        }
+        (*devs)[r] = dev;
+        if (dev != s->device && (hipDeviceCanAccessPeer(&can, s->device, dev) != hipSuccess || !can)) {
+            (void)hipGetLastError();
+            std::snprintf(out->why, sizeof(out->why), "device %d cannot access device %d (rank %d)", s->device,
+                          dev, r);
+            out->ok = 0;
+            break;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, all[r].handle, sizeof(h));
+        void* p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            std::snprintf(out->why, sizeof(out->why), "hipIpcOpenMemHandle of rank %d's block: %s", r,
+                          hipGetErrorString(e));
+            out->ok = 0;
+            break;
+        }
+        opened->push_back(p);
+        (*bases)[r] = (uint64_t*)p;
+    }
+    if (!out->ok) {
+        for (void* p : *opened) (void)hipIpcCloseMemHandle(p);
+        opened->clear();
+    }
+}
+
+// This rank's record: its exchange block's IPC handle and its device's PCI bus id (ok = 0 with the
+// reason when either cannot be had).  DLP_TEST_PEER_FAIL=<rank> (tests only) makes that rank fail.
+void make_xrec(dlp_session* s, XRec* me) {
+    *me = XRec{};
+    me->ok = 1;
+    auto fail = [&](const std::string& w) {
+        if (!me->ok) return;
+        me->ok = 0;
+        std::snprintf(me->why, sizeof(me->why), "%s", w.c_str());
+    };
+    if (const char* e = std::getenv("DLP_TEST_PEER_FAIL"))
+        if (std::atoi(e) == s->rank) fail("injected (DLP_TEST_PEER_FAIL)");
+    if (me->ok && ensure_xblock(s) != DLP_OK) fail(std::string("exchange block: ") + dlp_last_error());
+    if (me->ok) {
+        hipIpcMemHandle_t h;
+        if (hipIpcGetMemHandle(&h, s->xblk) != hipSuccess) {
+            (void)hipGetLastError();
+            fail("hipIpcGetMemHandle of the exchange block failed");
+        } else {
+            std::memcpy(me->handle, &h, sizeof(h));
+        }
+    }
+    if (hipDeviceGetPCIBusId(me->bus, (int)sizeof(me->bus), s->device) != hipSuccess) {
+        (void)hipGetLastError();
+        fail("hipDeviceGetPCIBusId failed");
+    }
+}
+
 // Owner-rooted peer exchange over the communicator, agreed by every rank: each rank makes its
 // block and IPC handle, the records are all-gathered, each rank checks peer access to every
 // other rank's device and opens their blocks, and a second all-gather agrees on the outcome.
@@ -2037,29 +2158,8 @@ int comm_allgather(dlp_session* s, const void* mine, void* all, size_t bytes) {
 // not; other errors are failures of the communicator itself.  DLP_TEST_PEER_FAIL=<rank>
 // (tests only) makes that rank report a failure.
 int peer_connect_collective(dlp_session* s, std::string* why) {
-    XRec me{};
-    me.ok = 1;
-    auto fail = [&](const std::string& w) {
-        if (!me.ok) return;
-        me.ok = 0;
-        std::snprintf(me.why, sizeof(me.why), "%s", w.c_str());
-    };
-    if (const char* e = std::getenv("DLP_TEST_PEER_FAIL"))
-        if (std::atoi(e) == s->rank) fail("injected (DLP_TEST_PEER_FAIL)");
-    if (me.ok && ensure_xblock(s) != DLP_OK) fail(std::string("exchange block: ") + dlp_last_error());
-    if (me.ok) {
-        hipIpcMemHandle_t h;
-        if (hipIpcGetMemHandle(&h, s->xblk) != hipSuccess) {
-            (void)hipGetLastError();
-            fail("hipIpcGetMemHandle of the exchange block failed");
-        } else {
-            std::memcpy(me.handle, &h, sizeof(h));
-        }
-    }
-    if (hipDeviceGetPCIBusId(me.bus, (int)sizeof(me.bus), s->device) != hipSuccess) {
-        (void)hipGetLastError();
-        fail("hipDeviceGetPCIBusId failed");
-    }
+    XRec me;
+    make_xrec(s, &me);
     std::vector<XRec> all(s->nranks);
     CALL_TRY(comm_allgather(s, &me, all.data(), sizeof(XRec)));
     for (int r = 0; r < s->nranks; ++r)
@@ -2071,55 +2171,22 @@ int peer_connect_collective(dlp_session* s, std::string* why) {
     XRec me2{};
     me2.ok = 1;
     std::vector<void*> opened;
-    std::vector<uint64_t*> bases(s->nranks, nullptr);
-    for (int r = 0; r < s->nranks && me2.ok; ++r) {
-        if (r == s->rank) {
-            bases[r] = s->xblk;
-            continue;
-        }
-        int dev = -1, can = 0;
-        all[r].bus[sizeof(all[r].bus) - 1] = 0;
-        if (hipDeviceGetByPCIBusId(&dev, all[r].bus) != hipSuccess || dev < 0) {
-            (void)hipGetLastError();
-            std::snprintf(me2.why, sizeof(me2.why), "rank %d's device %s is not visible to this process",
-                          r, all[r].bus);
-            me2.ok = 0;
-            break;
-        }
-        if (dev != s->device && (hipDeviceCanAccessPeer(&can, s->device, dev) != hipSuccess || !can)) {
-            (void)hipGetLastError();
-            std::snprintf(me2.why, sizeof(me2.why), "device %d cannot access device %d (rank %d)", s->device,
-                          dev, r);
-            me2.ok = 0;
-            break;
-        }
-        hipIpcMemHandle_t h;
-        std::memcpy(&h, all[r].handle, sizeof(h));
-        void* p = nullptr;
-        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            std::snprintf(me2.why, sizeof(me2.why), "hipIpcOpenMemHandle of rank %d's block: %s", r,
-                          hipGetErrorString(e));
-            me2.ok = 0;
-            break;
-        }
-        opened.push_back(p);
-        bases[r] = (uint64_t*)p;
-    }
+    std::vector<uint64_t*> bases;
+    std::vector<int> devs;
+    open_peer_blocks(s, all.data(), &me2, &opened, &bases, &devs);
     std::vector<XRec> all2(s->nranks);
     const int rc = comm_allgather(s, &me2, all2.data(), sizeof(XRec));
     int bad = -1;
     for (int r = 0; r < s->nranks && rc == DLP_OK && bad < 0; ++r)
         if (!all2[r].ok) bad = r;
     if (rc != DLP_OK || bad >= 0) {
-        for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+        for (void* p : opened) (void)hipIpcCloseMemHandle(p);   // (nothing is open when me2.ok == 0)
         if (rc != DLP_OK) return rc;
         *why = "rank " + std::to_string(bad) + ": " + std::string(all2[bad].why, strnlen(all2[bad].why, sizeof(all2[bad].why)));
         return DLP_ERR_UNSUPPORTED;
     }
     s->ipc_open.insert(s->ipc_open.end(), opened.begin(), opened.end());
-    return install_peers(s, bases);
+    return install_peers(s, bases, devs);
 }
 
 // A communicator session's exchange: `mode` DLP_XCHG_RCCL, DLP_XCHG_PEER (an error when the
@@ -2811,10 +2878,12 @@ int dlp_sessions_connect(dlp_session* const* ranks, int nranks) {
         }
     std::vector<uint64_t*> bases(nranks);
     for (int r = 0; r < nranks; ++r) bases[r] = by[r]->xblk;
+    std::vector<int> devs(nranks);
+    for (int r = 0; r < nranks; ++r) devs[r] = by[r]->device;
     for (dlp_session* s : by) {
         HIP_TRY(hipSetDevice(s->device));
         HIP_TRY(hipStreamSynchronize(s->stream));
-        CALL_TRY(install_peers(s, bases));
+        CALL_TRY(install_peers(s, bases, devs));
         CALL_TRY(la_policy(s));
     }
     return DLP_OK;
@@ -2827,6 +2896,58 @@ int dlp_session_exchange_handle(dlp_session* s, void* out64) {
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipIpcGetMemHandle(&h, s->xblk));
     std::memcpy(out64, &h, sizeof(h));
+    return DLP_OK;
+}
+
+int dlp_session_exchange_record(dlp_session* s, void* out256) {
+    if (!s || !out256) return DLP_ERR_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    XRec me;
+    make_xrec(s, &me);
+    if (!me.ok) {
+        set_error(std::string("dlp_session_exchange_record: ") + std::string(me.why, strnlen(me.why, sizeof(me.why))));
+        return DLP_ERR_UNSUPPORTED;
+    }
+    static_assert(sizeof(XRec) == DLP_XREC_BYTES, "XRec is the exchange record");
+    std::memcpy(out256, &me, sizeof(me));
+    return DLP_OK;
+}
+
+int dlp_session_connect_records(dlp_session* s, const void* records) {
+    if (!s || !records) return DLP_ERR_ARG;
+    if (!s->ipc_open.empty() || s->xmode == dlp_session::X_PEER) {
+        set_error("dlp_session_connect_records: already connected");
+        return DLP_ERR_STATE;
+    }
+    CALL_TRY(ensure_xblock(s));
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    std::vector<XRec> all(s->nranks);
+    std::memcpy(all.data(), records, sizeof(XRec) * s->nranks);
+    for (int r = 0; r < s->nranks; ++r)
+        if (!all[r].ok) {
+            set_error("dlp_session_connect_records: rank " + std::to_string(r) + " has no record");
+            return DLP_ERR_ARG;
+        }
+    XRec out{};
+    out.ok = 1;
+    std::vector<void*> opened;
+    std::vector<uint64_t*> bases;
+    std::vector<int> devs;
+    open_peer_blocks(s, all.data(), &out, &opened, &bases, &devs);
+    if (!out.ok) {
+        set_error(std::string("peer exchange unavailable: ") + std::string(out.why, strnlen(out.why, sizeof(out.why))));
+        return DLP_ERR_UNSUPPORTED;
+    }
+    s->ipc_open.insert(s->ipc_open.end(), opened.begin(), opened.end());
+    CALL_TRY(install_peers(s, bases, devs));
+    return la_policy(s);
+}
+
+int dlp_session_colocated(dlp_session* s, int* n, int* index) {
+    if (!s || !n || !index) return DLP_ERR_ARG;
+    *n = s->coloc_n;
+    *index = s->coloc_i;
     return DLP_OK;
 }
 
@@ -3151,7 +3272,7 @@ int dlp_result_timings(const dlp_result* r, double* ms_out) {
     return DLP_OK;
 }
 int dlp_release_cached_memory(int device, int64_t* bytes) {
-    const size_t n = pool_drain(device < 0 ? kAllDevices : device);
+    const size_t n = pool_drain(device < 0 ? kAllDevices : device) + dlp::batched_release(device);
     if (bytes) *bytes = (int64_t)n;
     return DLP_OK;
 }

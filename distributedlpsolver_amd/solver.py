@@ -29,6 +29,8 @@ def _dptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
 
+XREC_BYTES = 256   # include/dlp.h DLP_XREC_BYTES
+
 class Problem:
     """An LP owned by libdlp: dense / random / ad-allocation problems are
     max c^T x s.t. A x <= b, x >= 0 (b >= 0); general problems
@@ -365,6 +367,27 @@ class Session:
             raise ValueError("connect_ipc needs nranks 64-byte handles")
         buf = C.create_string_buffer(raw, len(raw))
         L.check(L.lib().dlp_session_connect_ipc(self._h, buf), "dlp_session_connect_ipc")
+
+    def exchange_record(self) -> bytes:
+        """This rank's 256-B exchange record: its block's IPC handle and its device's PCI bus id."""
+        buf = C.create_string_buffer(XREC_BYTES)
+        L.check(L.lib().dlp_session_exchange_record(self._h, buf), "dlp_session_exchange_record")
+        return buf.raw
+
+    def connect_records(self, records) -> None:
+        """Every rank's exchange_record(), in rank order (gathered by the caller): the peer connect
+        that also learns which ranks share this session's device (their chains get disjoint CUs)."""
+        raw = b"".join(records)
+        if len(raw) != XREC_BYTES * self.nranks:
+            raise ValueError("connect_records needs nranks 256-byte records")
+        buf = C.create_string_buffer(raw, len(raw))
+        L.check(L.lib().dlp_session_connect_records(self._h, buf), "dlp_session_connect_records")
+
+    def colocated(self) -> tuple[int, int]:
+        """(ranks of this exchange on this session's device, this rank's index among them)."""
+        n, i = C.c_int(), C.c_int()
+        L.check(L.lib().dlp_session_colocated(self._h, C.byref(n), C.byref(i)), "dlp_session_colocated")
+        return n.value, i.value
 
     def set_exchange(self, mode: int) -> None:
         """L.XCHG_RCCL or L.XCHG_PEER (PEER over a communicator: an all-gather of IPC handles)."""

@@ -187,9 +187,12 @@ int         dlp_candidate_select(const dlp_candidate* cands, int n, int* winner)
 int64_t     dlp_tableau_ld(int64_t m, int64_t n);   /* roundup(N+1,16); sessions may pad more */
 int         dlp_update_variants(void);               /* number of rank-1 update variants */
 /* Sessions return their small buffers (<= 32 MiB each, <= 512 MiB in all) and streams to a
- * per-process cache for the next session.  This frees the cached buffers of `device`
- * (-1: every device and the pinned host buffers); *bytes (may be NULL) = bytes freed.  An
- * allocation that fails frees its device's cached buffers and retries by itself. */
+ * per-process cache for the next session, and dlp_batched_solve keeps one context per device
+ * (stream, events, tableau / output buffers sized by the largest batch so far).  This frees the
+ * cached buffers and batch contexts of `device` (-1: every device and the pinned host buffers);
+ * *bytes (may be NULL) = device bytes freed.  A session allocation that fails frees its device's
+ * cached session buffers and retries by itself; that hipFree may synchronise the device, so it
+ * waits for work other sessions have in flight on it (call this between runs to avoid that). */
 int         dlp_release_cached_memory(int device, int64_t* bytes);
 
 /* ---- problems ------------------------------------------------------------ */
@@ -371,6 +374,18 @@ int dlp_session_get_lookahead(dlp_session* s, int* on);
 int dlp_sessions_connect(dlp_session* const* ranks, int nranks);
 int dlp_session_exchange_handle(dlp_session* s, void* out64);
 int dlp_session_connect_ipc(dlp_session* s, const void* handles /* nranks x 64 B, rank order */);
+/* The same connect from records that also carry each rank's device (PCI bus id): ranks that
+ * share a device then split the lookahead's chain CUs into disjoint slices (dlp_session_chain_cus;
+ * slices under 32 CUs turn the masks off for those ranks), which several rank processes on one
+ * GPU need.  dlp_session_exchange_record fills DLP_XREC_BYTES (the exchange
+ * block's IPC handle, the bus id); the caller all-gathers them in rank order.  The RCCL-agreed
+ * connect (dlp_session_set_exchange / DLP_XCHG_DEFAULT) all-gathers the same records itself.
+ * dlp_session_colocated: ranks of the session's exchange on its device (itself included) and its
+ * index among them (1, 0 before a connect and after dlp_session_connect_ipc). */
+#define DLP_XREC_BYTES 256
+int dlp_session_exchange_record(dlp_session* s, void* out /* DLP_XREC_BYTES */);
+int dlp_session_connect_records(dlp_session* s, const void* records /* nranks x DLP_XREC_BYTES, rank order */);
+int dlp_session_colocated(dlp_session* s, int* n, int* index);
 int dlp_session_set_exchange(dlp_session* s, int mode);
 int dlp_session_get_exchange(dlp_session* s, int* mode);
 /* Why an auto exchange (DLP_XCHG_DEFAULT) fell back to RCCL ("" when it did not). */

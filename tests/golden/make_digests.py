@@ -24,9 +24,13 @@ for the GPU to reproduce.  Run in the build container (CPU only):
   rank_split  bench.py's c3r4 LP (8192 x 57344 seed 34) split over 2 processes of
       4,096 rows (the per-process rank path, tests/test_gpu_ranks.py): per-rank block
       digests, objective row, log and basis at 136 / 200 / 264 pivots.
-  rank_split_c3  C3 itself (32768 x 32768 seed 3) split over 2, 4 and 8 processes (the
-      rank geometries of the N = 2, 4, 8 scaling runs): the same digests at 136 / 200
-      pivots, with the block digests of each split ("blocks": {"2": [...], "4": [...], "8": [...]}).
+  rank_split_c3  C3 itself (32768 x 32768 seed 3) split over 2, 3, 4 and 8 processes (the
+      rank geometries of the N = 2, 4, 8 scaling runs, and a ragged 3-way split of 10,922 /
+      10,923 / 10,923 rows): the same digests at 136 / 200 pivots, with the block digests of
+      each split ("blocks": {"2": [...], "3": [...], "4": [...], "8": [...]}).
+  c4_degen_2048x4096  C4's large degenerate LP (2048 x 4096 seed 4, degenerate family: b_i = 0
+      on half the rows, Bland after every degenerate pivot): whole-tableau, log, basis and
+      objective digests at 500 and 2,000 pivots, plus the degenerate-pivot count.
 
 The digests hash little-endian fp64 / int32 bytes of the oracle's outputs
 (tests/oracle_py.py), so the GPU side compares bit for bit."""
@@ -134,6 +138,26 @@ def rank_split(m=8192, n=57344, seed=34, P=2, stops=(136, 200, 264), Ps=None):
     return out
 
 
+def c4_degen(m=2048, n=4096, seed=4, stops=(500, 2000)):
+    """the 50%-zero-RHS degenerate LP at 2,048 x 4,096, the
+    size the small-LP launch does not cover (auto: the deferred K = 16 path).  Whole-tableau
+    digests (all 2,049 rows, objective row last, each its first `width` doubles) at each stop."""
+    t0 = time.time()
+    w = ((n + m + 1) + 15) // 16 * 16
+    out = {"m": m, "n": n, "seed": seed, "degenerate": True, "width": w, "stops": {}}
+
+    def at(k, T, log, basis):
+        rec = {"log_sha256": sha(log), "basis_sha256": sha(basis), "tableau_sha256": tableau_sha(T, w),
+               "objective_hex": float(log[-1]["objective"]).hex(),
+               "degenerate_pivots": int((log["ratio"] == 0.0).sum()),
+               "oracle_seconds": time.time() - t0}
+        out["stops"][str(k)] = rec
+        print(k, rec, flush=True)
+
+    O.run_generated_stops(m, n, seed, list(stops), at, degenerate=True, nthreads=os.cpu_count() or 8)
+    return out
+
+
 C5_SHAPES = [(64, 64), (64, 128)]
 
 
@@ -183,7 +207,8 @@ def main():
     for w in which:
         d[w] = {"c2": c2, "c3": c3, "c3_k64": lambda: c3(C3_K64_PIVOTS), "c3_tableau": c3_tableau,
                 "c5": c5, "rank_split": rank_split,
-                "rank_split_c3": lambda: rank_split(32768, 32768, 3, P=2, stops=(136, 200), Ps=(2, 4, 8))}[w]()
+                "rank_split_c3": lambda: rank_split(32768, 32768, 3, P=2, stops=(136, 200), Ps=(2, 3, 4, 8)),
+                "c4_degen_2048x4096": c4_degen}[w]()
         with open(OUT, "w") as f:
             json.dump(d, f, indent=1)
         print(w, json.dumps(d[w]), flush=True)

@@ -192,6 +192,36 @@ def test_c2_full_solve_digest(lookahead):
     assert _sha(res.basis) == g["basis_sha256"]
 
 
+@pytest.mark.parametrize("split", ["stops", "ragged"])
+def test_c4_degenerate_2048x4096_digest(split):
+    """C4's large degenerate LP (2,048 x 4,096, half the RHS zero)
+    through the auto path at this size (deferred K = 16: the tableau is 100 MB, above the small-LP
+    launch and below lookahead), against the oracle's committed stops (tests/golden/make_digests.py
+    c4_degen_2048x4096): pivot log, basis, objective bits and the WHOLE tableau (2,049 rows).  Every
+    pivot of these windows is degenerate (r_p = 0), so each one exercises Bland after a degenerate
+    pivot and the exact-tie rule of the ratio test.  "ragged": windows that end inside K = 16 blocks."""
+    g = load_golden("digests.json")["c4_degen_2048x4096"]
+    stops = sorted(int(k) for k in g["stops"])
+    with dlp.Session(dlp.Problem.random(g["m"], g["n"], g["seed"], degenerate=True),
+                     check_interval=97, max_pivots=stops[-1] + 1) as s:
+        assert s.update_stats()[2] == 16 and not s.lookahead() and not s.small_lp()
+        total = 0
+        for k in stops:
+            windows = [k - total] if split == "stops" else [(k - total) // 3 + 5, k - total - ((k - total) // 3 + 5)]
+            for w in windows:
+                st, done = s.run(w)
+                assert st == L.RUNNING and done == w
+                total += w
+            want = g["stops"][str(k)]
+            res = s.result()
+            assert len(res.pivot_log) == k
+            assert _sha(res.pivot_log) == want["log_sha256"]
+            assert int((res.pivot_log["ratio"] == 0.0).sum()) == want["degenerate_pivots"]
+            assert _sha(res.basis) == want["basis_sha256"]
+            assert float(res.objective).hex() == want["objective_hex"]
+            assert tableau_sha256([s], g["width"]) == want["tableau_sha256"]
+
+
 @pytest.mark.parametrize("m,n", [(64, 64), (64, 128)])
 def test_c5_full_batch(m, n):
     """4,096 independent LPs (C5; BASELINE.json: 64 x 128): EVERY LP of the batch against the

@@ -61,10 +61,6 @@ def _rank_worker(rank, world, port, g, windows, env, q):
     windows on its own stream), checked against the oracle's stops after each window."""
     import torch.distributed as dist
     os.environ.update(env)
-    if "CHAIN_SLICE" in env:   # this rank's chain on CUs no other rank process's chain uses
-        n = int(env["CHAIN_SLICE"])
-        os.environ["DLP_CHAIN_CUS"] = str(n)
-        os.environ["DLP_TEST_CHAIN_CU_FIRST"] = str(256 - n * (rank + 1))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -75,12 +71,15 @@ def _rank_worker(rank, world, port, g, windows, env, q):
         s = dlp.Session(dlp.Problem.random(g["m"], g["n"], g["seed"]), rank=rank, nranks=world,
                         defer=0, lookahead=la, check_interval=64 * 20, log_pivots=1,
                         max_pivots=sum(windows) + 2)
+        # the records carry each rank's device (PCI bus id), so the library sees that the ranks
+        # share this GPU and gives each chain a CU slice of its own (chain_cus_policy)
         hs = [None] * world
-        dist.all_gather_object(hs, s.exchange_handle())
-        s.connect_ipc(hs)
+        dist.all_gather_object(hs, s.exchange_record())
+        s.connect_records(hs)
         s.set_exchange_timeout(60.0)
         out["config"] = {"exchange": s.get_exchange(), "lookahead": s.lookahead(),
-                         "chain_cus": s.chain_cus(), "defer_tuning": s.get_defer_tuning(),
+                         "chain_cus": s.chain_cus(), "colocated": s.colocated(),
+                         "defer_tuning": s.get_defer_tuning(),
                          "rows": s.rows, "row_first": s.row_first, "ld": s.ld}
         dist.barrier()
         total = 0
@@ -137,8 +136,9 @@ def _run_two(windows, env, timeout=240, key="rank_split", world=None):
 
 @pytest.mark.parametrize("case", ["default", "chain_cus_0", "no_lookahead", "ratio64"])
 def test_two_process_rank_path(case):
-    """default: the shipped auto policy (K = 64, lookahead on with the peer exchange, 128
-    chain CUs, form 21 + band publication, two-launch peer pivot), 136 pivots (two full
+    """default: the shipped auto policy (K = 64, lookahead on with the peer exchange, the 128
+    chain CUs of a 4,096-row rank split into two disjoint 64-CU slices because both processes
+    share this GPU, form 21 + band publication, two-launch peer pivot), 136 pivots (two full
     blocks + 8) then a 64-pivot window that ends inside a block (200), then 64 more (264);
     chain_cus_0: DLP_CHAIN_CUS=0 (chain and pass unmasked); no_lookahead: lookahead = 0
     (the form-23 LDS-ring pass in place); ratio64: 64-lane ratio workgroups (65 candidate slots
@@ -149,21 +149,21 @@ def test_two_process_rank_path(case):
     g, out = _run_two(windows, env)
     for o in out:
         cfg = o["config"]
-        assert cfg["exchange"] == L.XCHG_PEER
+        assert cfg["exchange"] == L.XCHG_PEER and cfg["colocated"] == (2, o["rank"])
         assert cfg["rows"] == g["m"] // g["P"] and cfg["row_first"] == o["rank"] * g["m"] // g["P"]
         assert cfg["defer_tuning"][2] == 64
         if case == "no_lookahead":
             assert not cfg["lookahead"] and cfg["defer_tuning"][1] == 23
         else:
             assert cfg["lookahead"] and cfg["defer_tuning"][1] == 21
-            assert cfg["chain_cus"] == (0 if case == "chain_cus_0" else 128)
+            assert cfg["chain_cus"] == (0 if case == "chain_cus_0" else 64)
         assert [d for _, d in o["runs"]] == windows
         assert set(o["checks"]) == {str(k) for k in np.cumsum(windows)}
         for k, got in o["checks"].items():
             assert all(got.values()), (o["rank"], k, got)
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_c3_rank_processes(world):
     """The rank geometries of the N = 2, 4 and 8 scaling runs, each rank its own process on this
     one GPU: C3 itself (32,768 x 32,768 seed 3, bench.py's default LP) split into 2 x 16,384 rows
@@ -171,21 +171,25 @@ def test_c3_rank_processes(world):
     4 x 8,192 (128-lane ratio workgroups, form 23, the register pivot-row kernel of a chain on CUs
     of its own) or 8 x 4,096 (the same with the form-21 pass), with lookahead and the two-launch
     peer pivot; 136 pivots (two full blocks + 8; N = 2: then 64 more, ending inside a block)
-    against the oracle's stops (tests/golden/make_digests.py rank_split_c3).
-    Four or eight processes on one GPU: each rank's chain on 32 CUs of its own
-    (DLP_TEST_CHAIN_CU_FIRST) instead of all on the same top 128 — with the shared mask their
-    spinning chain workgroups fill those CUs and starve the owner's (3+ processes,
-    profiles/r05w/; on N GPUs each chain has its GPU's CUs to itself)."""
+    against the oracle's stops (tests/golden/make_digests.py rank_split_c3); world 3 is a ragged
+    split (10,922 / 10,923 / 10,923 rows).
+    All processes share this one GPU, under the default environment: the library learns that from
+    the exchange records (each rank's PCI bus id) and gives each rank's chain a disjoint CU slice
+    of its budget (2 x 32 of 64 at P = 2, 4 x 32 of 128 at P = 4), or no masks where a slice would
+    be under 32 CUs (P = 3: 64 / 3, P = 8: 128 / 8).  With one shared mask the spinning chain
+    workgroups of the waiting ranks filled those CUs and starved the owner's (3+ processes,
+    profiles/r05w/); on N GPUs each rank is alone on its device and keeps the whole budget."""
     windows = [136, 64] if world == 2 else [136]
-    env = {} if world == 2 else {"CHAIN_SLICE": "32"}
-    g, out = _run_two(windows, env, timeout=420, key="rank_split_c3", world=world)
-    rows = g["m"] // world
+    g, out = _run_two(windows, {}, timeout=420, key="rank_split_c3", world=world)
+    want_cus = {2: 32, 3: 0, 4: 32, 8: 0}[world]
     for o in out:
         cfg = o["config"]
+        first, last = o["rank"] * g["m"] // world, (o["rank"] + 1) * g["m"] // world
         assert cfg["exchange"] == L.XCHG_PEER and cfg["lookahead"]
-        assert cfg["rows"] == rows and cfg["row_first"] == o["rank"] * rows
-        assert cfg["defer_tuning"][1:] == (23 if rows > 4096 else 21, 64)
-        assert cfg["chain_cus"] == (64 if world == 2 else 32)
+        assert cfg["colocated"] == (world, o["rank"])
+        assert cfg["rows"] == last - first and cfg["row_first"] == first
+        assert cfg["chain_cus"] == want_cus
+        assert cfg["defer_tuning"][1:] == (23 if (want_cus > 0 and cfg["rows"] > 4096) else 21, 64)
         assert [d for _, d in o["runs"]] == windows
         assert set(o["checks"]) == {str(k) for k in np.cumsum(windows)}
         for k, got in o["checks"].items():

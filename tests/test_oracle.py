@@ -190,6 +190,28 @@ def test_c5_batch_digests_reproduce():
     assert h.hexdigest() == g["log64_sha256"]
 
 
+def test_c4_degen_digest_reproduces():
+    """tests/golden/digests.json c4_degen_2048x4096 (the GPU test checks the whole tableau against
+    it): the oracle re-run here to the first stop gives the committed digests."""
+    import hashlib
+    g = load_golden("digests.json")["c4_degen_2048x4096"]
+    first = min(int(k) for k in g["stops"])
+    want = g["stops"][str(first)]
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    got = {}
+
+    def at(k, T, log, basis):
+        h = hashlib.sha256()
+        for r in range(0, T.shape[0], 512):
+            h.update(np.ascontiguousarray(T[r:r + 512, :g["width"]]).tobytes())
+        got.update(log=sha(log), basis=sha(basis), tableau=h.hexdigest(), obj=float(log[-1]["objective"]).hex(),
+                   degen=int((log["ratio"] == 0.0).sum()))
+
+    O.run_generated_stops(g["m"], g["n"], g["seed"], [first], at, degenerate=True, nthreads=8)
+    assert got == {"log": want["log_sha256"], "basis": want["basis_sha256"], "tableau": want["tableau_sha256"],
+                   "obj": want["objective_hex"], "degen": want["degenerate_pivots"]}
+
+
 @pytest.mark.parametrize("m,n,seed,K,k,degen", [(150, 170, 4, 16, 10 ** 6, False), (150, 170, 4, 64, 10 ** 6, False),
                                                 (96, 128, 6, 7, 10 ** 6, True), (300, 420, 11, 64, 200, False),
                                                 (300, 420, 11, 1, 77, False)])
