@@ -736,8 +736,11 @@ def main():
     launches, upd_total_ms, _ = sess.update_stats()
     variant, rb_used, nt_used = sess.get_tuning()
     form = sess.defer_form() if K > 1 else None
-    ld_used = sess.ld
-    rows_local, N1 = sess.rows, sess.ncols + 1
+    # the tableau as stored: the condensed tableau keeps the n nonbasic columns
+    # + the RHS (the m basic columns are unit vectors the rule never changes)
+    condensed = bool(getattr(sess, "condensed", False))
+    ld_used = sess.storage_ld if condensed else sess.ld
+    rows_local, N1 = sess.rows, (sess.storage_ncols if condensed else sess.ncols) + 1
     upd_ms = upd_total_ms / max(launches, 1)   # per update-kernel launch (rank-1, or rank-K pass)
     # algorithmic bytes of one launch: one read + one write of every resident element
     # (the deferred pass skips the objective row, kept current by the pivot-row kernel)
@@ -811,6 +814,8 @@ def main():
         geo = {"workload": args.workload, "kernel": kind, "K": K, "form": form,
                "rows_per_block": rb_used, "nontemporal": nt_used, "ld": ld_used,
                "rows_local": rows_local}
+        if condensed:
+            geo["condensed"] = True
         if args.pmc_dir:
             traffic, traffic_src = pmc_traffic(args.pmc_dir, ksub), f"live: {args.pmc_dir}"
         elif world == 1:
@@ -838,6 +843,9 @@ def main():
             "config": {"workload": desc, "m": m, "n": n, "N": m + n, "ld": ld_used, "seed": seed,
                        "rows_per_rank": rows_local, "parallelism": f"rowblock{world}",
                        "pricing": "dantzig->bland on degeneracy", "pivots_per_tableau_pass": K,
+                       "tableau": (f"condensed: {N1 - 1} nonbasic columns + RHS stored per row (the {m} basic "
+                                   f"columns are unit vectors, DESIGN.md §16)" if condensed else
+                                   f"full: {N1} columns per row"),
                        "step": (f"{per_step} pivots + their rank-{K} tableau pass" if per_step > 1
                                 else "one pivot"),
                        "lookahead": lookahead_on},
@@ -869,6 +877,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": bytes_launch,
+                         "bytes_model": ("16 * rows_local * (stored columns): one read + one write of every "
+                                         "stored element" + ("; condensed tableau, n + 1 columns" if condensed else
+                                                             "")),
                          "kernel": (f"rank-1 update variant {variant} (rows/band {rb_used}, "
                                     f"nt {nt_used}, ld {ld_used})" if K == 1 else
                                     f"rank-{K} tableau pass, form {form} (rows/band {rb_used}, "

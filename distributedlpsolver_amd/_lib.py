@@ -55,6 +55,7 @@ class Options(C.Structure):
         ("n_gpus", C.c_int32),
         ("lookahead", C.c_int32),
         ("exchange", C.c_int32),
+        ("condensed", C.c_int32),
     ]
 
 
@@ -156,6 +157,7 @@ SIGNATURES = [
     ("dlp_session_exchange_record", C.c_int, [_P, C.c_void_p]),
     ("dlp_session_connect_records", C.c_int, [_P, C.c_void_p]),
     ("dlp_session_colocated", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("dlp_session_storage", C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
     ("dlp_session_set_exchange", C.c_int, [_P, C.c_int]),
     ("dlp_session_get_exchange", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("dlp_session_exchange_reason", C.c_int, [_P, C.c_char_p, C.c_size_t]),

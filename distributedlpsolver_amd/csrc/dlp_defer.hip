@@ -150,7 +150,7 @@ __device__ __forceinline__ void ratio_defer_body(
     dlp_pivot* log, int64_t log_cap, int nblocks, const double* __restrict__ Ccp = nullptr,
     const double* __restrict__ Pp = nullptr, int prev_seal = -1, const XPeers* xp = nullptr,
     uint32_t xseq = 0, uint32_t* bcnt = nullptr, int brb = 1, int bnt = 0, const double* Tn = nullptr,
-    int xsel = 0, uint32_t rseq = 0) {
+    int xsel = 0, uint32_t rseq = 0, Cond cd = Cond{}) {
     __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
     __shared__ Cand lds_c[kRatioDeferThreads / 64];
     __shared__ int s_last;
@@ -244,15 +244,35 @@ __device__ __forceinline__ void ratio_defer_body(
     }
 
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 1);
+    // condensed tableau: q's slot, and the step (of the replayed sequence: sealed steps first) at
+    // which that slot restarted from the unit vector of its new variable (R < 0: none replayed here)
+    // (the LCH = 8 tuning instance has no condensed build: its 32 VGPRs are full; the launcher
+    // never picks it for a condensed session)
+    int32_t sq = q, R = -1;
+    if (!(LEAN && LCH == 8) && cd.on) {
+        sq = __builtin_amdgcn_readfirstlane(cd.slot_of[q]);
+        if (sq < 0 || sq >= ncols) {   // (an invariant: a priced variable is nonbasic) — never fault
+            if constexpr (RING) vmwait<0>();
+            if (blockIdx.x == 0 && threadIdx.x == 0) st->status = DLP_ERR_STATE;
+            return;
+        }
+        const int32_t rv = __builtin_amdgcn_readfirstlane(cd.rst[sq]);
+        if (rv >= 0) {
+            if ((rv >> 7) == st->bser)
+                R = kp + (rv & 127);
+            else if (kp > 0 && (rv >> 7) == st->seal[prev_seal].ser)
+                R = rv & 127;
+        }
+    }
     // T0[i][q] is requested before the P[l][q] loads and their barrier: both wait only for q
     double a = 0.0;
     if (wdone)   // sc1 load (the pass stored Tn write-through)
-        a = __builtin_bit_cast(double, __hip_atomic_load((const uint64_t*)(Tn + i * ld + q), __ATOMIC_RELAXED,
+        a = __builtin_bit_cast(double, __hip_atomic_load((const uint64_t*)(Tn + i * ld + sq), __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT));
     else if (i <= rows)
-        a = T[i * ld + q];
+        a = T[i * ld + sq];
     for (int l = threadIdx.x; l < J; l += blockDim.x)
-        s_pq[l] = l < kp ? Pp[(int64_t)l * ld + q] : P[(int64_t)(l - kp) * ld + q];
+        s_pq[l] = l < kp ? Pp[(int64_t)l * ld + sq] : P[(int64_t)(l - kp) * ld + sq];
     __syncthreads();
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 2);
 
@@ -263,7 +283,9 @@ __device__ __forceinline__ void ratio_defer_body(
         // the LDS reads of a pair's two steps issue together instead of one per branch
         // (ok = false: a pair's second step past J-1, read from the tables' spare entries and
         // dropped: l <= J <= KMAX - 1)
+        // (condensed: at step R the slot's new column starts from the unit vector, +0 here)
         auto step = [&](int l, double fv, bool ok) {
+            if (l == R) a = 0.0;   // (uniform; the objective row's lane reloads z_q below)
             const double pq = s_pq[l];
             const bool piv = i == s_pl[l];
             const double u = __builtin_fma(-fv, pq, a);
@@ -284,14 +306,20 @@ __device__ __forceinline__ void ratio_defer_body(
             // no step replayed (first selection of a block on a finished band): the RHS cache
             // still advances by the sealed block's last step
             if (npairs == 0 && J > 0) flast = Ccp[(int64_t)(kp - 1) * ldcc + i];
+            // (condensed: the restart step zeroed every lane of the wave; the objective row is
+            // never replayed, its z_q is current)
+            if (R >= L0 && i == rows) a = T[i * ld + sq];
         }
         if (blockIdx.x == 0) CHAIN_STAMP(slot, 3);
     } else if constexpr (LEAN) {
         // LCH coefficient loads per round trip (the register budget of this kernel), from the
         // first step not applied to the row's source (L0: a published band starts after the
         // sealed block); the next chunk's loads are issued before this chunk is applied
+        // (condensed: a restart of q's slot at R >= L0 starts the replay there from +0)
+        const int Ls = R >= L0 ? R : L0;
+        if (R >= L0 && i < rows) a = 0.0;
         if (i < rows && J > L0 && !DB) {   // one chunk at a time (LEAN's 32 VGPRs)
-            for (int l0 = L0; l0 < J; l0 += LCH) {
+            for (int l0 = Ls; l0 < J; l0 += LCH) {
                 double fq[LCH];
 #pragma unroll
                 for (int u = 0; u < LCH; ++u) fq[u] = l0 + u < J ? fld(l0 + u) : 0.0;
@@ -328,8 +356,8 @@ __device__ __forceinline__ void ratio_defer_body(
                     }
                 }
             };
-            fetch(fa, L0);
-            for (int l0 = L0; l0 < J; l0 += 2 * LCH) {
+            fetch(fa, Ls);
+            for (int l0 = Ls; l0 < J; l0 += 2 * LCH) {
                 if (l0 + LCH < J) fetch(fb, l0 + LCH);
                 apply(fa, l0);
                 if (l0 + LCH >= J) break;
@@ -347,6 +375,7 @@ __device__ __forceinline__ void ratio_defer_body(
 #pragma unroll
                 for (int l = 0; l < KMAX; ++l) {
                     if (l < J) {
+                        if (l == R) a = 0.0;
                         if (i == s_pl[l])
                             a = s_pq[l];
                         else if (f[l] != 0.0)
@@ -414,8 +443,9 @@ __device__ __forceinline__ void ratio_defer_body(
         if (threadIdx.x == 0) {
             // one-launch pivot: z_q (the objective row is current; this launch's commit writes it
             // only after the record) before the selection, which writes the log entry's other fields
-            const double zq = xsel == 2 ? T[rows * ld + q] : 0.0;
-            do_select(st, w, q, basis, row_first, rows, pricing, log, log_cap, true, xsel != 2);
+            const double zq = xsel == 2 ? T[rows * ld + sq] : 0.0;
+            st->sq = sq;
+            do_select(st, w, q, basis, row_first, rows, pricing, log, log_cap, true, xsel != 2, cd);
             if (xsel == 2) sel_publish(st, rseq, st->status, zq);
         }
         if constexpr (LEAN) CHAIN_STAMP(slot, 6);
@@ -449,14 +479,15 @@ __device__ __forceinline__ void ratio_defer_body(
     if (threadIdx.x == 0) {
         st->ticket = 0;
         st->q = q;
+        st->sq = sq;
         if (nranks == 1)
-            do_select(st, best, q, basis, row_first, rows, pricing, log, log_cap, true);
+            do_select(st, best, q, basis, row_first, rows, pricing, log, log_cap, true, true, cd);
         else if (xp)
             x_push_cand(xp, xseq, best);   // peer exchange: straight into every rank's slot
         else
             cand_out[0] = best;
         if constexpr (FUSED) {
-            st->zq = T[rows * ld + q];   // the objective row is current; nobody writes it yet
+            st->zq = T[rows * ld + sq];   // the objective row is current; nobody writes it yet
             release_go(st);
         }
     }
@@ -472,11 +503,11 @@ __global__ __launch_bounds__(kRatioDeferThreads) void ratio_defer_kernel(
     const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
-    int prev_seal, const XPeers* xp, uint32_t xseq, int xsel) {
+    int prev_seal, const XPeers* xp, uint32_t xseq, int xsel, Cond cd) {
     ratio_defer_body<KMAX, false>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                   ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                   tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
-                                  xp, xseq, nullptr, 1, 0, nullptr, xsel);
+                                  xp, xseq, nullptr, 1, 0, nullptr, xsel, 0, cd);
 }
 
 // MID (round 5): beside the MFMA pass (form 22 leaves 104 VGPRs per SIMD), the replay's
@@ -490,11 +521,11 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
     int prev_seal, const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn,
-    int xsel) {
+    int xsel, Cond cd) {
     ratio_defer_body<KMAX, false, true, LCH, kRatioRingPairs, true>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                              ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                              tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
-                                             xp, xseq, bcnt, brb, bnt, Tn, xsel);
+                                             xp, xseq, bcnt, brb, bnt, Tn, xsel, 0, cd);
 }
 
 // The LEAN selection kernel, held to 32 VGPRs (lookahead at K = 64, beside the pass).
@@ -507,11 +538,11 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
     Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
     dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
     int prev_seal, const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn,
-    int xsel) {
+    int xsel, Cond cd) {
     ratio_defer_body<KMAX, false, true, LCH, RP>(T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C,
                                         ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                         tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
-                                        xp, xseq, bcnt, brb, bnt, Tn, xsel);
+                                        xp, xseq, bcnt, brb, bnt, Tn, xsel, 0, cd);
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
@@ -519,29 +550,44 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
 // Same per-element operations as the eager update kernel's objective band.
 // ZQ: 0 = z_q from C[rows][s]; 1 = the caller's early loads of T[rows][j..j+1] (zpre) and z_q
 // (zqv); 2 = z_q given (zqv: the selection record of a one-launch pivot), z loaded here
+// Condensed tableau (cd.on): slot sq is the entering variable's, now the leaving variable's: its
+// objective entry restarts from +0 (a basic column's), its restart is recorded (rst, block
+// serial bser, step s) and its entries of the block's earlier pivot rows become +0 (the pass
+// starts the slot from the unit vector written by reset_cols); pricing by variable (var_of).
 template <int ZQ = 0>
 __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols,
                                   int64_t nprice, int64_t klog, const double* __restrict__ C,
                                   int64_t ldc, double* __restrict__ P, int s, int64_t j, d2 pr,
                                   PricePart* pp, int tile, double tol_dj, dlp_pivot* log, int64_t log_cap,
-                                  PricePart* lds_pp, d2 zpre = d2{0.0, 0.0}, double zqv = 0.0) {
+                                  PricePart* lds_pp, d2 zpre = d2{0.0, 0.0}, double zqv = 0.0,
+                                  Cond cd = Cond{}, int32_t sq = -1, int32_t bser = 0) {
     const int64_t width = (ncols + 16) & ~(int64_t)15;
+    const bool rx = cd.on && j == sq, ry = cd.on && j + 1 == sq;
     if (j < ld) {
         *(d2*)(P + (int64_t)s * ld + j) = pr;
         if (s == 0)   // block start: pivot rows 1..K-1 := +0 (see the ratio kernel's C tails)
             for (int64_t l = 1; l < ldc; ++l) *(d2*)(P + l * ld + j) = d2{0.0, 0.0};
+        if (rx || ry) {
+            for (int l = 0; l < s; ++l) P[(int64_t)l * ld + sq] = 0.0;
+            cd.rst[sq] = (bser << 7) | s;
+        }
     }
     const double zq = ZQ == 0 ? C[rows * ldc + s] : zqv;
     PricePart acc = pp_empty();
     if (j < width) {
         double* zp = T + rows * ld + j;
         d2 z = ZQ == 1 ? zpre : *(const d2*)zp;
+        if (rx) z.x = 0.0;
+        if (ry) z.y = 0.0;
         if (zq != 0.0) {
             z.x = __builtin_fma(-zq, pr.x, z.x);
             z.y = __builtin_fma(-zq, pr.y, z.y);
-            *(d2*)zp = z;
         }
-        price_pair(acc, z.x, z.y, j, nprice, tol_dj);
+        if (zq != 0.0 || rx || ry) *(d2*)zp = z;
+        if (cd.on)
+            price_pair_var(acc, z.x, z.y, cd.var_of[j], cd.var_of[j + 1], tol_dj);
+        else
+            price_pair(acc, z.x, z.y, j, nprice, tol_dj);
         if (log && j <= ncols && ncols < j + 2) {
             if (klog >= 0 && klog < log_cap) log[klog].objective = (ncols == j) ? z.x : z.y;
         }
@@ -563,7 +609,7 @@ __device__ __forceinline__ void prow_defer_body(
     int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log, int64_t log_cap,
     int fused, const double* __restrict__ Cp, const double* __restrict__ Pp, int prev_seal,
     const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn, int xcommit,
-    int tile, int onelaunch = 0) {
+    int tile, int onelaunch = 0, Cond cd = Cond{}) {
     __shared__ PricePart lds_pp[4];
     __shared__ SelView s_sel;
     __shared__ int s_selok;
@@ -636,6 +682,43 @@ __device__ __forceinline__ void prow_defer_body(
     } else if (pl >= 0 && j < ld) {
         t0 = *(const d2*)(T + (int64_t)pl * ld + j);
     }
+    // condensed tableau: the lane's two slots' restarts (the step of the replayed sequence at which
+    // each restarts from +0, -1: none here) and the entering slot (its entry of row p is the
+    // leaving variable's unit 1)
+    int32_t Rx = -1, Ry = -1, sq = -1;
+    if (cd.on) {
+        sq = st->sq;
+        if (owner_lane) {
+            const int bs = st->bser, ss = kp > 0 ? st->seal[prev_seal].ser : -2;
+            auto rof = [&](int32_t rv) -> int32_t {
+                if (rv < 0) return -1;
+                if ((rv >> 7) == bs) return kp + (rv & 127);
+                return (rv >> 7) == ss ? (rv & 127) : -1;
+            };
+            Rx = rof(cd.rst[j]);
+            Ry = rof(cd.rst[j + 1]);
+        }
+    }
+    // after the replay (kept out of its loop, whose registers are budgeted): a slot that restarted
+    // inside the replayed steps (rare: at most one slot per step) is replayed again from +0 at its
+    // restart step, the pivot rows from global memory; the entering slot's entry is the leaving
+    // variable's unit 1
+    auto cond_fix = [&](d2& t) {
+        if (Rx >= 0 || Ry >= 0) {
+            const int r0 = Rx < 0 ? Ry : (Ry < 0 ? Rx : min(Rx, Ry));
+            if (Rx >= 0) t.x = 0.0;
+            if (Ry >= 0) t.y = 0.0;
+            for (int l = r0; l < S; ++l) {
+                const d2 pv = *(const d2*)((l < kp ? Pp + (int64_t)l * ld : P + (int64_t)(l - kp) * ld) + j);
+                const double cp = s_cp[l];
+                const bool piv = pl == s_pl[l];
+                if (Rx >= 0 && l >= Rx) t.x = piv ? pv.x : (cp != 0.0 ? __builtin_fma(-cp, pv.x, t.x) : t.x);
+                if (Ry >= 0 && l >= Ry) t.y = piv ? pv.y : (cp != 0.0 ? __builtin_fma(-cp, pv.y, t.y) : t.y);
+            }
+        }
+        if (j == sq) t.x = 1.0;
+        if (j + 1 == sq) t.y = 1.0;
+    };
     if (fused && !LEAN) {   // (LEAN: within the 32 VGPRs that let it run beside the pass)
         zqpre = C[rows * ldc + s];
         if (j < ((ncols + 16) & ~(int64_t)15)) zpre = *(const d2*)(T + rows * ld + j);
@@ -664,6 +747,7 @@ __device__ __forceinline__ void prow_defer_body(
             glds16(psrc(l + RING), lds_addr(&s_ring[wv][l % RING][0]));
         }
         vmwait<0>();   // the ring drained (the clamped tail DMAs) before the block exits
+        if (cd.on) cond_fix(t);
         const double piv = sv.piv;
         pr.x = t.x / piv;
         pr.y = t.y / piv;
@@ -703,6 +787,7 @@ __device__ __forceinline__ void prow_defer_body(
             if (l0 + 2 * CH < S) fetch(pa, l0 + 2 * CH);
             apply(pb, l0 + CH);
         }
+        if (cd.on) cond_fix(t);
         const double piv = sv.piv;
         pr.x = t.x / piv;
         pr.y = t.y / piv;
@@ -737,9 +822,10 @@ __device__ __forceinline__ void prow_defer_body(
         if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 13);
         if (onelaunch)   // z_q from the record (C[rows][s] is another workgroup's store of this launch)
             commit_row<2>(T, ld, rows, ncols, nprice, slot, C, ldc, P, s, j, pr, pp, tile, tol_dj, log, log_cap,
-                          lds_pp, d2{0.0, 0.0}, sv.zq);
+                          lds_pp, d2{0.0, 0.0}, sv.zq, cd, sq, cd.on ? st->bser : 0);
         else
-            commit_row(T, ld, rows, ncols, nprice, slot, C, ldc, P, s, j, pr, pp, tile, tol_dj, log, log_cap, lds_pp);
+            commit_row(T, ld, rows, ncols, nprice, slot, C, ldc, P, s, j, pr, pp, tile, tol_dj, log, log_cap, lds_pp,
+                       d2{0.0, 0.0}, 0.0, cd, sq, cd.on ? st->bser : 0);
         if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 14);
         return;
     }
@@ -755,7 +841,7 @@ __device__ __forceinline__ void prow_defer_body(
         return;
     }
     commit_row<LEAN ? 0 : 1>(T, ld, rows, ncols, nprice, slot, C, ldc, P, s, j, pr, pp, tile, tol_dj, log,
-                             log_cap, lds_pp, zpre, zqpre);
+                             log_cap, lds_pp, zpre, zqpre, cd, sq, cd.on ? st->bser : 0);
     if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 11);
 }
 #define DLP_PROW_ARGS                                                                              \
@@ -763,9 +849,9 @@ __device__ __forceinline__ void prow_defer_body(
         const double *__restrict__ C, int64_t ldc, double *__restrict__ P, int64_t *__restrict__ bits,  \
         PricePart *pp, double tol_dj, dlp_pivot *log, int64_t log_cap, int fused,                    \
         const double *__restrict__ Cp, const double *__restrict__ Pp, int prev_seal, const XPeers *xp, \
-        uint32_t xseq, uint32_t *bcnt, int brb, int bnt, const double *Tn, int xcommit
+        uint32_t xseq, uint32_t *bcnt, int brb, int bnt, const double *Tn, int xcommit, Cond cd
 #define DLP_PROW_PASS T, ld, rows, ncols, nprice, st, C, ldc, P, bits, pp, tol_dj, log, log_cap, fused, Cp, Pp, \
-                      prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xcommit, (int)blockIdx.x
+                      prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xcommit, (int)blockIdx.x, 0, cd
 // The LEAN instance (lookahead at K = 64, beside the form-21 pass) is held to 32 VGPRs in its
 // kernel descriptor: the pass leaves 32 per SIMD (with the LDS-DMA asm, hipcc's descriptor
 // otherwise requested 176 for a body that uses 30, and the kernel could not share a CU).
@@ -800,7 +886,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(104))) void pro
         int32_t *__restrict__ nzc, int nrat, double tol_dj, double tol_piv, int pricing, dlp_pivot *log,         \
         int64_t log_cap, const double *__restrict__ Ccp, const double *__restrict__ Pp,                          \
         const double *__restrict__ Cp, int prev_seal, const XPeers *xp, uint32_t xseq, uint32_t *bcnt, int brb, \
-        int bnt, const double *Tn, int xs
+        int bnt, const double *Tn, int xs, Cond cd
 // (xs = 2, passed at launch: as a compile-time constant hipcc gave the LEAN instance 34 VGPRs, at
 // run time 30 of the 32 the form-21 pass leaves per SIMD)
 #define DLP_PX_BODIES(KM, LEAN_, LCH_, RP_, RS_)                                                                 \
@@ -808,12 +894,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(104))) void pro
         ratio_defer_body<KM, false, LEAN_, LCH_, RP_>(T, ld, rows, rows_elig, ncols, row_first, basis, pp,       \
                                                      ntiles, st, C, ldc, Cc, ldcc, P, rhs, nzc, nullptr,          \
                                                      nullptr, 2, tol_dj, tol_piv, pricing, log, log_cap, nrat,    \
-                                                     Ccp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xs, xseq); \
+                                                     Ccp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xs, xseq, Cond{}); \
         return;                                                                                                  \
     }                                                                                                            \
     prow_defer_body<LEAN_, RS_>(T, ld, rows, ncols, nprice, st, C, ldc, P, nullptr, pp,      \
                                 tol_dj, log, log_cap, 0, Cp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn, 1,     \
-                                (int)blockIdx.x - nrat, 1)
+                                (int)blockIdx.x - nrat, 1, Cond{})
 template <int KMAX>
 __global__ __launch_bounds__(256) void pivot_x_kernel(DLP_PX_RATIO_ARGS) {
     DLP_PX_BODIES(KMAX, false, 4, kRatioRingPairs, kProwRingSteps);
@@ -828,7 +914,7 @@ __global__ __launch_bounds__(256) void commit_defer_kernel(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
     const int64_t* __restrict__ bits, PricePart* pp, double tol_dj, dlp_pivot* log,
-    int64_t log_cap, const XPeers* xp, uint32_t xseq) {
+    int64_t log_cap, const XPeers* xp, uint32_t xseq, Cond cd) {
     __shared__ PricePart lds_pp[4];
     __shared__ int s_ok;
     if (st->status != DLP_RUNNING) return;
@@ -857,7 +943,7 @@ __global__ __launch_bounds__(256) void commit_defer_kernel(
         pr = *(const d2*)(bits + j);
     }
     commit_row(T, ld, rows, ncols, nprice, st->npivots - 1, C, ldc, P, s, j, pr, pp, (int)blockIdx.x, tol_dj, log,
-               log_cap, lds_pp);
+               log_cap, lds_pp, d2{0.0, 0.0}, 0.0, cd, cd.on ? st->sq : -1, cd.on ? st->bser : 0);
     if (blockIdx.x == 0) CHAIN_STAMP(slot, 14);
 }
 
@@ -2275,7 +2361,26 @@ __global__ __launch_bounds__(256, 2) void pass_m_kernel(const double* __restrict
 }
 
 __global__ void blk_reset_kernel(DevState* st) {
-    if (threadIdx.x == 0) st->blk = 0;
+    if (threadIdx.x == 0) {
+        st->blk = 0;
+        st->bser = st->bser + 1;   // (condensed tableau: the next block's restarts are its own)
+    }
+}
+
+// Condensed tableau: before a block's pass, each slot restarted in the block gets the unit
+// vector of its new variable (1 in the step's pivot row, +0 elsewhere) in the pass's INPUT, in
+// step order (a slot restarted twice keeps the later one): the pass then replays every step on it,
+// the steps before the restart being no-ops (their P entries of the slot were zeroed by the
+// commit).  One lane per local row; a column write, 8 B per row per restart.
+__global__ __launch_bounds__(256) void reset_cols_kernel(double* __restrict__ T, int64_t ld, int64_t rows,
+                                                         const int32_t* __restrict__ blkp,
+                                                         const int32_t* __restrict__ pl,
+                                                         const int32_t* __restrict__ qs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows) return;
+    const int kb = *blkp;
+    double* r = T + i * ld;
+    for (int l = 0; l < kb; ++l) r[qs[l]] = (pl[l] == (int32_t)i) ? 1.0 : 0.0;
 }
 
 // Lookahead: the block just selected becomes st->seal[slot] (read by its pass and
@@ -2284,13 +2389,18 @@ __global__ void blk_reset_kernel(DevState* st) {
 // output the next block's selections poll; the slot's previous pass has finished.)
 __global__ __launch_bounds__(64) void seal_kernel(DevState* st, int slot, uint32_t* bcnt, int64_t nb) {
     const int kb = st->blk;
-    for (int l = threadIdx.x; l < kMaxDefer; l += 64) st->seal[slot].pl[l] = l < kb ? st->pl[l] : -1;
+    for (int l = threadIdx.x; l < kMaxDefer; l += 64) {
+        st->seal[slot].pl[l] = l < kb ? st->pl[l] : -1;
+        st->seal[slot].qs[l] = st->qs[l];
+    }
     if (bcnt)
         for (int64_t b = threadIdx.x; b < nb; b += 64) bcnt[b] = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
         st->seal[slot].blk = kb;
+        st->seal[slot].ser = st->bser;
         st->blk = 0;
+        st->bser = st->bser + 1;
     }
 }
 
@@ -2324,7 +2434,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
     ratio_defer_kernel<KM><<<nblocks, g.rthreads, 0, s>>>(                               \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, \
         d.Cc, d.ldcc, d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing,   \
-        log, log_cap, Ccp, Pp, prev_seal, xp, xseq, xfuse ? 1 : 0)
+        log, log_cap, Ccp, Pp, prev_seal, xp, xseq, xfuse ? 1 : 0, g.cd)
     if (steps <= 8)
         DLP_RATIO_DEFER(8);
     else if (steps <= 16)
@@ -2342,7 +2452,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                 g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc,
                 d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp,
                 prev_seal, xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1,
-                pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xfuse ? 1 : 0);
+                pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xfuse ? 1 : 0, g.cd);
             return hipGetLastError();
         }
         static const int ring_env = std::getenv("DLP_CHAIN_RING") ? std::atoi(std::getenv("DLP_CHAIN_RING")) : 0;
@@ -2351,9 +2461,9 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
         d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
         xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,   \
-        pub ? bp->Tn : nullptr, xfuse ? 1 : 0)
+        pub ? bp->Tn : nullptr, xfuse ? 1 : 0, g.cd)
         // the LDS ring (0); 4 or 8 coefficient loads per round trip for tuning only (DLP_LEAN_LCH)
-        if (lch == 8)
+        if (lch == 8 && !g.cd.on)
             DLP_RATIO_LEAN(8, 0);
         else if (lch == 4)
             DLP_RATIO_LEAN(4, 0);
@@ -2377,7 +2487,7 @@ hipError_t launch_pivot_defer(const Geometry& g, const Defer& d, int32_t* basis,
     const int nprow = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     // every block resident at once (the pivot-row blocks wait on the ratio blocks): the
     // caller keeps the grid within 2 blocks per CU (fused_pivot_fits); K <= 32
-    if (d.K > 32) return hipErrorInvalidValue;
+    if (d.K > 32 || g.cd.on) return hipErrorInvalidValue;   // (no condensed-tableau instance)
 #define DLP_PIVOT_DEFER(KM)                                                                       \
     pivot_defer_kernel<KM><<<nrat + nprow, 256, 0, s>>>(                                          \
         g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.nprice, g.row_first, basis, pp, ntiles, st,    \
@@ -2428,7 +2538,7 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                                               pp, tol_dj, log, log_cap, nranks == 1 ? 1 : 0, prev->C, prev->P,
                                               prev_seal, nranks == 1 ? nullptr : xp, xseq,
                                               pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1,
-                                              pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xc);
+                                              pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xc, g.cd);
     } else if (prev_seal >= 0 && d.K > 32 && fat) {
         // lookahead with the chain on CUs of its own (no pass waves beside it): the register
         // kernel, 2 x 16 pivot rows in flight, with band publication
@@ -2436,14 +2546,14 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                                                  pp, tol_dj, log, log_cap, nranks == 1 ? 1 : 0, prev->C, prev->P,
                                                  prev_seal, nranks == 1 ? nullptr : xp, xseq,
                                                  pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1,
-                                                 pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xc);
+                                                 pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xc, g.cd);
     } else if (prev_seal >= 0 && d.K > 32) {   // lookahead at K = 64: beside the form-21 pass
 #define DLP_PROW_LEAN(RS)                                                                                  \
     prow_lean_kernel<RS><<<blocks, 256, prow_ring_bytes(RS), s>>>(                                          \
         g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap,     \
         nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal, nranks == 1 ? nullptr : xp, xseq,                \
         pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,           \
-        pub ? bp->Tn : nullptr, xc)
+        pub ? bp->Tn : nullptr, xc, g.cd)
         static const int ring_env = std::getenv("DLP_CHAIN_RING") ? std::atoi(std::getenv("DLP_CHAIN_RING")) : 0;
         if (ring_env == 16)
             DLP_PROW_LEAN(16);
@@ -2455,7 +2565,7 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
                                                  d.P, prow_bits, pp, tol_dj, log, log_cap,
                                                  nranks == 1 ? 1 : 0, prev_seal >= 0 ? prev->C : nullptr,
                                                  prev_seal >= 0 ? prev->P : nullptr, prev_seal,
-                                                 nranks == 1 ? nullptr : xp, xseq, nullptr, 1, 0, nullptr, xc);
+                                                 nranks == 1 ? nullptr : xp, xseq, nullptr, 1, 0, nullptr, xc, g.cd);
     return hipGetLastError();
 }
 
@@ -2463,7 +2573,8 @@ hipError_t launch_pivot_x(const Geometry& g, const Defer& d, int32_t* basis, Pri
                           double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
                           hipStream_t s, const Defer* prev, int prev_seal, const XPeers* xp, uint32_t seq,
                           const BandPub* bp) {
-    if (!xp || g.rthreads != kRatioDeferThreads) return hipErrorInvalidValue;   // 256-lane ratio blocks
+    // 256-lane ratio blocks; no condensed-tableau instance (its selection record has no slot field)
+    if (!xp || g.rthreads != kRatioDeferThreads || g.cd.on) return hipErrorInvalidValue;
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     const int nrat = ratio_defer_blocks(g);
@@ -2477,7 +2588,7 @@ hipError_t launch_pivot_x(const Geometry& g, const Defer& d, int32_t* basis, Pri
     g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.nprice, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, \
         d.ldcc, d.P, d.rhs, d.nzc, nrat, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, Cp, prev_seal, xp, \
         seq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,     \
-        pub ? bp->Tn : nullptr, 2
+        pub ? bp->Tn : nullptr, 2, g.cd
     if (steps > 64)   // lookahead at K = 64, beside the form-21 pass
         pivot_x_lean_kernel<<<nrat + nprow, 256, std::max(ratio_ring_bytes(kRatioRingPairs),
                                                           prow_ring_bytes(kProwRingSteps)), s>>>(DLP_PX_ARGS);
@@ -2498,7 +2609,7 @@ hipError_t launch_commit_defer(const Geometry& g, const Defer& d, DevState* st,
     const int blocks = (int)((g.ld + kDeferTile - 1) / kDeferTile);
     commit_defer_kernel<<<blocks, 256, 0, s>>>(g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C,
                                                d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap, xp,
-                                               xseq);
+                                               xseq, g.cd);
     return hipGetLastError();
 }
 
@@ -2757,6 +2868,10 @@ hipError_t launch_flush_defer(const Geometry& g, const Defer& d, DevState* st, b
     uint32_t* bcnt = nullptr;
     if (bp && bp->cnt && seal >= 0 && Tout && Tout != g.T && band_pub_ok(*bp, g, d, rows_per_block))
         bcnt = bp->cnt + seal * bp->stride;
+    if (g.cd.on) {
+        const hipError_t e = launch_reset_cols(g, st, seal, s);
+        if (e != hipSuccess) return e;
+    }
     return nontemporal ? pass_k<true>(g, d, st, rows_per_block, occupancy, s, Tout, seal, bcnt)
                        : pass_k<false>(g, d, st, rows_per_block, occupancy, s, Tout, seal, bcnt);
 }
@@ -2767,6 +2882,15 @@ hipError_t chain_stamps_enable() {
 }
 hipError_t chain_stamps_dump(uint64_t* host64x16) {
     return hipMemcpyFromSymbol(host64x16, HIP_SYMBOL(g_chain_stamps), sizeof(uint64_t) * 64 * 16);
+}
+
+hipError_t launch_reset_cols(const Geometry& g, const DevState* st, int seal, hipStream_t s) {
+    if (!g.cd.on || g.rows <= 0) return hipSuccess;
+    const int32_t* blkp = seal >= 0 ? &st->seal[seal].blk : &st->blk;
+    const int32_t* pl = seal >= 0 ? st->seal[seal].pl : st->pl;
+    const int32_t* qs = seal >= 0 ? st->seal[seal].qs : st->qs;
+    reset_cols_kernel<<<(unsigned)((g.rows + 255) / 256), 256, 0, s>>>(g.T, g.ld, g.rows, blkp, pl, qs);
+    return hipGetLastError();
 }
 
 hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s, const BandPub* bp) {

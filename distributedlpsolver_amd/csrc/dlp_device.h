@@ -149,13 +149,28 @@ __device__ inline void price_pair(PricePart& acc, double z0, double z1, int64_t 
     }
 }
 
+// Condensed tableau (Cond): the same for two slots holding variables v0, v1 (-1: not priced), in
+// any order: ties to the smaller variable index, Bland's first index = the smallest variable.
+__device__ inline void price_pair_var(PricePart& acc, double z0, double z1, int32_t v0, int32_t v1,
+                                      double tol_dj) {
+    if (v0 >= 0) {
+        if (z0 < acc.zmin || (z0 == acc.zmin && v0 < acc.jmin)) { acc.zmin = z0; acc.jmin = v0; }
+        if (z0 < -tol_dj && v0 < acc.jbland) acc.jbland = v0;
+    }
+    if (v1 >= 0) {
+        if (z1 < acc.zmin || (z1 == acc.zmin && v1 < acc.jmin)) { acc.zmin = z1; acc.jmin = v1; }
+        if (z1 < -tol_dj && v1 < acc.jbland) acc.jbland = v1;
+    }
+}
+
 // a4: select + basis bookkeeping + pivot log (one lane).
 // track: deferred mode, record the step's local pivot row and count it in the block.
 // write_obj = false (one-launch pivot): the log entry's objective is left to the commit of the
 // same launch, which writes it from another workgroup (the two writes never share bytes).
+// cd.on (condensed tableau): the leaving variable takes the entering one's slot st->sq.
 __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* basis,
                           int64_t row_first, int64_t rows, int pricing, dlp_pivot* log,
-                          int64_t log_cap, bool track = false, bool write_obj = true) {
+                          int64_t log_cap, bool track = false, bool write_obj = true, Cond cd = Cond{}) {
     if (!best.valid) {
         st->status = DLP_UNBOUNDED;
         return;
@@ -173,6 +188,13 @@ __device__ void do_select(DevState* st, const Cand& best, int32_t q, int32_t* ba
     const int64_t pl = (int64_t)p - row_first;
     st->p_local = (pl >= 0 && pl < rows) ? (int32_t)pl : -1;
     st->piv = best.pivot;
+    if (cd.on) {
+        const int32_t sq = st->sq;
+        cd.slot_of[q] = -1;
+        cd.slot_of[leaving] = sq;
+        cd.var_of[sq] = leaving;
+        if (track) st->qs[st->blk] = sq;
+    }
     if (track) {
         st->pl[st->blk] = st->p_local;
         st->blk = st->blk + 1;

@@ -72,6 +72,8 @@ struct alignas(128) DevState {
         uint32_t pad[2];
         int32_t pl[kMaxDefer];
         int32_t pad4;
+        int32_t ser;              // condensed tableau: the block's serial (bser when sealed)
+        int32_t qs[kMaxDefer];    // condensed tableau: slot of each step's entering variable
     } seal[2];
     // peer exchange, one launch per pivot (xfuse 2): the selection handed from the ratio
     // workgroups to the pivot-row workgroups of the same launch, on a line of its own: the fields
@@ -84,9 +86,31 @@ struct alignas(128) DevState {
         int64_t npivots;
         uint32_t pad[22];
     } sel;
+    // condensed tableau (Cond): the entering variable's slot (written with q by the
+    // ratio kernel), the open block's serial, and each step's entering slot
+    int32_t sq;
+    int32_t bser;
+    int32_t qs[kMaxDefer];
 };
 // A pass's block: DevState::blk/pl (in-place passes) or a sealed copy (lookahead).
 typedef DevState::Seal BlockDesc;
+
+// Condensed tableau.  A deferred session stores only the columns of the n
+// nonbasic variables ("slots" [0, n)) and the RHS (slot n): the m basic columns are exact unit
+// vectors (1 in their row, +0 elsewhere; the objective row +0) that the rule never changes, so
+// the pass, the pivot-row replay and the exchange move (n + 1) instead of (n + m + 1) columns.
+// When variable q (in slot s) enters at row p and v leaves, v takes slot s: its column is the
+// step applied to the unit vector e_p, i.e. the replay of slot s restarts at that step from +0
+// (row p: the pivot-row rule), and P_step[s] = 1 / pivot.  rst[s] records the restart
+// (block serial << 7 | step) for the replays; the pass gets e_p written into its input
+// (reset_cols) and P[l < step][s] = +0.  Results, read-outs and pivots are bit-identical to the
+// full tableau's (pricing ties by variable index, not slot).
+struct Cond {
+    int32_t* slot_of = nullptr;   // [N]: slot of a nonbasic variable, -1 for a basic one
+    int32_t* var_of = nullptr;    // [ld]: variable in a slot, -1 for the RHS slot and padding
+    int32_t* rst = nullptr;       // [ld]: the slot's last restart (serial << 7 | step), -1 none
+    int on = 0;
+};
 
 // Candidate order: valid first, then smaller ratio, then smaller basis index.
 // Total and order-independent, so any reduction tree picks the same winner.
@@ -183,6 +207,7 @@ struct Geometry {
     int rows_per_block;   // update kernel
     int rthreads = kRatioDeferThreads;   // deferred ratio workgroup (64 / 128 / 256 lanes; the
                                          // session's ratio_threads_policy, fixed at creation)
+    Cond cd;              // condensed tableau (cd.on): ncols = n is the RHS slot, width = round16(n + 1)
 };
 
 // Update-kernel variants (tuning): 0 U4/2dbl/scalar-colq (default), 1 U8, 2 U4/LDS-colq,
@@ -215,6 +240,10 @@ hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32
                          DevState* st, int pricing, dlp_pivot* log, int64_t log_cap,
                          hipStream_t s, bool forced = false, bool track = false,
                          const XPeers* xp = nullptr, uint32_t seq = 0);
+// Condensed tableau: the initial slot maps (variables 0..n-1 in slots 0..n-1, the m slacks basic),
+// no restarts; and the block's restart columns e_p written into the pass input (before its pass).
+hipError_t launch_cond_init(const Geometry& g, int64_t N, DevState* st, hipStream_t s);
+hipError_t launch_reset_cols(const Geometry& g, const DevState* st, int seal, hipStream_t s);
 // General LPs (Phase I -> II).  drive: forced-pivot candidate for global row
 // `row` (nranks == 1: also select + colq capture); gather_q: colq of st->q;
 // carry_out / carry_in: ship the carried objective row through the int64 MAX

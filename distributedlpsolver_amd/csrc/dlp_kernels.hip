@@ -28,9 +28,10 @@ namespace {
 
 // a1 at start-up: pricing partials of the initial objective row, one per
 // 512-column tile (the same tiling the update kernel's fused epilogue uses).
+// cd.on (condensed tableau): the partials carry variable indices (var_of), as commit_row's
 __global__ __launch_bounds__(kUpdThreads) void price_init_kernel(const double* __restrict__ zrow,
                                                                  int64_t nprice, int tile,
-                                                                 PricePart* pp, double tol_dj) {
+                                                                 PricePart* pp, double tol_dj, Cond cd) {
     __shared__ PricePart lds[4];
     PricePart acc = pp_empty();
     const int per_lane = tile / kUpdThreads;   // 2 or 4 columns per lane, ascending
@@ -39,7 +40,10 @@ __global__ __launch_bounds__(kUpdThreads) void price_init_kernel(const double* _
         if (j + k < nprice) {
             const double z0 = zrow[j + k];
             const double z1 = (j + k + 1 < nprice) ? zrow[j + k + 1] : 0.0;
-            price_pair(acc, z0, z1, j + k, nprice, tol_dj);
+            if (cd.on)
+                price_pair_var(acc, z0, z1, cd.var_of[j + k], j + k + 1 < nprice ? cd.var_of[j + k + 1] : -1, tol_dj);
+            else
+                price_pair(acc, z0, z1, j + k, nprice, tol_dj);
         }
     acc = block_price(acc, lds);
     if (threadIdx.x == 0) pp[blockIdx.x] = acc;
@@ -156,7 +160,7 @@ __device__ inline void forced_select(DevState* st, const Cand& best, int32_t* ba
 __global__ void select_kernel(const Cand* cands, int nranks, int32_t* basis, DevState* st,
                               int64_t row_first, int64_t rows, int pricing, dlp_pivot* log,
                               int64_t log_cap, int forced, int track, const XPeers* xp,
-                              uint32_t seq) {
+                              uint32_t seq, Cond cd) {
     __shared__ Cand s_c[kMaxRanks];
     __shared__ int s_ok;
     if (st->status != DLP_RUNNING) return;   // uniform: every rank holds the same status
@@ -174,7 +178,7 @@ __global__ void select_kernel(const Cand* cands, int nranks, int32_t* basis, Dev
     if (forced)
         forced_select(st, best, basis, row_first, rows, pricing, log, log_cap);
     else
-        do_select(st, best, st->q, basis, row_first, rows, pricing, log, log_cap, track != 0);
+        do_select(st, best, st->q, basis, row_first, rows, pricing, log, log_cap, track != 0, true, cd);
 }
 
 // ---- peer exchange, stand-alone kernels (the eager and Phase I -> II paths; the deferred
@@ -726,10 +730,11 @@ __device__ inline double unit01(uint64_t key, uint64_t idx) {
 // One wavefront per local row: lane l writes A[i][l + 64k] (coalesced) and
 // accumulates the strided fma chain of b_i; the 64 chains are combined by the
 // fixed halving tree (shfl_down 32..1) that the oracle restates.
+// rhs: the RHS column (N; n for a condensed tableau, which stores no slack columns)
 __global__ __launch_bounds__(256) void generate_rows_kernel(double* __restrict__ T, int64_t ld,
                                                             int64_t rows, int64_t row_first,
                                                             int64_t m, int64_t n, int kind,
-                                                            uint64_t seed) {
+                                                            uint64_t seed, int64_t rhs) {
     const int lane = threadIdx.x & 63;
     const int64_t il = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (il >= rows) return;
@@ -752,7 +757,7 @@ __global__ __launch_bounds__(256) void generate_rows_kernel(double* __restrict__
     double bi = __shfl(acc, 0) + unit01(kU, (uint64_t)i);
     if (kind == DLP_GEN_DEGENERATE && (mix64(kD + (uint64_t)i) >> 63) == 0) bi = 0.0;
     // slack identity column, RHS and zero padding: each cell written by one lane
-    for (int64_t j = n + lane; j < ld; j += 64) r[j] = (j == n + i) ? 1.0 : (j == N ? bi : 0.0);
+    for (int64_t j = n + lane; j < ld; j += 64) r[j] = (j == n + i && rhs == N) ? 1.0 : (j == rhs ? bi : 0.0);
 }
 
 __global__ __launch_bounds__(256) void generate_objective_kernel(double* __restrict__ z,
@@ -789,7 +794,7 @@ hipError_t launch_price_init(const Geometry& g, PricePart* pp, double tol_dj, in
     const double* z = g.T + g.rows * g.ld;
     const int tile = update_tile(variant);
     const int ntiles = (int)((g.width + tile - 1) / tile);
-    price_init_kernel<<<ntiles, kUpdThreads, 0, s>>>(z, g.nprice, tile, pp, tol_dj);
+    price_init_kernel<<<ntiles, kUpdThreads, 0, s>>>(z, g.nprice, tile, pp, tol_dj, g.cd);
     return hipGetLastError();
 }
 
@@ -810,7 +815,30 @@ hipError_t launch_select(const Geometry& g, const Cand* cands, int nranks, int32
                          hipStream_t s, bool forced, bool track, const XPeers* xp, uint32_t seq) {
     if (nranks > kMaxRanks) return hipErrorInvalidValue;
     select_kernel<<<1, 64, 0, s>>>(cands, nranks, basis, st, g.row_first, g.rows, pricing, log,
-                                   log_cap, forced ? 1 : 0, track ? 1 : 0, xp, seq);
+                                   log_cap, forced ? 1 : 0, track ? 1 : 0, xp, seq, g.cd);
+    return hipGetLastError();
+}
+
+// Condensed tableau: slots [0, n) hold variables 0..n-1 (the structural columns), the RHS slot and
+// the padding no variable; the slacks n..N-1 start basic; no slot has restarted.
+__global__ void cond_init_kernel(Cond cd, int64_t n, int64_t N, int64_t ld, DevState* st) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < N) cd.slot_of[k] = k < n ? (int32_t)k : -1;
+    if (k < ld) {
+        cd.var_of[k] = k < n ? (int32_t)k : -1;
+        cd.rst[k] = -1;
+    }
+    if (k == 0) {
+        st->sq = -1;
+        st->bser = 0;
+        st->seal[0].ser = st->seal[1].ser = -1;
+    }
+}
+
+hipError_t launch_cond_init(const Geometry& g, int64_t N, DevState* st, hipStream_t s) {
+    if (!g.cd.on) return hipSuccess;
+    const int64_t tot = N > g.ld ? N : g.ld;
+    cond_init_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(g.cd, g.ncols, N, g.ld, st);
     return hipGetLastError();
 }
 
@@ -1005,7 +1033,8 @@ hipError_t launch_generate(const Geometry& g, int kind, int64_t m, int64_t n, ui
         const int wpb = 4;   // wavefronts (rows) per workgroup
         const int64_t blocks = (g.rows + wpb - 1) / wpb;
         generate_rows_kernel<<<(unsigned)blocks, 64 * wpb, 0, s>>>(g.T, g.ld, g.rows,
-                                                                   g.row_first, m, n, kind, seed);
+                                                                   g.row_first, m, n, kind, seed,
+                                                                   g.cd.on ? n : n + m);
     }
     const int64_t zb = (g.ld + 255) / 256;
     generate_objective_kernel<<<(unsigned)zb, 256, 0, s>>>(g.T + g.rows * g.ld, g.ld, n, seed);

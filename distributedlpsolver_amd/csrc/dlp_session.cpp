@@ -178,6 +178,7 @@ struct dlp_session {
     // ranks of this session's exchange on its device (itself included) and this rank's index among
     // them, from the device of every rank the peer connect saw (install_peers); 1 / 0 otherwise
     int coloc_n = 1, coloc_i = 0;
+    int64_t ld_full = 0;   // condensed tableau: the row stride the full layout would have (read-outs)
 };
 
 extern "C" int flush_pending(dlp_session* s);   // defined with the C entry points
@@ -503,7 +504,8 @@ void free_session(dlp_session* s) {
     clk.mark("free: comm");
     void* dev[] = {s->Tb[0] ? s->Tb[0] : s->T, s->Tb[1], s->colq, s->prow_send, s->partials,
                    s->cand_send, s->cand_recv, s->pp, s->basis, s->st, s->log, s->d.C, s->d.Cc,
-                   s->d.P, s->d.rhs, s->d.nzc, s->cl_gran, s->band_cnt};
+                   s->d.P, s->d.rhs, s->d.nzc, s->cl_gran, s->band_cnt, s->g.cd.slot_of, s->g.cd.var_of,
+                   s->g.cd.rst};
     for (void* p : dev) pool_release(s, s->device, p);
     if (s->la || s->dslot[1].C) {   // slot 0 aliases s->d
         void* sl[] = {s->dslot[1].C, s->dslot[1].Cc, s->dslot[1].P, s->dslot[1].nzc};
@@ -571,6 +573,13 @@ int flush_pending_block(dlp_session* s);
 // vs 24.8-25.0 k pivots/s, c3r4 21.0 k vs 20.7-20.9 k, profiles/r05d/; C2 44.7 k vs 42.7 k,
 // profiles/r05o/; 64 lanes gain nothing more), else 256 (C3 at P = 1: no difference,
 // profiles/r05e/).  DLP_RATIO_THREADS=64/128/256 overrides.
+// Condensed tableau by default (dlp_options.condensed = 0); DLP_CONDENSED=0 / 1 overrides the
+// auto choice (A/B and tests).
+bool condensed_auto() {
+    static const int v = std::getenv("DLP_CONDENSED") ? std::atoi(std::getenv("DLP_CONDENSED")) : 1;
+    return v == 1;
+}
+
 int ratio_threads_policy(const dlp_session* s) {
     if (const char* e = std::getenv("DLP_RATIO_THREADS")) {
         const int n = std::atoi(e);
@@ -897,10 +906,34 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         // x 4 rows elsewhere (K = 16 streaming: form 3 6.1 ms vs form 4 6.4, r01g)
         s->d.form = (K == 64 && s->streaming) ? 21
                     : ((K == 32 && s->streaming) || (K == 16 && !s->streaming)) ? 4 : 3;
+        // condensed tableau: a deferred session of a dense / random /
+        // ad-allocation LP stores only the n nonbasic columns + the RHS (the m basic columns are
+        // unit vectors); the size-based policies above keep the full tableau's scale
+        const int creq = opt->condensed;
+        if (creq < -1 || creq > 1) {
+            set_error("condensed must be -1 (off), 0 (auto) or 1 (on)");
+            return DLP_ERR_ARG;
+        }
+        if ((creq == 1 || (creq == 0 && condensed_auto())) && K > 1 && !s->general && !s->cluster) {
+            s->g.cd.on = 1;
+            s->ld_full = s->ld;   // (the read-outs keep the full layout's stride)
+            s->width = round16(s->n + 1);
+            s->ld = (s->width + align - 1) / align * align;
+            g.ld = s->ld;
+            g.width = s->width;
+            g.ncols = s->n;
+            g.nprice = s->n;
+            g.ntiles = (int)((s->width + tile - 1) / tile);
+        }
     }
     g.rows_per_block = opt->rows_per_block > 0 ? opt->rows_per_block : auto_rows_per_block(s);
     g.rows_per_block = std::min(g.rows_per_block, dlp::kMaxBandLdsHost);
     const size_t tbytes = (size_t)rows_total * s->ld * sizeof(double);
+    if (s->g.cd.on) {
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->g.cd.slot_of, sizeof(int32_t) * s->N));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->g.cd.var_of, sizeof(int32_t) * s->ld));
+        HIP_TRY(pool_alloc(s, s->device, (void**)&s->g.cd.rst, sizeof(int32_t) * s->ld));
+    }
     if (pool_alloc(s, s->device, (void**)&s->T, tbytes) != hipSuccess) {
         set_error("hipMalloc of the tableau failed (" + std::to_string(tbytes) + " bytes)");
         return DLP_ERR_OOM;
@@ -962,7 +995,18 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
         HIP_TRY(dlp::launch_generate(g, prob->gen_kind, s->m, s->n, prob->seed, s->stream));
     } else {
         std::vector<double> host;
-        host_tableau(prob, s->row_first, s->rows, s->ld, host, s->carry_local);
+        if (s->g.cd.on) {   // the full rows, then only the structural columns and the RHS kept
+            const int64_t ldf = round16(s->N + 1);
+            std::vector<double> full;
+            host_tableau(prob, s->row_first, s->rows, ldf, full, s->carry_local);
+            host.assign((size_t)rows_total * s->ld, 0.0);
+            for (int64_t i = 0; i < rows_total; ++i) {
+                std::memcpy(host.data() + i * s->ld, full.data() + i * ldf, sizeof(double) * s->n);
+                host[(size_t)(i * s->ld + s->n)] = full[(size_t)(i * ldf + s->N)];
+            }
+        } else {
+            host_tableau(prob, s->row_first, s->rows, s->ld, host, s->carry_local);
+        }
         HIP_TRY(hipMemcpyAsync(s->T, host.data(), tbytes, hipMemcpyHostToDevice, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
     }
@@ -980,8 +1024,12 @@ int session_init(const dlp_problem* prob, const dlp_options* opt, int rank, int 
     st0.p_local = -1;
     st0.leaving = -1;
     st0.bland = opt->pricing == DLP_PRICING_BLAND ? 1 : 0;
+    st0.sq = -1;
+    st0.bser = 0;
+    st0.seal[0].ser = st0.seal[1].ser = -1;
     *s->host_st = st0;
     HIP_TRY(hipMemcpyAsync(s->st, s->host_st, sizeof(st0), hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(dlp::launch_cond_init(g, s->N, s->st, s->stream));
     HIP_TRY(dlp::launch_price_init(g, s->pp, opt->tol_dj, opt->update_variant, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     s->Tb[0] = s->T;
@@ -1221,7 +1269,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     }
     if (phase == 0) {
         if (ev) HIP_TRY(hipEventRecord(ev[0], s->stream));
-        if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) {
+        if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !s->g.cd.on && !ev) {
             // single rank: ratio test, selection and pivot row in one launch
             HIP_TRY(dlp::launch_pivot_defer(s->g, s->d, s->basis, s->pp, s->st, s->partials,
                                             s->ratio_blocks_max, o.tol_dj, o.tol_piv, o.pricing, s->log,
@@ -1232,7 +1280,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         // selection, the selection record to the pivot-row workgroups, row push, commit).  Bit-exact,
         // but 1-3 % slower than two launches at the C3 rank geometries: the record's hand-off and its
         // ~130 pollers cost what the launch boundary did (profiles/r04i/, r04j/)
-        if (xf && peer_onelaunch() && s->g.rthreads == dlp::kRatioDeferThreads) {
+        if (xf && peer_onelaunch() && !s->g.cd.on && s->g.rthreads == dlp::kRatioDeferThreads) {
             s->xseq_c += 1;
             s->xseq_r += 1;   // (equal: every pivot, drive-out and carry step advances both)
             HIP_TRY(dlp::launch_pivot_x(gsel, *dcur, s->basis, s->pp, s->st, o.tol_dj, o.tol_piv, o.pricing, s->log,
@@ -1252,8 +1300,8 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         return DLP_OK;
     }
     if (phase == 1) {
-        if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !ev) return DLP_OK;
-        if (xf && peer_onelaunch() && s->g.rthreads == dlp::kRatioDeferThreads) {   // (the whole pivot ran in phase 0's launch)
+        if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !s->g.cd.on && !ev) return DLP_OK;
+        if (xf && peer_onelaunch() && !s->g.cd.on && s->g.rthreads == dlp::kRatioDeferThreads) {   // (the whole pivot ran in phase 0's launch)
             if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
             return DLP_OK;
         }
@@ -1690,11 +1738,59 @@ int general_result(dlp_session* s, const std::vector<double>& z, const std::vect
 
 // The RHS column entries of this rank's ratio-eligible rows (the values of their
 // basic variables).
+// Condensed tableau: the slot of every variable (-1: basic).
+int cond_slots(dlp_session* s, std::vector<int32_t>& slot_of) {
+    slot_of.resize(s->N);
+    HIP_TRY(hipMemcpyAsync(slot_of.data(), s->g.cd.slot_of, sizeof(int32_t) * s->N, hipMemcpyDeviceToHost,
+                           s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return DLP_OK;
+}
+
+// z (the stored objective row, ld doubles) -> the full row in variable order (basic: +0, RHS at N).
+int cond_expand_z(dlp_session* s, std::vector<double>& z) {
+    std::vector<int32_t> so;
+    CALL_TRY(cond_slots(s, so));
+    std::vector<double> f(std::max<int64_t>(round16(s->N + 1), s->N + 1), 0.0);
+    for (int64_t v = 0; v < s->N; ++v)
+        if (so[v] >= 0) f[v] = z[so[v]];
+    f[s->N] = z[s->g.ncols];
+    z.swap(f);
+    return DLP_OK;
+}
+
+// Rows [first, first + count) of a condensed session (the objective row is local row `rows`) in
+// the full tableau's layout, ldl doubles per row: a nonbasic variable's entry from its slot, a
+// basic one's unit entry (1 in its row, +0 elsewhere and in the objective row), the RHS at N.
+int cond_read_rows(dlp_session* s, int64_t first, int64_t count, double* host, int64_t ldl) {
+    std::vector<double> c((size_t)count * s->ld);
+    HIP_TRY(hipMemcpyAsync(c.data(), s->T + first * s->ld, sizeof(double) * count * s->ld,
+                           hipMemcpyDeviceToHost, s->stream));
+    std::vector<int32_t> basis(s->m);
+    HIP_TRY(hipMemcpyAsync(basis.data(), s->basis, sizeof(int32_t) * s->m, hipMemcpyDeviceToHost, s->stream));
+    std::vector<int32_t> so;
+    CALL_TRY(cond_slots(s, so));   // (synchronises the stream)
+    for (int64_t k = 0; k < count; ++k) {
+        const double* src = c.data() + k * s->ld;
+        double* dst = host + k * ldl;
+        for (int64_t v = 0; v < ldl; ++v) dst[v] = 0.0;
+        for (int64_t v = 0; v < s->N; ++v)
+            if (so[v] >= 0) dst[v] = src[so[v]];
+        dst[s->N] = src[s->g.ncols];
+        const int64_t il = first + k;
+        if (il < s->rows) {
+            const int32_t bv = basis[s->row_first + il];
+            if (bv >= 0 && bv < s->N) dst[bv] = 1.0;
+        }
+    }
+    return DLP_OK;
+}
+
 int local_rhs(dlp_session* s, std::vector<double>& rhs) {
     HIP_TRY(hipSetDevice(s->device));
     rhs.assign(s->g.rows_elig, 0.0);
     if (s->g.rows_elig > 0) {
-        HIP_TRY(dlp::launch_gather_column(s->T, s->ld, s->rows, s->N, s->colq, s->stream));
+        HIP_TRY(dlp::launch_gather_column(s->T, s->ld, s->rows, s->g.ncols, s->colq, s->stream));
         HIP_TRY(hipMemcpyAsync(rhs.data(), s->colq, sizeof(double) * s->g.rows_elig,
                                hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1716,7 +1812,7 @@ int extract_result(dlp_session* s, dlp_result* r, const std::vector<double>* rhs
     HIP_TRY(hipMemcpyAsync(z.data(), s->T + s->rows * s->ld, sizeof(double) * s->ld,
                            hipMemcpyDeviceToHost, s->stream));
     if (s->rows > 0) {
-        HIP_TRY(dlp::launch_gather_column(s->T, s->ld, s->rows, s->N, s->colq, s->stream));
+        HIP_TRY(dlp::launch_gather_column(s->T, s->ld, s->rows, s->g.ncols, s->colq, s->stream));
         HIP_TRY(hipMemcpyAsync(rhs.data(), s->colq, sizeof(double) * s->rows,
                                hipMemcpyDeviceToHost, s->stream));
     }
@@ -1729,6 +1825,7 @@ int extract_result(dlp_session* s, dlp_result* r, const std::vector<double>* rhs
         HIP_TRY(hipMemcpyAsync(r->log.data(), s->log, sizeof(dlp_pivot) * nlog,
                                hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->g.cd.on) CALL_TRY(cond_expand_z(s, z));   // the objective row in variable order
     for (int ph = 0; ph < DLP_NUM_PHASES; ++ph) r->timings[ph] = s->timings[ph];
     const std::vector<double>& rh = rhs_all ? *rhs_all : rhs;
     const int64_t rows_elig = rhs_all ? (int64_t)rhs_all->size() : s->g.rows_elig;
@@ -3110,7 +3207,7 @@ int dlp_session_get_lookahead(dlp_session* s, int* on) {
 }
 
 int dlp_session_set_fused_pivot(dlp_session* s, int on) {
-    if (!s || on < 0 || on > 1) return DLP_ERR_ARG;
+    if (!s || on < 0 || on > 1) return DLP_ERR_ARG;   // (a condensed session keeps two launches)
     s->fuse_pivot = on != 0;
     if (s->gexec) { (void)hipGraphExecDestroy(s->gexec); s->gexec = nullptr; }
     if (s->graph) { (void)hipGraphDestroy(s->graph); s->graph = nullptr; }
@@ -3141,13 +3238,25 @@ int dlp_session_update_stats(dlp_session* s, int64_t* launches, double* ms, int*
     return DLP_OK;
 }
 
+// the row stride of dlp_session_tableau / read_rows: the stored one, or for a condensed tableau the
+// full layout's roundup(N + 1, 16)
+static int64_t logical_ld(const dlp_session* s) { return s->g.cd.on ? s->ld_full : s->ld; }
+
 int dlp_session_info(dlp_session* s, int64_t* rows_local, int64_t* row_first, int64_t* ld,
                      int64_t* ncols) {
     if (!s) return DLP_ERR_ARG;
     if (rows_local) *rows_local = s->rows;
     if (row_first) *row_first = s->row_first;
-    if (ld) *ld = s->ld;
+    if (ld) *ld = logical_ld(s);
     if (ncols) *ncols = s->N;
+    return DLP_OK;
+}
+
+int dlp_session_storage(dlp_session* s, int64_t* ld, int64_t* ncols, int* condensed) {
+    if (!s) return DLP_ERR_ARG;
+    if (ld) *ld = s->ld;
+    if (ncols) *ncols = s->g.ncols;
+    if (condensed) *condensed = s->g.cd.on;
     return DLP_OK;
 }
 
@@ -3155,6 +3264,7 @@ int dlp_session_tableau(dlp_session* s, double* host) {
     if (!s || !host) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
     CALL_TRY(flush_pending(s));
+    if (s->g.cd.on) return cond_read_rows(s, 0, s->rows + 1, host, logical_ld(s));
     HIP_TRY(hipMemcpyAsync(host, s->T, sizeof(double) * (s->rows + 1) * s->ld,
                            hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -3165,6 +3275,7 @@ int dlp_session_read_rows(dlp_session* s, int64_t first, int64_t count, double* 
     if (!s || !host || first < 0 || count < 0 || first + count > s->rows + 1) return DLP_ERR_ARG;
     HIP_TRY(hipSetDevice(s->device));
     CALL_TRY(flush_pending(s));
+    if (s->g.cd.on) return cond_read_rows(s, first, count, host, logical_ld(s));
     HIP_TRY(hipMemcpyAsync(host, s->T + first * s->ld, sizeof(double) * count * s->ld,
                            hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));

@@ -237,6 +237,10 @@ class Session:
         L.check(L.lib().dlp_session_info(h, C.byref(rows), C.byref(first), C.byref(ld),
                                          C.byref(ncols)), "dlp_session_info")
         self.rows, self.row_first, self.ld, self.ncols = rows.value, first.value, ld.value, ncols.value
+        # the tableau as stored: row stride, RHS column, condensed or full
+        sld, snc, cond = C.c_int64(), C.c_int64(), C.c_int()
+        L.check(L.lib().dlp_session_storage(h, C.byref(sld), C.byref(snc), C.byref(cond)), "dlp_session_storage")
+        self.storage_ld, self.storage_ncols, self.condensed = sld.value, snc.value, bool(cond.value)
 
     def run(self, max_pivots: int) -> tuple[int, int]:
         done = C.c_int64()
@@ -259,7 +263,7 @@ class Session:
             L.check(L.lib().dlp_session_write_buffer(self._h, L.BUF_CAND_RECV, g.ctypes.data,
                                                      g.nbytes), "dlp_session_write_buffer")
         L.check(L.lib().dlp_session_step_select(self._h), "dlp_session_step_select")
-        out = np.zeros(self.ld, np.int64)
+        out = np.zeros(self.storage_ld, np.int64)
         L.check(L.lib().dlp_session_read_buffer(self._h, L.BUF_PROW_SEND, out.ctypes.data,
                                                 out.nbytes), "dlp_session_read_buffer")
         return out

@@ -170,6 +170,12 @@ typedef struct dlp_options {
                                 dlp_solve(n_gpus) with DLP_XCHG_DEFAULT: a run that fails on the
                                 peer exchange is rerun from the start over RCCL
                                 (dlp_result_exchange reports it) */
+    int32_t condensed;       /* deferred sessions (defer > 1) of dense / random / ad-allocation LPs:
+                                store only the n nonbasic columns + the RHS, the m basic columns
+                                being exact unit vectors (results, pivots and
+                                read-outs bit-identical to the full tableau): 1 = on where
+                                supported, -1 = off, 0 = auto (default: on; DLP_CONDENSED=0/1
+                                overrides auto) */
 } dlp_options;
 /* Auto tuning (MI355X measurements): a local tableau > 1 GiB streams
  * from HBM -> row-serial kernel capped at 4 workgroups/CU, 8-row bands, nt;
@@ -386,6 +392,10 @@ int dlp_session_connect_ipc(dlp_session* s, const void* handles /* nranks x 64 B
 int dlp_session_exchange_record(dlp_session* s, void* out /* DLP_XREC_BYTES */);
 int dlp_session_connect_records(dlp_session* s, const void* records /* nranks x DLP_XREC_BYTES, rank order */);
 int dlp_session_colocated(dlp_session* s, int* n, int* index);
+/* The tableau as stored: row stride, RHS column (N, or n when condensed) and whether it is the
+ * condensed tableau.  dlp_session_info / _tableau / _read_rows always give the
+ * full layout (N + 1 columns, basic columns as unit vectors). */
+int dlp_session_storage(dlp_session* s, int64_t* ld, int64_t* ncols, int* condensed);
 int dlp_session_set_exchange(dlp_session* s, int mode);
 int dlp_session_get_exchange(dlp_session* s, int* mode);
 /* Why an auto exchange (DLP_XCHG_DEFAULT) fell back to RCCL ("" when it did not). */

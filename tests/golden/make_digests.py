@@ -30,7 +30,7 @@ for the GPU to reproduce.  Run in the build container (CPU only):
       each split ("blocks": {"2": [...], "3": [...], "4": [...], "8": [...]}).
   c4_degen_2048x4096  C4's large degenerate LP (2048 x 4096 seed 4, degenerate family: b_i = 0
       on half the rows, Bland after every degenerate pivot): whole-tableau, log, basis and
-      objective digests at 500 and 2,000 pivots, plus the degenerate-pivot count.
+      objective digests at 500, 2,000 and 30,000 pivots, plus the degenerate-pivot count.
 
 The digests hash little-endian fp64 / int32 bytes of the oracle's outputs
 (tests/oracle_py.py), so the GPU side compares bit for bit."""
@@ -138,7 +138,7 @@ def rank_split(m=8192, n=57344, seed=34, P=2, stops=(136, 200, 264), Ps=None):
     return out
 
 
-def c4_degen(m=2048, n=4096, seed=4, stops=(500, 2000)):
+def c4_degen(m=2048, n=4096, seed=4, stops=(500, 2000, 30000)):
     """the 50%-zero-RHS degenerate LP at 2,048 x 4,096, the
     size the small-LP launch does not cover (auto: the deferred K = 16 path).  Whole-tableau
     digests (all 2,049 rows, objective row last, each its first `width` doubles) at each stop."""
