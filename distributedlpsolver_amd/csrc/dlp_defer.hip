@@ -690,21 +690,24 @@ __device__ __forceinline__ void prow_defer_body(
         sq = st->sq;
         if (owner_lane) {
             const int bs = st->bser, ss = kp > 0 ? st->seal[prev_seal].ser : -2;
+            // (a sealed-block restart matters only where row p is replayed through the sealed
+            // block: a published row p already holds its result)
             auto rof = [&](int32_t rv) -> int32_t {
                 if (rv < 0) return -1;
                 if ((rv >> 7) == bs) return kp + (rv & 127);
-                return (rv >> 7) == ss ? (rv & 127) : -1;
+                return (!pdone && (rv >> 7) == ss) ? (rv & 127) : -1;
             };
             Rx = rof(cd.rst[j]);
             Ry = rof(cd.rst[j + 1]);
         }
     }
-    // after the replay (kept out of its loop, whose registers are budgeted): a slot that restarted
-    // inside the replayed steps (rare: at most one slot per step) is replayed again from +0 at its
-    // restart step, the pivot rows from global memory; the entering slot's entry is the leaving
-    // variable's unit 1
+    // The restarts: inside the replay loops (the slot's value becomes +0 at its restart step), or,
+    // in the MID instance (CHR 8), whose registers are budgeted beside the MFMA pass, after the
+    // loop: a restarted slot is replayed again from +0 at its restart step, its pivot rows from
+    // global memory.  Then the entering slot's entry is the leaving variable's unit 1.
+    constexpr bool kFixAfter = !LEAN && CHR == 8;
     auto cond_fix = [&](d2& t) {
-        if (Rx >= 0 || Ry >= 0) {
+        if (kFixAfter && (Rx >= 0 || Ry >= 0)) {
             const int r0 = Rx < 0 ? Ry : (Ry < 0 ? Rx : min(Rx, Ry));
             if (Rx >= 0) t.x = 0.0;
             if (Ry >= 0) t.y = 0.0;
@@ -741,6 +744,8 @@ __device__ __forceinline__ void prow_defer_body(
             const d2 pv = *(const d2*)&s_ring[wv][l % RING][2 * wl];
             const double cp = s_cp[l];
             const bool piv = pl == s_pl[l];
+            if (l == Rx) t.x = 0.0;
+            if (l == Ry) t.y = 0.0;
             const double ux = __builtin_fma(-cp, pv.x, t.x), uy = __builtin_fma(-cp, pv.y, t.y);
             t.x = piv ? pv.x : (cp != 0.0 ? ux : t.x);   // (branch-free, as the ratio ring's step)
             t.y = piv ? pv.y : (cp != 0.0 ? uy : t.y);
@@ -770,6 +775,8 @@ __device__ __forceinline__ void prow_defer_body(
             for (int u = 0; u < CH; ++u) {
                 const int l = l0 + u;
                 if (l < S) {
+                    if (!kFixAfter && l == Rx) t.x = 0.0;
+                    if (!kFixAfter && l == Ry) t.y = 0.0;
                     if (pl == s_pl[l]) {
                         t = pv[u];
                     } else if (s_cp[l] != 0.0) {

@@ -20,7 +20,7 @@ ev = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name
 
 def kind(name):
     n = name.replace("(anonymous namespace)::", "").split("(")[0]
-    for k in ("ratio_", "prow_", "pivot_x", "pass_", "seal_", "commit_", "blk_reset"):
+    for k in ("ratio_", "prow_", "pivot_x", "pass_", "seal_", "commit_", "blk_reset", "reset_cols"):
         if k in n:
             return k.rstrip("_")
     return None
@@ -44,6 +44,7 @@ for bi in range(max(0, len(passes) - 1 - nblk), len(passes) - 1):
         "ratio_us": [round((x[1] - x[0]) / 1e3, 1) for x in rat],
         "prow_us": [round((x[1] - x[0]) / 1e3, 1) for x in prw],
         "period_us": [round(v / 1e3, 1) for v in np.diff(starts)],
+        "reset_cols_us": [round((x[1] - x[0]) / 1e3, 1) for x in ev[a - 2:b] if x[2] == "reset_cols"][:2],
         "ratio_name": rat[0][3].replace("(anonymous namespace)::", "").split("(")[0][-60:] if rat else None,
     })
 print(json.dumps(out, indent=1))
