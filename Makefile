@@ -42,9 +42,12 @@ clean:
 
 .PHONY: all oracle ref asm clean
 
-tools: build/hbm_ceiling
+tools: build/hbm_ceiling build/fetch_calib
 
 build/hbm_ceiling: tools/hbm_ceiling.hip | build
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
+build/fetch_calib: tools/fetch_calib.hip | build
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 .PHONY: tools

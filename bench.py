@@ -50,15 +50,17 @@ WORKLOADS = {
                             "row-block over the GPUs"),
     "c2": (4096, 4096, 2, "C2 dense LP 4096 x 4096 (+4096 slack): fp64 tableau 4097 x 8193"),
     # the per-rank floor of the 8-GPU C3 split, on ONE GPU: a rank of C3 at P = 8 holds 4,096 rows
-    # x 65,537 columns; a 4096 x 61440 LP has exactly that tableau.  Run as a 1-rank exchange
-    # session (RCCL id, nranks = 1), so the chain carries the select / commit kernels and the
-    # exchange stores a rank of the split runs; only the xGMI latency is missing
-    "c3r8": (4096, 61440, 38, "C3 rank geometry at P = 8: dense LP 4096 x 61440 (+4096 slack), fp64 "
-                              "tableau 4097 x 65537 = one rank of the 8-GPU C3 split, 1-rank exchange"),
-    "c3r4": (8192, 57344, 34, "C3 rank geometry at P = 4: dense LP 8192 x 57344 (+8192 slack), fp64 "
-                              "tableau 8193 x 65537 = one rank of the 4-GPU C3 split, 1-rank exchange"),
-    "c3r2": (16384, 49152, 32, "C3 rank geometry at P = 2: dense LP 16384 x 49152 (+16384 slack), fp64 "
-                               "tableau 16385 x 65537 = one rank of the 2-GPU C3 split, 1-rank exchange"),
+    # of the condensed tableau's 32,769 columns (the n = 32,768 nonbasic columns + RHS, DESIGN.md
+    # §16); a 4096 x 32768 LP has exactly that stored tableau.  Run as a 1-rank exchange session
+    # (RCCL id, nranks = 1), so the chain carries the select / commit kernels and the exchange
+    # stores a rank of the split runs; only the xGMI latency is missing.  (Round 5's c3rP LPs,
+    # 4096 x 61440 etc., matched the full tableau's 65,537 columns.)
+    "c3r8": (4096, 32768, 38, "C3 rank geometry at P = 8: dense LP 4096 x 32768, condensed fp64 tableau "
+                              "4097 x 32769 = one rank of the 8-GPU C3 split, 1-rank exchange"),
+    "c3r4": (8192, 32768, 34, "C3 rank geometry at P = 4: dense LP 8192 x 32768, condensed fp64 tableau "
+                              "8193 x 32769 = one rank of the 4-GPU C3 split, 1-rank exchange"),
+    "c3r2": (16384, 32768, 32, "C3 rank geometry at P = 2: dense LP 16384 x 32768, condensed fp64 tableau "
+                               "16385 x 32769 = one rank of the 2-GPU C3 split, 1-rank exchange"),
 }
 RANK_WORKLOADS = ("c3r2", "c3r4", "c3r8")
 # C5 (BASELINE.json configs[4]): 4,096 independent 64 x 128 LPs, one workgroup per LP
@@ -798,9 +800,9 @@ def main():
             e_el = time.perf_counter() - t2
             e_launch, e_ms, _ = es.update_stats()
             e_var, e_rb, e_nt = es.get_tuning()
-            e_rows = es.rows
+            e_rows, e_N1 = es.rows, es.ncols + 1   # (the eager session stores the full tableau)
         e_ms1 = e_ms / max(e_launch, 1)
-        e_bytes = 16.0 * (e_rows + 1) * N1
+        e_bytes = 16.0 * (e_rows + 1) * e_N1
         e_ach = e_bytes / (e_ms1 * 1e-3) / 1e9 if e_ms1 > 0 else None
         eager = {"kernel": f"rank-1 update variant {e_var} (rows/band {e_rb}, nt {e_nt})",
                  "pivots": done, "launches": e_launch, "launch_ms": e_ms1,
@@ -903,4 +905,13 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    finally:
+        # pooled streams (CU-masked ones included), buffers and batch contexts released before the
+        # runtime's own teardown (a rocprofv3-traced run crashed at exit without it, profiles/r06i/)
+        if "distributedlpsolver_amd" in sys.modules and os.environ.get("DLP_BENCH_LAUNCHER") != "parent":
+            try:
+                sys.modules["distributedlpsolver_amd"].release_cached_memory(-1)
+            except Exception:  # noqa: BLE001 - best effort at exit
+                pass

@@ -224,6 +224,28 @@ hipError_t acquire_stream(int device, int prio, hipStream_t* out) {
     return hipStreamCreateWithPriority(out, hipStreamNonBlocking, prio);
 }
 
+// Destroy the pooled streams of `device` (< 0: all), e.g. before the process exits: CU-masked queues
+// left to the runtime's own teardown crashed a rocprofv3-traced process at exit (profiles/r06i/).
+void streams_drain(int device) {
+    std::vector<PooledStream> out;
+    {
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        for (size_t k = g_stream_pool.size(); k-- > 0;)
+            if (device < 0 || g_stream_pool[k].device == device) {
+                out.push_back(g_stream_pool[k]);
+                g_stream_pool.erase(g_stream_pool.begin() + (ptrdiff_t)k);
+            }
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (const auto& e : out) {
+        (void)hipSetDevice(e.device);
+        (void)hipStreamDestroy(e.s);
+    }
+    (void)hipSetDevice(cur);
+    (void)hipGetLastError();
+}
+
 // the caller has set the device; a stream whose work failed is destroyed, not pooled
 void release_stream(int device, int prio, hipStream_t s) {
     if (!s) return;
@@ -619,9 +641,12 @@ int chain_cus_policy(const dlp_session* s) {
     if (const char* e = std::getenv("DLP_CHAIN_CUS")) {
         n = std::atoi(e);
         n = n > 0 && n < cus ? n : 0;
-    } else if (s->rows < 32768) {
+    } else if (s->rows < 32768 || s->g.cd.on) {
         // (mask bits act in groups of 32: 112 and 128 chain bits, or 144 and 160, give the pass the
-        // same time, profiles/r04ah/)
+        // same time, profiles/r04ah/).  The condensed tableau halves the pass, so at C3 (32,768
+        // rows) the chain is the longer part too: 64 chain CUs with form 23 on the other 192 take
+        // the block from 5.62 to 4.73-4.79 ms (13.4-13.5 k vs 11.4 k pivots/s; 32 CUs 12.7 k, 96
+        // 12.6 k; profiles/r06f/)
         n = std::min(s->rows > 8192 ? 64 : 128, cus / 2);
     }
     const int nco = std::max(1, s->coloc_n);
@@ -3383,6 +3408,7 @@ int dlp_result_timings(const dlp_result* r, double* ms_out) {
     return DLP_OK;
 }
 int dlp_release_cached_memory(int device, int64_t* bytes) {
+    streams_drain(device);
     const size_t n = pool_drain(device < 0 ? kAllDevices : device) + dlp::batched_release(device);
     if (bytes) *bytes = (int64_t)n;
     return DLP_OK;

@@ -195,7 +195,8 @@ int         dlp_update_variants(void);               /* number of rank-1 update 
 /* Sessions return their small buffers (<= 32 MiB each, <= 512 MiB in all) and streams to a
  * per-process cache for the next session, and dlp_batched_solve keeps one context per device
  * (stream, events, tableau / output buffers sized by the largest batch so far).  This frees the
- * cached buffers and batch contexts of `device` (-1: every device and the pinned host buffers);
+ * cached buffers, pooled streams and batch contexts of `device` (-1: every device and the pinned host
+ * buffers);
  * *bytes (may be NULL) = device bytes freed.  A session allocation that fails frees its device's
  * cached session buffers and retries by itself; that hipFree may synchronise the device, so it
  * waits for work other sessions have in flight on it (call this between runs to avoid that). */

@@ -71,7 +71,8 @@ def test_c3_full_size():
     assert np.ascontiguousarray(obj_row[:w]).tobytes() == ref_rows[-1].tobytes()
 
 
-AUTO_K64_FORM = 21   # the streaming K = 64 default (dlp_session.cpp auto_form)
+AUTO_K64_FORM = 23   # the streaming K = 64 default at C3: condensed tableau, lookahead with the chain on 64 CUs
+                     # of its own and the LDS-ring pass on the rest (dlp_session.cpp pick_form, chain_cus_policy)
 
 
 def _sha(a):
