@@ -541,6 +541,24 @@ def c5_cpu_baseline(budget_s):
                       f"{piv} pivots in {secs:.2f} s of solve time (generation not timed)"}
 
 
+def c5_hardware_bound():
+    """The committed SQ-counter summary of the batched kernel (profiles/r*/c5_hardware_bound.json,
+    the latest): VALU-issue and LDS busy fractions, wave states; None when absent."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "c5_hardware_bound.json")))
+    if not paths:
+        return None
+    try:
+        with open(paths[-1]) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    keep = ("valu_issue_util", "lds_util", "wave_parked_frac", "wave_issue_stalled_frac", "effective_clock_ghz")
+    out = {k: d[k] for k in keep if k in d}
+    out["source"] = os.path.relpath(paths[-1], ROOT)
+    return out
+
+
 def c5_main(args):
     """--workload c5: the whole batch solved S times after W warm-ups.  A step = one
     dlp_batched_solve of the batch (tableaus generated on the device, then ONE solve kernel);
@@ -633,6 +651,9 @@ def c5_main(args):
                          "single_lp_us_per_pivot": t1 * 1e6,
                          "batch_us_per_pivot_per_lp": resident / achieved * 1e6,
                          "hbm_frac": bytes_solve / (kern / args.steps) / 1e9 / HBM_PEAK_GBS,
+                         # hardware-anchored: the VALU-issue and LDS busy fractions of the
+                         # same kernel from rocprofv3 SQ counters (committed, profiles/r06o/)
+                         "hardware": c5_hardware_bound(),
                          "fp64_frac": (2.0 * piv[-1] * (m + 1) * (m + n + 1) / (kern / args.steps) / 1e12
                                        / FP64_PEAK_TFS)},
             "cpu_baseline": None if (world > 1 or args.no_cpu_baseline) else c5_cpu_baseline(args.cpu_seconds),

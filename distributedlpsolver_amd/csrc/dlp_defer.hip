@@ -2728,8 +2728,36 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
         if constexpr (K == 64) {
             // ring depth D: 4 groups in flight (DLP_Q_DEPTH = 2 or 3: tuning only)
             static const int qd = std::getenv("DLP_Q_DEPTH") ? std::atoi(std::getenv("DLP_Q_DEPTH")) : 4;
+            // (tuning: DLP_Q_U=4, 4 rows per group — twice the independent fma chains per wave — with
+            // 2 or 3 groups in flight)
+            static const int qu = std::getenv("DLP_Q_U") ? std::atoi(std::getenv("DLP_Q_U")) : 2;
             constexpr int U = 2;
             const int D = qd == 2 || qd == 3 || qd == 6 || qd == 8 ? qd : 4;
+            if (qu == 4) {
+                const int D4 = qd == 3 ? 3 : 2;
+                size_t dyn4 = std::max((size_t)4 * D4 * 128 * 4 * sizeof(double), pass_lds_env());
+                if (occ > 0) dyn4 = std::max(dyn4, (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t));
+                const dim3 grid4((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));
+                if (g.rows > 0) {
+                    if (D4 == 3) {
+                        if (bcnt)
+                            pass_q_kernel<NT, 4, 3, true><<<grid4, 256, dyn4, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
+                                                                                d.C, d.ldc, d.P, d.nzc, rb, bcnt);
+                        else
+                            pass_q_kernel<NT, 4, 3><<<grid4, 256, dyn4, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C,
+                                                                          d.ldc, d.P, d.nzc, rb);
+                    } else {
+                        if (bcnt)
+                            pass_q_kernel<NT, 4, 2, true><<<grid4, 256, dyn4, s>>>(g.T, To, g.ld, g.rows, g.width, bd,
+                                                                                d.C, d.ldc, d.P, d.nzc, rb, bcnt);
+                        else
+                            pass_q_kernel<NT, 4, 2><<<grid4, 256, dyn4, s>>>(g.T, To, g.ld, g.rows, g.width, bd, d.C,
+                                                                          d.ldc, d.P, d.nzc, rb);
+                    }
+                }
+                if (seal < 0) blk_reset_kernel<<<1, 64, 0, s>>>(st);
+                return hipGetLastError();
+            }
             size_t dyn = std::max((size_t)4 * D * 128 * U * sizeof(double), pass_lds_env());
             if (occ > 0) dyn = std::max(dyn, (size_t)160 * 1024 / occ - 1024 * sizeof(int32_t));
             const dim3 grid((unsigned)((g.width + 255) / 256), (unsigned)((g.rows + rb - 1) / rb));

@@ -33,6 +33,7 @@ if kind == "defer":   # one rank of C3 at P = 8 (2.15 GB) or P = 4 (4.3 GB): K =
     with dlp.Session(dlp.Problem.random(m, n, seed), check_interval=64, lookahead=la,
                      max_pivots=200) as s:
         out["lookahead"], out["form"], out["chain_cus"] = s.lookahead(), s.defer_form(), s.chain_cus()
+        out["condensed"] = s.condensed
         st, done = s.run(136)   # two full blocks and a partial one
         r = s.result()
         out.update(done=done, log=h(r.pivot_log), obj=float(r.objective).hex(), basis=h(r.basis),
@@ -54,7 +55,7 @@ print(json.dumps(out))
 def _run(kind, args=(), env=None):
     e = dict(os.environ)
     for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB", "DLP_CHAIN_CUS",
-              "DLP_FAT_PROW", "DLP_TEST_MASK_FAIL"):
+              "DLP_FAT_PROW", "DLP_TEST_MASK_FAIL", "DLP_CONDENSED"):
         e.pop(k, None)
     e.update(env or {})
     p = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, kind, *map(str, args)], env=e,
@@ -82,6 +83,18 @@ def test_lookahead_chain_knobs(env):
         assert got.pop("chain_cus") == int(env["DLP_CHAIN_CUS"])
         ref = {k: v for k, v in ref.items() if k != "chain_cus"}
     assert got == ref
+
+
+@pytest.mark.parametrize("la", [0, 1])
+def test_full_tableau_knob(la):
+    """DLP_CONDENSED=0: the full tableau (every basic column stored) instead of the condensed one
+     — the same pivot log, objective, basis and whole tableau (read back in the full
+    layout), with lookahead (the restart replays in the LEAN chain kernels) and without."""
+    ref = _ref("defer", la)
+    assert ref["condensed"]
+    got = _run("defer", [la], {"DLP_CONDENSED": "0"})
+    assert got.pop("condensed") is False
+    assert got == {k: v for k, v in ref.items() if k != "condensed"}
 
 
 def test_cu_split_with_the_form23_pass():
