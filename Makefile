@@ -42,12 +42,15 @@ clean:
 
 .PHONY: all oracle ref asm clean
 
-tools: build/hbm_ceiling build/fetch_calib
+tools: build/hbm_ceiling build/fetch_calib build/chainlab
 
 build/hbm_ceiling: tools/hbm_ceiling.hip | build
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 build/fetch_calib: tools/fetch_calib.hip | build
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
+build/chainlab: tools/chainlab.hip | build
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -o $@ $<
 
 .PHONY: tools

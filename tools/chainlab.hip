@@ -1,0 +1,588 @@
+// chainlab.hip — the selection chain's two replay loops in isolation (the P = 8 chain).
+// Per pivot the ratio launch replays J steps of the coefficient chain on one column (one row per
+// lane: a = pq[l] on the step's pivot row, else fma(-C[l][i], pq[l], a) where C[l][i] != 0), and
+// the pivot-row launch replays S pivot rows on one row (per column c: t = P[l][c] on the step
+// whose pivot row it is, else fma(-cp[l], P[l][c], t) where cp[l] != 0).  Every variant below
+// computes the same values in the same order and is checked bit for bit against a one-lane-per-
+// element kernel with plain loads.
+//   ratio variants (rows, J):
+//     ring    the product's LEAN ring (ratio_defer_body, RING): 64 rows per wave, 2 steps per
+//             16-B LDS-DMA, 8 DMAs in flight, one wait + LDS round trip per pair of steps
+//     ringg   the same ring, 16 DMAs in flight, 4 pairs (8 steps) per wait and LDS round trip
+//     r16     16 rows per wave (4x the waves), 8 steps per DMA, 8 DMAs in flight, one wait per 8 steps
+//     reg     one row per lane, coefficients in registers, 2 x 16 loads in flight (ratio_mid_kernel)
+//   pivot-row variants (ncols, S):
+//     fat     the product's register replay (prow_defer_body, !LEAN): 2 columns per lane, 2 x 16 rows
+//     fat1    1 column per lane, 2 x 32 rows in flight (twice the waves)
+//     ringg   2 columns per lane, LDS ring of 16 rows, 4 rows per wait and LDS round trip
+//     ring1   1 column per lane, 2 rows per DMA, 16 DMAs in flight, 4 DMAs (8 rows) per wait
+// The chain runs on CU-mask bits [0, cus) like the product's split (cus = 0: every CU).
+//   build: hipcc --offload-arch=gfx950 -O3 -o build/chainlab tools/chainlab.hip
+//   run:   build/chainlab ratio <variant> <rows> <J> <cus> [copies]
+//          build/chainlab prow  <variant> <ncols> <S> <cus> [copies]
+// copies > 1 rotates over that many copies of the inputs per launch (defeats L2 / Infinity Cache).
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e = (x);                                                     \
+        if (e != hipSuccess) {                                                  \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));         \
+            std::exit(1);                                                       \
+        }                                                                       \
+    } while (0)
+
+constexpr int kMaxJ = 128;
+
+__device__ __forceinline__ void glds16(const void* g, uint32_t m0) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p);
+}
+
+// ---------------------------------------------------------------- ratio replay
+// inputs: Cc[l * ldcc + i] (column-major coefficient chain), a0[i], pq[l], pl[l]; out[i]
+__global__ void r_ref(const double* Cc, int64_t ldcc, const double* a0, const double* pq, const int* pl, int J,
+                      int64_t rows, double* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows) return;
+    double a = a0[i];
+    for (int l = 0; l < J; ++l) {
+        const double f = Cc[(int64_t)l * ldcc + i];
+        if (i == pl[l])
+            a = pq[l];
+        else if (f != 0.0)
+            a = __builtin_fma(-f, pq[l], a);
+    }
+    out[i] = a;
+}
+
+// the product's ring (RP DMAs in flight, G pairs per wait; G = 1: ratio_defer_body's loop)
+template <int RP, int G>
+__global__ __launch_bounds__(256) void r_ring(const double* Cc, int64_t ldcc, const double* a0, const double* pqg,
+                                             const int* plg, int J, int64_t rows, double* out) {
+    __shared__ double s_pq[kMaxJ + 2 * G];
+    __shared__ int s_pl[kMaxJ + 2 * G];
+    extern __shared__ double s_dyn[];
+    for (int l = threadIdx.x; l < kMaxJ + 2 * G; l += blockDim.x) {
+        s_pq[l] = l < J ? pqg[l] : 0.0;
+        s_pl[l] = l < J ? plg[l] : -1;
+    }
+    const int wl = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + wv * 64;
+    const int64_t i = i0 + wl;
+    auto ring_at = [&](int p) { return s_dyn + (wv * RP + p % RP) * 128; };
+    auto sbase = [&](int l) -> const double* {
+        l = l < J ? l : J - 1;
+        return Cc + (int64_t)l * ldcc + i0;
+    };
+    auto csrc = [&](int p) -> const double* { return ((wl >> 5) ? sbase(2 * p + 1) : sbase(2 * p)) + 2 * (wl & 31); };
+    const bool wave_rows = i0 < rows;
+    if (wave_rows)
+#pragma unroll
+        for (int p = 0; p < RP; ++p) glds16(csrc(p), lds_addr(ring_at(p)));
+    double a = i < rows ? a0[i] : 0.0;
+    __syncthreads();
+    auto step = [&](int l, double fv, bool ok) {
+        const double pq = s_pq[l];
+        const bool piv = i == s_pl[l];
+        const double u = __builtin_fma(-fv, pq, a);
+        a = ok ? (piv ? pq : (fv != 0.0 ? u : a)) : a;
+    };
+    if (wave_rows) {
+        const int npairs = (J + 1) >> 1;
+        if constexpr (G == 1) {
+            for (int p = 0; p < npairs; ++p) {
+                vmwait<RP - 1>();
+                double* rs = ring_at(p);
+                const double f0 = rs[wl], f1 = rs[64 + wl];
+                step(2 * p, f0, true);
+                step(2 * p + 1, f1, 2 * p + 1 < J);
+                glds16(csrc(p + RP), lds_addr(rs));
+            }
+        } else {
+            for (int p0 = 0; p0 < npairs; p0 += G) {
+                vmwait<RP - G>();
+                double f[2 * G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const double* rs = ring_at(p0 + g);
+                    f[2 * g] = rs[wl];
+                    f[2 * g + 1] = rs[64 + wl];
+                }
+#pragma unroll
+                for (int g = 0; g < 2 * G; ++g) step(2 * p0 + g, f[g], 2 * p0 + g < J);
+#pragma unroll
+                for (int g = 0; g < G; ++g) glds16(csrc(p0 + g + RP), lds_addr(ring_at(p0 + g)));
+            }
+        }
+        vmwait<0>();
+    }
+    if (i < rows) out[i] = a;
+}
+
+// 16 rows per wave: DMA p brings steps 8p..8p+7 of the wave's 16 rows (lane x: step 8p + x / 8,
+// rows 2 (x % 8), +1); lane r < 16 replays row i0 + r
+template <int RP>
+__global__ __launch_bounds__(256) void r_r16(const double* Cc, int64_t ldcc, const double* a0, const double* pqg,
+                                            const int* plg, int J, int64_t rows, double* out) {
+    __shared__ double s_pq[kMaxJ + 8];
+    __shared__ int s_pl[kMaxJ + 8];
+    extern __shared__ double s_dyn[];
+    for (int l = threadIdx.x; l < kMaxJ + 8; l += blockDim.x) {
+        s_pq[l] = l < J ? pqg[l] : 0.0;
+        s_pl[l] = l < J ? plg[l] : -1;
+    }
+    const int wl = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t i0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * 16;
+    const int r = wl & 15;
+    const int64_t i = i0 + r;
+    auto ring_at = [&](int p) { return s_dyn + (wv * RP + p % RP) * 128; };
+    auto csrc = [&](int p) -> const double* {
+        int l = 8 * p + (wl >> 3);
+        l = l < J ? l : J - 1;
+        return Cc + (int64_t)l * ldcc + i0 + 2 * (wl & 7);
+    };
+    const bool wave_rows = i0 < rows;
+    if (wave_rows)
+#pragma unroll
+        for (int p = 0; p < RP; ++p) glds16(csrc(p), lds_addr(ring_at(p)));
+    double a = i < rows ? a0[i] : 0.0;
+    __syncthreads();
+    if (wave_rows) {
+        const int nd = (J + 7) >> 3;
+        for (int p = 0; p < nd; ++p) {
+            vmwait<RP - 1>();
+            const double* rs = ring_at(p);
+            double f[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) f[k] = rs[k * 16 + r];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int l = 8 * p + k;
+                const double pq = s_pq[l];
+                const bool piv = i == s_pl[l];
+                const double u = __builtin_fma(-f[k], pq, a);
+                a = l < J ? (piv ? pq : (f[k] != 0.0 ? u : a)) : a;
+            }
+            glds16(csrc(p + RP), lds_addr(ring_at(p)));
+        }
+        vmwait<0>();
+    }
+    if (wl < 16 && i < rows) out[i] = a;
+}
+
+// registers: one row per lane, 2 x CH coefficient loads in flight
+template <int CH>
+__global__ __launch_bounds__(256) void r_reg(const double* Cc, int64_t ldcc, const double* a0, const double* pqg,
+                                            const int* plg, int J, int64_t rows, double* out) {
+    __shared__ double s_pq[kMaxJ];
+    __shared__ int s_pl[kMaxJ];
+    for (int l = threadIdx.x; l < J; l += blockDim.x) {
+        s_pq[l] = pqg[l];
+        s_pl[l] = plg[l];
+    }
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ic = i < rows ? i : rows - 1;
+    double a = a0[ic];
+    __syncthreads();
+    double fa[CH], fb[CH];
+    auto fetch = [&](double (&f)[CH], int l0) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) f[u] = l0 + u < J ? Cc[(int64_t)(l0 + u) * ldcc + ic] : 0.0;
+    };
+    auto apply = [&](const double (&f)[CH], int l0) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int l = l0 + u;
+            if (l < J) {
+                if (i == s_pl[l])
+                    a = s_pq[l];
+                else if (f[u] != 0.0)
+                    a = __builtin_fma(-f[u], s_pq[l], a);
+            }
+        }
+    };
+    fetch(fa, 0);
+    for (int l0 = 0; l0 < J; l0 += 2 * CH) {
+        if (l0 + CH < J) fetch(fb, l0 + CH);
+        apply(fa, l0);
+        if (l0 + CH >= J) break;
+        if (l0 + 2 * CH < J) fetch(fa, l0 + 2 * CH);
+        apply(fb, l0 + CH);
+    }
+    if (i < rows) out[i] = a;
+}
+
+// ---------------------------------------------------------------- pivot-row replay
+// inputs: P[l * ld + c] (S pivot rows), t0[c], cp[l], piv[l] (1: step l's pivot row is row p); out[c]
+__global__ void p_ref(const double* P, int64_t ld, const double* t0, const double* cp, const int* piv, int S,
+                      int64_t ncols, double* out) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncols) return;
+    double t = t0[c];
+    for (int l = 0; l < S; ++l) {
+        const double pv = P[(int64_t)l * ld + c];
+        if (piv[l])
+            t = pv;
+        else if (cp[l] != 0.0)
+            t = __builtin_fma(-cp[l], pv, t);
+    }
+    out[c] = t;
+}
+
+// the product's register replay: 2 columns per lane, 2 x CH rows in flight
+template <int CH>
+__global__ __launch_bounds__(256) void p_fat(const double* P, int64_t ld, const double* t0g, const double* cpg,
+                                            const int* pivg, int S, int64_t ncols, double* out) {
+    __shared__ double s_cp[kMaxJ];
+    __shared__ int s_pv[kMaxJ];
+    for (int l = threadIdx.x; l < S; l += blockDim.x) {
+        s_cp[l] = cpg[l];
+        s_pv[l] = pivg[l];
+    }
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    const bool lane = j < ld;
+    d2 t = lane ? *(const d2*)(t0g + j) : d2{0.0, 0.0};
+    __syncthreads();
+    if (lane) {
+        d2 pa[CH], pb[CH];
+        auto fetch = [&](d2 (&pv)[CH], int l0) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int l = min(l0 + u, S - 1);
+                pv[u] = *(const d2*)(P + (int64_t)l * ld + j);
+            }
+        };
+        auto apply = [&](const d2 (&pv)[CH], int l0) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int l = l0 + u;
+                if (l < S) {
+                    if (s_pv[l]) {
+                        t = pv[u];
+                    } else if (s_cp[l] != 0.0) {
+                        t.x = __builtin_fma(-s_cp[l], pv[u].x, t.x);
+                        t.y = __builtin_fma(-s_cp[l], pv[u].y, t.y);
+                    }
+                }
+            }
+        };
+        if (S > 0) fetch(pa, 0);
+        for (int l0 = 0; l0 < S; l0 += 2 * CH) {
+            if (l0 + CH < S) fetch(pb, l0 + CH);
+            apply(pa, l0);
+            if (l0 + CH >= S) break;
+            if (l0 + 2 * CH < S) fetch(pa, l0 + 2 * CH);
+            apply(pb, l0 + CH);
+        }
+        if (j < ncols) out[j] = t.x;
+        if (j + 1 < ncols) out[j + 1] = t.y;
+    }
+}
+
+// 1 column per lane, 2 x CH rows in flight
+template <int CH>
+__global__ __launch_bounds__(256) void p_fat1(const double* P, int64_t ld, const double* t0g, const double* cpg,
+                                             const int* pivg, int S, int64_t ncols, double* out) {
+    __shared__ double s_cp[kMaxJ];
+    __shared__ int s_pv[kMaxJ];
+    for (int l = threadIdx.x; l < S; l += blockDim.x) {
+        s_cp[l] = cpg[l];
+        s_pv[l] = pivg[l];
+    }
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool lane = c < ld;
+    double t = lane ? t0g[c] : 0.0;
+    __syncthreads();
+    if (lane) {
+        double pa[CH], pb[CH];
+        auto fetch = [&](double (&pv)[CH], int l0) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int l = min(l0 + u, S - 1);
+                pv[u] = P[(int64_t)l * ld + c];
+            }
+        };
+        auto apply = [&](const double (&pv)[CH], int l0) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int l = l0 + u;
+                if (l < S) {
+                    if (s_pv[l])
+                        t = pv[u];
+                    else if (s_cp[l] != 0.0)
+                        t = __builtin_fma(-s_cp[l], pv[u], t);
+                }
+            }
+        };
+        if (S > 0) fetch(pa, 0);
+        for (int l0 = 0; l0 < S; l0 += 2 * CH) {
+            if (l0 + CH < S) fetch(pb, l0 + CH);
+            apply(pa, l0);
+            if (l0 + CH >= S) break;
+            if (l0 + 2 * CH < S) fetch(pa, l0 + 2 * CH);
+            apply(pb, l0 + CH);
+        }
+        if (c < ncols) out[c] = t;
+    }
+}
+
+// LDS ring, 2 columns per lane: RING rows in flight (1 KB per wave per row), G rows per wait
+template <int RING, int G>
+__global__ __launch_bounds__(256) void p_ringg(const double* P, int64_t ld, const double* t0g, const double* cpg,
+                                              const int* pivg, int S, int64_t ncols, double* out) {
+    __shared__ double s_cp[kMaxJ + G];
+    __shared__ int s_pv[kMaxJ + G];
+    extern __shared__ double s_dyn[];
+    for (int l = threadIdx.x; l < kMaxJ + G; l += blockDim.x) {
+        s_cp[l] = l < S ? cpg[l] : 0.0;
+        s_pv[l] = l < S ? pivg[l] : 0;
+    }
+    const int wv = threadIdx.x >> 6, wl = threadIdx.x & 63;
+    const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+    const bool lane = j < ld;
+    auto slot = [&](int l) { return s_dyn + (wv * RING + l % RING) * 128; };
+    auto psrc = [&](int l) -> const double* {
+        l = l < S ? l : S - 1;
+        return P + (int64_t)l * ld + j;
+    };
+    if (lane)
+#pragma unroll
+        for (int r = 0; r < RING; ++r) glds16(psrc(r), lds_addr(slot(r)));
+    d2 t = lane ? *(const d2*)(t0g + j) : d2{0.0, 0.0};
+    __syncthreads();
+    if (lane) {
+        asm volatile("" ::"v"(t.x), "v"(t.y));
+        for (int l0 = 0; l0 < S; l0 += G) {
+            vmwait<RING - G>();
+            d2 pv[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) pv[g] = *(const d2*)&slot(l0 + g)[2 * wl];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int l = l0 + g;
+                const double cp = s_cp[l];
+                const bool piv = s_pv[l] != 0;
+                const double ux = __builtin_fma(-cp, pv[g].x, t.x), uy = __builtin_fma(-cp, pv[g].y, t.y);
+                const bool ok = l < S;
+                t.x = ok ? (piv ? pv[g].x : (cp != 0.0 ? ux : t.x)) : t.x;
+                t.y = ok ? (piv ? pv[g].y : (cp != 0.0 ? uy : t.y)) : t.y;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) glds16(psrc(l0 + g + RING), lds_addr(slot(l0 + g)));
+        }
+        vmwait<0>();
+        if (j < ncols) out[j] = t.x;
+        if (j + 1 < ncols) out[j + 1] = t.y;
+    }
+}
+
+// LDS ring, 1 column per lane: DMA p brings rows 2p (lanes 0-31) and 2p+1 (lanes 32-63) of the
+// wave's 64 columns; RD DMAs in flight, G DMAs per wait
+template <int RD, int G>
+__global__ __launch_bounds__(256) void p_ring1(const double* P, int64_t ld, const double* t0g, const double* cpg,
+                                              const int* pivg, int S, int64_t ncols, double* out) {
+    __shared__ double s_cp[kMaxJ + 2 * G];
+    __shared__ int s_pv[kMaxJ + 2 * G];
+    extern __shared__ double s_dyn[];
+    for (int l = threadIdx.x; l < kMaxJ + 2 * G; l += blockDim.x) {
+        s_cp[l] = l < S ? cpg[l] : 0.0;
+        s_pv[l] = l < S ? pivg[l] : 0;
+    }
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wl = threadIdx.x & 63;
+    const int64_t c0 = (int64_t)blockIdx.x * blockDim.x + wv * 64;
+    const int64_t c = c0 + wl;
+    const bool wave = c0 < ld;
+    auto slot = [&](int p) { return s_dyn + (wv * RD + p % RD) * 128; };
+    auto psrc = [&](int p) -> const double* {
+        int l = 2 * p + (wl >> 5);
+        l = l < S ? l : S - 1;
+        return P + (int64_t)l * ld + c0 + 2 * (wl & 31);
+    };
+    if (wave)
+#pragma unroll
+        for (int p = 0; p < RD; ++p) glds16(psrc(p), lds_addr(slot(p)));
+    double t = c < ld ? t0g[c] : 0.0;
+    __syncthreads();
+    if (wave) {
+        asm volatile("" ::"v"(t));
+        const int nd = (S + 1) >> 1;
+        for (int p0 = 0; p0 < nd; p0 += G) {
+            vmwait<RD - G>();
+            double pv[2 * G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const double* rs = slot(p0 + g);
+                pv[2 * g] = rs[wl];
+                pv[2 * g + 1] = rs[64 + wl];
+            }
+#pragma unroll
+            for (int g = 0; g < 2 * G; ++g) {
+                const int l = 2 * p0 + g;
+                const double cp = s_cp[l];
+                const bool piv = s_pv[l] != 0;
+                const double u = __builtin_fma(-cp, pv[g], t);
+                t = l < S ? (piv ? pv[g] : (cp != 0.0 ? u : t)) : t;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) glds16(psrc(p0 + g + RD), lds_addr(slot(p0 + g)));
+        }
+        vmwait<0>();
+        if (c < ncols) out[c] = t;
+    }
+}
+
+__global__ void empty_kernel(double* out) {
+    if (threadIdx.x == 1024) out[0] = 1.0;
+}
+
+// ---------------------------------------------------------------- host
+static uint64_t g_rng = 0x9E3779B97F4A7C15ull;
+static uint64_t rnd() {
+    uint64_t z = (g_rng += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static double rndd() { return (double)(rnd() >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0; }
+
+int main(int argc, char** argv) {
+    if (argc < 6) {
+        std::fprintf(stderr, "usage: chainlab ratio|prow <variant> <n> <steps> <cus> [copies]\n");
+        return 2;
+    }
+    const bool ratio = !std::strcmp(argv[1], "ratio");
+    const char* var = argv[2];
+    const int64_t n = std::atoll(argv[3]);
+    const int J = std::atoi(argv[4]);
+    const int cus = std::atoi(argv[5]);
+    const int copies = argc > 6 ? std::max(1, std::atoi(argv[6])) : 1;
+    if (J < 1 || J > kMaxJ || n < 64 || n % 64) {
+        std::fprintf(stderr, "need 1 <= steps <= %d and n a multiple of 64\n", kMaxJ);
+        return 2;
+    }
+    const int64_t ld = (n + 1 + 127) / 128 * 128;   // leading dimension (rows of Cc / columns of P)
+    // one copy: J x ld chain / pivot rows, the start vector; the step tables shared
+    std::vector<double> h_chain((size_t)J * ld), h_start(ld), h_sv(J);
+    std::vector<int> h_si(J);
+    for (auto& v : h_chain) v = (rnd() % 10 < 3) ? 0.0 : rndd();
+    for (auto& v : h_start) v = rndd();
+    for (int l = 0; l < J; ++l) {
+        h_sv[l] = (l % 7 == 3) ? 0.0 : rndd();
+        h_si[l] = ratio ? (int)(rnd() % n) : (l % 23 == 5 ? 1 : 0);
+    }
+    double *d_chain, *d_start, *d_sv, *d_out, *d_ref;
+    int* d_si;
+    const size_t chain_bytes = (size_t)J * ld * sizeof(double);
+    CK(hipMalloc(&d_chain, chain_bytes * copies));
+    for (int c = 0; c < copies; ++c)
+        CK(hipMemcpy((char*)d_chain + c * chain_bytes, h_chain.data(), chain_bytes, hipMemcpyHostToDevice));
+    CK(hipMalloc(&d_start, ld * sizeof(double)));
+    CK(hipMemcpy(d_start, h_start.data(), ld * sizeof(double), hipMemcpyHostToDevice));
+    CK(hipMalloc(&d_sv, J * sizeof(double)));
+    CK(hipMemcpy(d_sv, h_sv.data(), J * sizeof(double), hipMemcpyHostToDevice));
+    CK(hipMalloc(&d_si, J * sizeof(int)));
+    CK(hipMemcpy(d_si, h_si.data(), J * sizeof(int), hipMemcpyHostToDevice));
+    CK(hipMalloc(&d_out, ld * sizeof(double)));
+    CK(hipMalloc(&d_ref, ld * sizeof(double)));
+
+    hipStream_t s;
+    if (cus > 0) {
+        uint32_t mask[8] = {};
+        for (int b = 0; b < cus && b < 256; ++b) mask[b / 32] |= 1u << (b % 32);
+        CK(hipExtStreamCreateWithCUMask(&s, 8, mask));
+    } else {
+        CK(hipStreamCreate(&s));
+    }
+    if (ratio)
+        r_ref<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(d_chain, ld, d_start, d_sv, d_si, J, n, d_ref);
+    else
+        p_ref<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(d_chain, ld, d_start, d_sv, d_si, J, n, d_ref);
+    CK(hipGetLastError());
+
+    // threads per workgroup: ratio 128 (the product at <= 8,192 rows per rank) or 256 above
+    const int rthr = n <= 8192 ? 128 : 256;
+    auto launch = [&](int c) -> bool {
+        const double* ch = (const double*)((const char*)d_chain + (size_t)(c % copies) * chain_bytes);
+        if (ratio) {
+            const unsigned nb = (unsigned)((n + rthr - 1) / rthr);
+            if (!std::strcmp(var, "ring"))
+                r_ring<8, 1><<<nb, rthr, (rthr / 64) * 8 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "ringg"))
+                r_ring<16, 4><<<nb, rthr, (rthr / 64) * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "ringg2"))
+                r_ring<16, 2><<<nb, rthr, (rthr / 64) * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "r16"))
+                r_r16<8><<<(unsigned)((n / 16 + rthr / 64 - 1) / (rthr / 64)), rthr, (rthr / 64) * 8 * 1024, s>>>(
+                    ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "reg"))
+                r_reg<16><<<nb, rthr, 0, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else
+                return false;
+        } else {
+            const unsigned nb2 = (unsigned)((ld / 2 + 255) / 256), nb1 = (unsigned)((ld + 255) / 256);
+            if (!std::strcmp(var, "fat"))
+                p_fat<16><<<nb2, 256, 0, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "fat1"))
+                p_fat1<32><<<nb1, 256, 0, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "ringg"))
+                p_ringg<16, 4><<<nb2, 256, 4 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "ring8"))
+                p_ringg<8, 1><<<nb2, 256, 4 * 8 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "ring1"))
+                p_ring1<16, 4><<<nb1, 256, 4 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else
+                return false;
+        }
+        return true;
+    };
+    if (!launch(0)) {
+        std::fprintf(stderr, "unknown variant %s\n", var);
+        return 2;
+    }
+    CK(hipGetLastError());
+    CK(hipStreamSynchronize(s));
+    std::vector<double> ho(ld), hr(ld);
+    CK(hipMemcpy(ho.data(), d_out, n * sizeof(double), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hr.data(), d_ref, n * sizeof(double), hipMemcpyDeviceToHost));
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i)
+        if (std::memcmp(&ho[i], &hr[i], sizeof(double))) ++bad;
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 200;
+    for (int w = 0; w < 20; ++w) launch(w);
+    CK(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) launch(r);
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) empty_kernel<<<1, 64, 0, s>>>(d_out);
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms0 = 0.f;
+    CK(hipEventElapsedTime(&ms0, e0, e1));
+    std::printf("{\"kernel\": \"%s\", \"variant\": \"%s\", \"n\": %lld, \"steps\": %d, \"cus\": %d, \"copies\": %d, "
+                "\"us_per_launch\": %.2f, \"empty_us\": %.2f, \"mismatches\": %lld}\n",
+                argv[1], var, (long long)n, J, cus, copies, ms * 1e3 / reps, ms0 * 1e3 / reps, (long long)bad);
+    return bad ? 1 : 0;
+}
