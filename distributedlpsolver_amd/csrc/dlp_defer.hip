@@ -140,7 +140,13 @@ __device__ int g_chain_stamps_on;
 // (RP = kRatioRingPairs: 16 measured equal at C3, 8,239-8,267 vs 8,262-8,263 pivots/s, profiles/r04c/)
 constexpr int kRatioRingPairs = 8;
 constexpr size_t ratio_ring_bytes(int rp) { return (size_t)(kRatioDeferThreads / 64) * rp * 128 * sizeof(double); }
-template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4, int RP = kRatioRingPairs, bool DB = false>
+// ROWS / RG (the ring only, round 6): ROWS rows per wave (64, 32, 16; 128 / ROWS steps per 1-KB
+// DMA, lane x bringing step x / (ROWS / 2) of rows 2 (x % (ROWS / 2)), +1) and RG DMAs retired per
+// wait, their LDS reads issued together: one wait and one LDS round trip per 2 RG (ROWS 64) steps
+// instead of per pair.  A workgroup of blockDim.x lanes covers blockDim.x ROWS / 64 rows; lanes
+// wl >= ROWS hold no row.  ROWS = 64, RG = 1 is the LEAN loop beside the pass.
+template <int KMAX, bool FUSED, bool LEAN = false, int LCH = 4, int RP = kRatioRingPairs, bool DB = false,
+          int ROWS = 64, int RG = 1>
 __device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
     int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
@@ -151,11 +157,15 @@ __device__ __forceinline__ void ratio_defer_body(
     const double* __restrict__ Pp = nullptr, int prev_seal = -1, const XPeers* xp = nullptr,
     uint32_t xseq = 0, uint32_t* bcnt = nullptr, int brb = 1, int bnt = 0, const double* Tn = nullptr,
     int xsel = 0, uint32_t rseq = 0, Cond cd = Cond{}) {
-    __shared__ PricePart lds_pp[kRatioDeferThreads / 64];
-    __shared__ Cand lds_c[kRatioDeferThreads / 64];
+    // (the grouped ring reads up to 128 / ROWS * (RG + 1) table entries past J - 1, dropped)
+    constexpr bool GRING = ROWS != 64 || RG != 1;
+    constexpr int kPad = GRING ? 128 / ROWS * (RG + 1) : 0;
+    constexpr int kWaves = GRING ? 16 : kRatioDeferThreads / 64;
+    __shared__ PricePart lds_pp[kWaves];
+    __shared__ Cand lds_c[kWaves];
     __shared__ int s_last;
-    __shared__ double s_pq[KMAX], s_pn[KMAX];
-    __shared__ int32_t s_pl[KMAX];
+    __shared__ double s_pq[KMAX + kPad], s_pn[KMAX];
+    __shared__ int32_t s_pl[KMAX + kPad];
     auto cand_red = [&](Cand v) { return block_cand(v, lds_c); };
     // this lane's pricing partial is requested first: it depends on nothing, and the reduce
     // below then waits for it alongside the step-table loads instead of after them
@@ -169,7 +179,14 @@ __device__ __forceinline__ void ratio_defer_body(
     const int j = st->blk;
     const int kp = prev_seal >= 0 ? st->seal[prev_seal].blk : 0;
     const int J = kp + j;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int wl = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the wave's rows [i0, i0 + ROWS); this lane's row i (none: far past every bound)
+    const bool lane_row = !GRING || wl < ROWS;
+    const int64_t i0 = GRING ? (int64_t)blockIdx.x * (blockDim.x / 64 * ROWS) + wv * ROWS
+                             : (int64_t)blockIdx.x * blockDim.x + wv * 64;
+    const int64_t i = !GRING ? (int64_t)blockIdx.x * blockDim.x + threadIdx.x
+                             : (lane_row ? i0 + wl : ((int64_t)1 << 62));
     for (int l = threadIdx.x; l < J; l += blockDim.x) {
         s_pn[l] = l < kp ? Pp[(int64_t)l * ld + ncols] : P[(int64_t)(l - kp) * ld + ncols];
         s_pl[l] = l < kp ? st->seal[prev_seal].pl[l] : st->pl[l - kp];
@@ -179,17 +196,15 @@ __device__ __forceinline__ void ratio_defer_body(
     // first DMAs are issued here and land during the pricing reduce.  Steps past J-1 re-read
     // step J-1 (harmless), so every pair issues exactly one DMA.
     constexpr bool RING = LEAN && LCH == 0;
+    constexpr int SPD = 128 / ROWS, HL = ROWS / 2;   // steps per DMA; lanes per step
     extern __shared__ double s_dyn[];
-    const int wl = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + wv * 64;
-    const bool wave_rows = i0 < rows;   // (i0 + 63 < ldcc = round64(rows + 1))
+    const bool wave_rows = i0 < rows;   // (i0 + ROWS - 1 < ldcc = round64(rows + 1))
     // band publication (RING): the wave's 64 rows final in Tn (their bands of the sealed
     // block's pass are done): start there and replay this block's steps only
     bool wdone = false;
     if constexpr (LEAN)
-        if (bcnt && kp > 0 && i0 + 63 < rows) {
-            const int64_t b0 = i0 / brb, b1 = (i0 + 63) / brb;
+        if (bcnt && kp > 0 && i0 + ROWS - 1 < rows) {
+            const int64_t b0 = i0 / brb, b1 = (i0 + ROWS - 1) / brb;
             const uint32_t c0 = __hip_atomic_load(&bcnt[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t c1 = b1 == b0 ? c0 : __hip_atomic_load(&bcnt[b1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             wdone = __builtin_amdgcn_readfirstlane(c0 == (uint32_t)bnt && c1 == (uint32_t)bnt ? 1 : 0) != 0;
@@ -201,7 +216,10 @@ __device__ __forceinline__ void ratio_defer_body(
         return (l < kp ? Ccp + (int64_t)l * ldcc : Cc + (int64_t)(l - kp) * ldcc) + i0;
     };
     auto csrc = [&](int p) -> const double* {
-        return ((wl >> 5) ? sbase(L0 + 2 * p + 1) : sbase(L0 + 2 * p)) + 2 * (wl & 31);
+        if constexpr (ROWS == 64)
+            return ((wl >> 5) ? sbase(L0 + 2 * p + 1) : sbase(L0 + 2 * p)) + 2 * (wl & 31);
+        else
+            return sbase(L0 + SPD * p + wl / HL) + 2 * (wl % HL);
     };
     if constexpr (RING)
         if (wave_rows && J > L0)
@@ -293,19 +311,39 @@ __device__ __forceinline__ void ratio_defer_body(
             flast = ok ? fv : flast;
         };
         if (wave_rows) {
-            const int npairs = (J - L0 + 1) >> 1;
-            for (int p = 0; p < npairs; ++p) {
-                vmwait<RP - 1>();   // pair p landed: only ring DMAs issue in this loop
-                double* rs = ring_at(p);
-                const double f0 = rs[wl], f1 = rs[64 + wl];
-                step(L0 + 2 * p, f0, true);
-                step(L0 + 2 * p + 1, f1, L0 + 2 * p + 1 < J);
-                glds16(csrc(p + RP), lds_addr(rs));
+            const int npairs = (J - L0 + SPD - 1) / SPD;   // (DMAs holding replayed steps)
+            if constexpr (!GRING) {
+                for (int p = 0; p < npairs; ++p) {
+                    vmwait<RP - 1>();   // pair p landed: only ring DMAs issue in this loop
+                    double* rs = ring_at(p);
+                    const double f0 = rs[wl], f1 = rs[64 + wl];
+                    step(L0 + 2 * p, f0, true);
+                    step(L0 + 2 * p + 1, f1, L0 + 2 * p + 1 < J);
+                    glds16(csrc(p + RP), lds_addr(rs));
+                }
+            } else {
+                // RG DMAs per wait: their LDS reads together, then the SPD RG steps, then RG refills
+                // (a group past the last DMA re-reads clamped steps, dropped: every group issues RG)
+                const int r = wl % ROWS;
+                for (int p0 = 0; p0 < npairs; p0 += RG) {
+                    vmwait<RP - RG>();
+                    double fq[SPD * RG];
+#pragma unroll
+                    for (int g = 0; g < RG; ++g) {
+                        const double* rs = ring_at(p0 + g);
+#pragma unroll
+                        for (int k = 0; k < SPD; ++k) fq[g * SPD + k] = rs[k * ROWS + r];
+                    }
+#pragma unroll
+                    for (int u = 0; u < SPD * RG; ++u) step(L0 + SPD * p0 + u, fq[u], L0 + SPD * p0 + u < J);
+#pragma unroll
+                    for (int g = 0; g < RG; ++g) glds16(csrc(p0 + g + RP), lds_addr(ring_at(p0 + g)));
+                }
             }
             vmwait<0>();
             // no step replayed (first selection of a block on a finished band): the RHS cache
             // still advances by the sealed block's last step
-            if (npairs == 0 && J > 0) flast = Ccp[(int64_t)(kp - 1) * ldcc + i];
+            if (npairs == 0 && J > 0 && lane_row) flast = Ccp[(int64_t)(kp - 1) * ldcc + i];
             // (condensed: the restart step zeroed every lane of the wave; the objective row is
             // never replayed, its z_q is current)
             if (R >= L0 && i == rows) a = T[i * ld + sq];
@@ -543,6 +581,27 @@ __global__ __launch_bounds__(kRatioDeferThreads) __attribute__((amdgpu_num_vgpr(
                                         ldc, Cc, ldcc, P, rhs, nzc, partials, cand_out, nranks, tol_dj,
                                         tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal,
                                         xp, xseq, bcnt, brb, bnt, Tn, xsel, 0, cd);
+}
+
+// The grouped ring (round 6): the selection kernel of a chain on CUs of its own (the lookahead's
+// disjoint CU masks: no pass waves beside it, so no 32-VGPR budget).  ROWS rows per wave, RP DMAs
+// in flight, RG retired per wait (tools/chainlab.hip, profiles/r06q/-r06s/).  Launched with
+// rthreads x 64 / ROWS lanes, so a workgroup covers the session's rthreads rows and the grid, the
+// partials and the exchange's candidate slots are those of every other ratio kernel.
+template <int ROWS, int RP, int RG>
+__global__ __launch_bounds__(1024) void ratio_ring_kernel(
+    const double* __restrict__ T, int64_t ld, int64_t rows, int64_t rows_elig, int64_t ncols,
+    int64_t row_first, int32_t* basis, const PricePart* __restrict__ pp, int ntiles,
+    DevState* st, double* __restrict__ C, int64_t ldc, double* __restrict__ Cc, int64_t ldcc,
+    const double* __restrict__ P, double* __restrict__ rhs, int32_t* __restrict__ nzc,
+    Cand* partials, Cand* cand_out, int nranks, double tol_dj, double tol_piv, int pricing,
+    dlp_pivot* log, int64_t log_cap, const double* __restrict__ Ccp, const double* __restrict__ Pp,
+    int prev_seal, const XPeers* xp, uint32_t xseq, uint32_t* bcnt, int brb, int bnt, const double* Tn,
+    int xsel, Cond cd) {
+    ratio_defer_body<128, false, true, 0, RP, false, ROWS, RG>(
+        T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C, ldc, Cc, ldcc, P, rhs, nzc, partials,
+        cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, (int)gridDim.x, Ccp, Pp, prev_seal, xp, xseq, bcnt,
+        brb, bnt, Tn, xsel, 0, cd);
 }
 
 // P[s] := pr for columns j, j+1; objective row z -= z_q * P[s] (z_q != 0);
@@ -2413,6 +2472,17 @@ __global__ __launch_bounds__(64) void seal_kernel(DevState* st, int slot, uint32
 
 }  // namespace
 
+// Rows per wave of the grouped ring.  In isolation (chainlab, cold inputs, 127 / 64 replayed steps)
+// it replays 1.6-2x faster than the LEAN ring: 64 rows per wave on 256-lane workgroups (C3 rows on
+// 64 CUs: 20.4 / 10.0 us vs 36.4 / 14.0), 32 on the rank geometries' 128-lane ones (c3r4 on 128
+// CUs: 11.9 / 6.8 vs 22.6 / 11.5; profiles/r06q/-r06s/).  In the product the selection launch is
+// bound by its other round trips, so the pivot rate barely moves (profiles/r06t/, alternating):
+// c3r2 +1.5% (both pairs), C3 equal (pass-bound), c3r4 equal, c3r8 -1.5% (both pairs).  Auto: the
+// grouped ring on 256-lane workgroups, the LEAN ring on 128-lane ones.
+static int ratio_ring_rows(const Geometry& g) {
+    return g.rthreads >= 256 ? 64 : 0;
+}
+
 int ratio_defer_blocks(const Geometry& g) {
     return (int)((g.rows + 1 + g.rthreads - 1) / g.rthreads);
 }
@@ -2426,7 +2496,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               Cand* cand_out, int nranks, double tol_dj, double tol_piv,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
                               const Defer* prev, int prev_seal, const XPeers* xp, uint32_t xseq,
-                              const BandPub* bp, bool xfuse) {
+                              const BandPub* bp, bool xfuse, bool own_cus) {
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
     xfuse = xfuse && xp && nranks > 1;
@@ -2460,6 +2530,28 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                 d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp,
                 prev_seal, xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1,
                 pub ? bp->ntiles : 0, pub ? bp->Tn : nullptr, xfuse ? 1 : 0, g.cd);
+            return hipGetLastError();
+        }
+        // the chain on CUs of its own: the grouped ring, ROWS rows per wave (DLP_RATIO_ROWS = 64 / 32 / 16
+        // overrides the policy, 0 keeps the LEAN ring)
+        static const int rows_env = std::getenv("DLP_RATIO_ROWS") ? std::atoi(std::getenv("DLP_RATIO_ROWS")) : -1;
+        const int rrows = rows_env >= 0 ? rows_env : (own_cus ? ratio_ring_rows(g) : 0);
+        if (rrows == 64 || rrows == 32 || rrows == 16) {
+            const int lanes = g.rthreads * 64 / rrows;
+            if (lanes > 1024) return hipErrorInvalidValue;
+#define DLP_RATIO_RING(R_, RP_, RG_)                                                                         \
+    ratio_ring_kernel<R_, RP_, RG_><<<nblocks, lanes, (size_t)(lanes / 64) * RP_ * 1024, s>>>(                 \
+        g.T, g.ld, g.rows, g.rows_elig, g.ncols, g.row_first, basis, pp, ntiles, st, d.C, d.ldc, d.Cc, d.ldcc, \
+        d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
+        xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,   \
+        pub ? bp->Tn : nullptr, xfuse ? 1 : 0, g.cd)
+            if (rrows == 64)
+                DLP_RATIO_RING(64, 16, 4);
+            else if (rrows == 32)
+                DLP_RATIO_RING(32, 16, 4);
+            else
+                DLP_RATIO_RING(16, 16, 2);
+#undef DLP_RATIO_RING
             return hipGetLastError();
         }
         static const int ring_env = std::getenv("DLP_CHAIN_RING") ? std::atoi(std::getenv("DLP_CHAIN_RING")) : 0;
@@ -2728,9 +2820,12 @@ static hipError_t pass(const Geometry& g, const Defer& d, DevState* st, int rb, 
         if constexpr (K == 64) {
             // ring depth D: 4 groups in flight (DLP_Q_DEPTH = 2 or 3: tuning only)
             static const int qd = std::getenv("DLP_Q_DEPTH") ? std::atoi(std::getenv("DLP_Q_DEPTH")) : 4;
-            // (tuning: DLP_Q_U=4, 4 rows per group — twice the independent fma chains per wave — with
-            // 2 or 3 groups in flight)
-            static const int qu = std::getenv("DLP_Q_U") ? std::atoi(std::getenv("DLP_Q_U")) : 2;
+            // rows per group: 4 (twice the independent fma chains per wave, 2 or 3 groups in flight)
+            // from 16,384 rows, else 2 (alternating pairs, profiles/r06w/: C3 pass 4.455-4.458 vs
+            // 4.519-4.523 ms, 13,951-13,956 vs 13,753-13,755 pivots/s; c3r2 equal; c3r4's pass 2%
+            // slower with U = 4); DLP_Q_U = 2 / 4 overrides
+            static const int qu_env = std::getenv("DLP_Q_U") ? std::atoi(std::getenv("DLP_Q_U")) : 0;
+            const int qu = qu_env == 2 || qu_env == 4 ? qu_env : (g.rows >= 16384 ? 4 : 2);
             constexpr int U = 2;
             const int D = qd == 2 || qd == 3 || qd == 6 || qd == 8 ? qd : 4;
             if (qu == 4) {

@@ -267,7 +267,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
                               int pricing, dlp_pivot* log, int64_t log_cap, hipStream_t s,
                               const Defer* prev = nullptr, int prev_seal = -1,
                               const XPeers* xp = nullptr, uint32_t seq = 0, const BandPub* bp = nullptr,
-                              bool xfuse = false);
+                              bool xfuse = false, bool own_cus = false);
 // xfuse (peer exchange, nranks > 1): the last workgroup also waits for every rank's candidate and
 // selects (no select launch); launch_prow_defer's xfuse: the pivot-row launch also commits the
 // exchanged row (no commit launch).  Only where each rank's launches run on hardware queues of

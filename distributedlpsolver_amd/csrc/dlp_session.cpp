@@ -1317,7 +1317,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         HIP_TRY(dlp::launch_ratio_defer(gsel, *dcur, s->basis, s->pp, s->st, s->partials,
                                         s->ratio_blocks_max, s->cand_send, s->exchange ? 2 : 1, o.tol_dj,
                                         o.tol_piv, o.pricing, s->log, s->log_cap, s->stream, dprev,
-                                        pseal, xp, s->xseq_c, &bp, xf));
+                                        pseal, xp, s->xseq_c, &bp, xf, s->chain_cus > 0));
         if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
         if (s->xmode == dlp_session::X_RCCL)
             NCCL_TRY(ncclAllGather(s->cand_send, s->cand_recv, sizeof(dlp::Cand), ncclUint8, s->comm,

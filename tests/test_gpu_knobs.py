@@ -55,7 +55,8 @@ print(json.dumps(out))
 def _run(kind, args=(), env=None):
     e = dict(os.environ)
     for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB", "DLP_CHAIN_CUS",
-              "DLP_FAT_PROW", "DLP_TEST_MASK_FAIL", "DLP_CONDENSED"):
+              "DLP_FAT_PROW", "DLP_TEST_MASK_FAIL", "DLP_CONDENSED", "DLP_Q_U", "DLP_RATIO_ROWS", "DLP_CHAIN_RING",
+              "DLP_RATIO_THREADS", "DLP_PASS_LDS"):
         e.pop(k, None)
     e.update(env or {})
     p = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, kind, *map(str, args)], env=e,
@@ -127,6 +128,26 @@ def test_form23_ring_depth(depth):
     ref = _ref("defer", 0)
     assert not ref["lookahead"] and ref["form"] == 23 and ref["chain_cus"] == 0
     assert _run("defer", [0], {"DLP_Q_DEPTH": depth}) == ref
+
+
+@pytest.mark.parametrize("env", [{"DLP_Q_U": "2"}, {"DLP_Q_U": "4"}, {"DLP_Q_U": "4", "DLP_Q_DEPTH": "3"}])
+def test_form23_rows_per_group(env):
+    """The LDS-ring pass with 2 or 4 rows per group (2 / 3 groups in flight): the same bits, alone (no
+    lookahead) and on the lookahead's CU split at 8,192 rows."""
+    assert _run("defer", [0], env) == _ref("defer", 0)
+    ref = _ref("defer", 1, "p4")
+    assert ref["form"] == 23 and ref["chain_cus"] == 128
+    assert _run("defer", [1, "p4"], env) == ref
+
+
+@pytest.mark.parametrize("rows", ["0", "16", "32", "64"])
+def test_ratio_ring_rows(rows):
+    """The selection kernel of a chain on CUs of its own: the LEAN ring (0) or the grouped ring with 16 /
+    32 / 64 rows per wave (ratio_ring_kernel, 512 / 256 / 128 lanes per 128-row workgroup): the same
+    bits (4,096 rows: the chain on 128 CUs)."""
+    ref = _ref("defer", 1)
+    assert ref["chain_cus"] == 128
+    assert _run("defer", [1], {"DLP_RATIO_ROWS": rows}) == ref
 
 
 @pytest.mark.parametrize("env", [{"DLP_PASS_LDS": "57344"}, {"DLP_PASS_LDS": "57344", "DLP_Q_DEPTH": "6"}])

@@ -447,6 +447,122 @@ __global__ __launch_bounds__(256) void p_ring1(const double* P, int64_t ld, cons
     }
 }
 
+
+// generic: ROWS rows per wave (64 / 32 / 16), 128 / ROWS steps per 1-KB DMA (lane x: step
+// x / (ROWS / 2), rows 2 (x % (ROWS / 2)), +1), RP DMAs in flight, G DMAs per wait; lane r < ROWS
+// replays row i0 + r
+template <int ROWS, int RP, int G>
+__global__ __launch_bounds__(1024) void r_gen(const double* Cc, int64_t ldcc, const double* a0, const double* pqg,
+                                            const int* plg, int J, int64_t rows, double* out) {
+    constexpr int SPD = 128 / ROWS, HL = ROWS / 2;
+    __shared__ double s_pq[kMaxJ + SPD * G];
+    __shared__ int s_pl[kMaxJ + SPD * G];
+    extern __shared__ double s_dyn[];
+    for (int l = threadIdx.x; l < kMaxJ + SPD * G; l += blockDim.x) {
+        s_pq[l] = l < J ? pqg[l] : 0.0;
+        s_pl[l] = l < J ? plg[l] : -1;
+    }
+    const int wl = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t i0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * ROWS;
+    const int r = wl % ROWS;
+    const int64_t i = i0 + r;
+    auto ring_at = [&](int p) { return s_dyn + (wv * RP + p % RP) * 128; };
+    auto csrc = [&](int p) -> const double* {
+        int l = SPD * p + wl / HL;
+        l = l < J ? l : J - 1;
+        return Cc + (int64_t)l * ldcc + i0 + 2 * (wl % HL);
+    };
+    const bool wave_rows = i0 < rows;
+    if (wave_rows)
+#pragma unroll
+        for (int p = 0; p < RP; ++p) glds16(csrc(p), lds_addr(ring_at(p)));
+    double a = i < rows ? a0[i] : 0.0;
+    __syncthreads();
+    if (wave_rows) {
+        const int nd = (J + SPD - 1) / SPD;
+        for (int p0 = 0; p0 < nd; p0 += G) {
+            vmwait<RP - G>();
+            double f[SPD * G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const double* rs = ring_at(p0 + g);
+#pragma unroll
+                for (int k = 0; k < SPD; ++k) f[g * SPD + k] = rs[k * ROWS + r];
+            }
+#pragma unroll
+            for (int u = 0; u < SPD * G; ++u) {
+                const int l = SPD * p0 + u;
+                const double pq = s_pq[l];
+                const bool piv = i == s_pl[l];
+                const double uu = __builtin_fma(-f[u], pq, a);
+                a = l < J ? (piv ? pq : (f[u] != 0.0 ? uu : a)) : a;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) glds16(csrc(p0 + g + RP), lds_addr(ring_at(p0 + g)));
+        }
+        vmwait<0>();
+    }
+    if (wl < ROWS && i < rows) out[i] = a;
+}
+
+// generic, 1 column per lane: COLS columns per wave (64 / 32), 128 / COLS rows per DMA, RD DMAs in
+// flight, G DMAs per wait
+template <int COLS, int RD, int G>
+__global__ __launch_bounds__(1024) void p_gen1(const double* P, int64_t ld, const double* t0g, const double* cpg,
+                                             const int* pivg, int S, int64_t ncols, double* out) {
+    constexpr int RPD = 128 / COLS, HL = COLS / 2;
+    __shared__ double s_cp[kMaxJ + RPD * G];
+    __shared__ int s_pv[kMaxJ + RPD * G];
+    extern __shared__ double s_dyn[];
+    for (int l = threadIdx.x; l < kMaxJ + RPD * G; l += blockDim.x) {
+        s_cp[l] = l < S ? cpg[l] : 0.0;
+        s_pv[l] = l < S ? pivg[l] : 0;
+    }
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wl = threadIdx.x & 63;
+    const int64_t c0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * COLS;
+    const int cl = wl % COLS;
+    const int64_t c = c0 + cl;
+    const bool wave = c0 < ld;
+    auto slot = [&](int p) { return s_dyn + (wv * RD + p % RD) * 128; };
+    auto psrc = [&](int p) -> const double* {
+        int l = RPD * p + wl / HL;
+        l = l < S ? l : S - 1;
+        return P + (int64_t)l * ld + c0 + 2 * (wl % HL);
+    };
+    if (wave)
+#pragma unroll
+        for (int p = 0; p < RD; ++p) glds16(psrc(p), lds_addr(slot(p)));
+    double t = c < ld ? t0g[c] : 0.0;
+    __syncthreads();
+    if (wave) {
+        asm volatile("" ::"v"(t));
+        const int nd = (S + RPD - 1) / RPD;
+        for (int p0 = 0; p0 < nd; p0 += G) {
+            vmwait<RD - G>();
+            double pv[RPD * G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const double* rs = slot(p0 + g);
+#pragma unroll
+                for (int k = 0; k < RPD; ++k) pv[g * RPD + k] = rs[k * COLS + cl];
+            }
+#pragma unroll
+            for (int u = 0; u < RPD * G; ++u) {
+                const int l = RPD * p0 + u;
+                const double cp = s_cp[l];
+                const bool piv = s_pv[l] != 0;
+                const double uu = __builtin_fma(-cp, pv[u], t);
+                t = l < S ? (piv ? pv[u] : (cp != 0.0 ? uu : t)) : t;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) glds16(psrc(p0 + g + RD), lds_addr(slot(p0 + g)));
+        }
+        vmwait<0>();
+        if (wl < COLS && c < ncols) out[c] = t;
+    }
+}
+
 __global__ void empty_kernel(double* out) {
     if (threadIdx.x == 1024) out[0] = 1.0;
 }
@@ -516,7 +632,8 @@ int main(int argc, char** argv) {
     CK(hipGetLastError());
 
     // threads per workgroup: ratio 128 (the product at <= 8,192 rows per rank) or 256 above
-    const int rthr = n <= 8192 ? 128 : 256;
+    int rthr = n <= 8192 ? 128 : 256;
+    if (const char* e = std::getenv("LAB_THREADS")) rthr = std::atoi(e);
     auto launch = [&](int c) -> bool {
         const double* ch = (const double*)((const char*)d_chain + (size_t)(c % copies) * chain_bytes);
         if (ratio) {
@@ -529,6 +646,24 @@ int main(int argc, char** argv) {
                 r_ring<16, 2><<<nb, rthr, (rthr / 64) * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
             else if (!std::strcmp(var, "r16"))
                 r_r16<8><<<(unsigned)((n / 16 + rthr / 64 - 1) / (rthr / 64)), rthr, (rthr / 64) * 8 * 1024, s>>>(
+                    ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "g64x16x4"))
+                r_gen<64, 16, 4><<<nb, rthr, (rthr / 64) * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "g64x24x8"))
+                r_gen<64, 24, 8><<<nb, rthr, (rthr / 64) * 24 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "g64x32x8"))
+                r_gen<64, 32, 8><<<nb, rthr, (rthr / 64) * 32 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "g32x16x2"))
+                r_gen<32, 16, 2><<<(unsigned)((n / 32 + rthr / 64 - 1) / (rthr / 64)), rthr, (rthr / 64) * 16 * 1024, s>>>(
+                    ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "g32x16x4"))
+                r_gen<32, 16, 4><<<(unsigned)((n / 32 + rthr / 64 - 1) / (rthr / 64)), rthr, (rthr / 64) * 16 * 1024, s>>>(
+                    ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "g16x8x1"))
+                r_gen<16, 8, 1><<<(unsigned)((n / 16 + rthr / 64 - 1) / (rthr / 64)), rthr, (rthr / 64) * 8 * 1024, s>>>(
+                    ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "g16x16x2"))
+                r_gen<16, 16, 2><<<(unsigned)((n / 16 + rthr / 64 - 1) / (rthr / 64)), rthr, (rthr / 64) * 16 * 1024, s>>>(
                     ch, ld, d_start, d_sv, d_si, J, n, d_out);
             else if (!std::strcmp(var, "reg"))
                 r_reg<16><<<nb, rthr, 0, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
@@ -544,6 +679,20 @@ int main(int argc, char** argv) {
                 p_ringg<16, 4><<<nb2, 256, 4 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
             else if (!std::strcmp(var, "ring8"))
                 p_ringg<8, 1><<<nb2, 256, 4 * 8 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "ringg128"))
+                p_ringg<16, 4><<<(unsigned)((ld / 2 + 127) / 128), 128, 2 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "q64x16x8"))
+                p_gen1<64, 16, 8><<<nb1, 256, 4 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "q64x24x8"))
+                p_gen1<64, 24, 8><<<nb1, 256, 4 * 24 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "q32x16x4"))
+                p_gen1<32, 16, 4><<<(unsigned)((ld / 32 + 3) / 4), 256, 4 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "q32x16x4t128"))
+                p_gen1<32, 16, 4><<<(unsigned)((ld / 32 + 1) / 2), 128, 2 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "q64x16x4t512"))
+                p_gen1<64, 16, 4><<<(unsigned)((ld + 511) / 512), 512, 8 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "q64x12x4t512"))
+                p_gen1<64, 12, 4><<<(unsigned)((ld + 511) / 512), 512, 8 * 12 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
             else if (!std::strcmp(var, "ring1"))
                 p_ring1<16, 4><<<nb1, 256, 4 * 16 * 1024, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
             else
@@ -582,7 +731,7 @@ int main(int argc, char** argv) {
     float ms0 = 0.f;
     CK(hipEventElapsedTime(&ms0, e0, e1));
     std::printf("{\"kernel\": \"%s\", \"variant\": \"%s\", \"n\": %lld, \"steps\": %d, \"cus\": %d, \"copies\": %d, "
-                "\"us_per_launch\": %.2f, \"empty_us\": %.2f, \"mismatches\": %lld}\n",
-                argv[1], var, (long long)n, J, cus, copies, ms * 1e3 / reps, ms0 * 1e3 / reps, (long long)bad);
+                "\"threads\": %d, \"us_per_launch\": %.2f, \"empty_us\": %.2f, \"mismatches\": %lld}\n",
+                argv[1], var, (long long)n, J, cus, copies, rthr, ms * 1e3 / reps, ms0 * 1e3 / reps, (long long)bad);
     return bad ? 1 : 0;
 }
