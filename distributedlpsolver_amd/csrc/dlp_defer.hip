@@ -127,6 +127,15 @@ __device__ int g_chain_stamps_on;
     do {                                                                                      \
         if (g_chain_stamps_on && threadIdx.x == 0) g_chain_stamps[(slot) & 63][k] = wall_clock64(); \
     } while (0)
+// Per-workgroup stamps of one selection per block (slot 40 mod 64; the grouped-ring kernel only):
+// start / q known / T0 in / replay done / block reduce done / ticket taken, the CU (HW_ID), and
+// wave 0's replayed steps (J - L0).
+__device__ uint64_t g_wg_stamps[1024][8];
+#define WG_STAMP(slot, k, v)                                                                   \
+    do {                                                                                       \
+        if (g_chain_stamps_on && threadIdx.x == 0 && ((slot) & 63) == 40 && blockIdx.x < 1024) \
+            g_wg_stamps[blockIdx.x][k] = (v);                                                  \
+    } while (0)
 
 // LEAN (lookahead beside the form-21 pass): no register-resident chain (coefficients in
 // pairs during the replay) and DPP wave minima for the block reductions (round 3: LDS trees),
@@ -173,6 +182,7 @@ __device__ __forceinline__ void ratio_defer_body(
     if (st->status != DLP_RUNNING) return;
     const int64_t slot = st->npivots;
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 0);
+    if constexpr (ROWS != 64 || RG != 1) WG_STAMP(slot, 0, wall_clock64());
 
     // replayed steps: the sealed previous block (lookahead: not yet applied to T, its kp
     // steps first), then this block's j steps; C / Cc / nzc are written at index j
@@ -262,6 +272,7 @@ __device__ __forceinline__ void ratio_defer_body(
     }
 
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 1);
+    if constexpr (GRING) WG_STAMP(slot, 1, wall_clock64());
     // condensed tableau: q's slot, and the step (of the replayed sequence: sealed steps first) at
     // which that slot restarted from the unit vector of its new variable (R < 0: none replayed here)
     // (the LCH = 8 tuning instance has no condensed build: its 32 VGPRs are full; the launcher
@@ -293,6 +304,7 @@ __device__ __forceinline__ void ratio_defer_body(
         s_pq[l] = l < kp ? Pp[(int64_t)l * ld + sq] : P[(int64_t)(l - kp) * ld + sq];
     __syncthreads();
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 2);
+    if constexpr (GRING) WG_STAMP(slot, 2, wall_clock64());
 
     Cand c = cand_empty();
     double flast = 0.0;   // LEAN: C of step J-1 (the RHS cache's step)
@@ -349,6 +361,11 @@ __device__ __forceinline__ void ratio_defer_body(
             if (R >= L0 && i == rows) a = T[i * ld + sq];
         }
         if (blockIdx.x == 0) CHAIN_STAMP(slot, 3);
+        if constexpr (GRING) {
+            WG_STAMP(slot, 3, wall_clock64());
+            WG_STAMP(slot, 6, (uint64_t)__smid());
+            WG_STAMP(slot, 7, (uint64_t)(J - L0));
+        }
     } else if constexpr (LEAN) {
         // LCH coefficient loads per round trip (the register budget of this kernel), from the
         // first step not applied to the row's source (L0: a published band starts after the
@@ -460,6 +477,7 @@ __device__ __forceinline__ void ratio_defer_body(
     }
     c = cand_red(c);
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 4);
+    if constexpr (GRING) WG_STAMP(slot, 4, wall_clock64());
     if (xp && xsel) {
         // peer exchange, selection in this launch: every workgroup's candidate straight into slot
         // [seq & 1][me][blockIdx] of every rank (no partials, no ticket); workgroup 0 of every rank
@@ -504,6 +522,7 @@ __device__ __forceinline__ void ratio_defer_body(
     }
     __syncthreads();
     if constexpr (LEAN) if (blockIdx.x == 0) CHAIN_STAMP(slot, 5);
+    if constexpr (GRING) WG_STAMP(slot, 5, wall_clock64());
     if (!s_last) return;
     Cand best = cand_empty();
     for (int k = threadIdx.x; k < nblocks; k += blockDim.x) {
@@ -3012,6 +3031,9 @@ hipError_t chain_stamps_enable() {
 }
 hipError_t chain_stamps_dump(uint64_t* host64x16) {
     return hipMemcpyFromSymbol(host64x16, HIP_SYMBOL(g_chain_stamps), sizeof(uint64_t) * 64 * 16);
+}
+hipError_t chain_wg_stamps_dump(uint64_t* host1024x8) {
+    return hipMemcpyFromSymbol(host1024x8, HIP_SYMBOL(g_wg_stamps), sizeof(uint64_t) * 1024 * 8);
 }
 
 hipError_t launch_reset_cols(const Geometry& g, const DevState* st, int seal, hipStream_t s) {

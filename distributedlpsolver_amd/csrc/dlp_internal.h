@@ -318,6 +318,7 @@ bool lookahead_form(int form);
 // Diagnostics (DLP_CHAIN_STAMPS): phase stamps of the LEAN chain kernels (dlp_defer.hip).
 hipError_t chain_stamps_enable();
 hipError_t chain_stamps_dump(uint64_t* host64x16);
+hipError_t chain_wg_stamps_dump(uint64_t* host1024x8);
 // End of a lookahead block: st->seal[slot] := (blk, pl), blk := 0.
 hipError_t launch_seal_defer(DevState* st, int slot, hipStream_t s, const BandPub* bp = nullptr);
 hipError_t launch_prow(const Geometry& g, const DevState* st, int64_t* prow_bits, int nranks,

@@ -514,6 +514,12 @@ void free_session(dlp_session* s) {
                 std::fwrite(h.data(), sizeof(uint64_t), h.size(), f);
                 std::fclose(f);
             }
+        std::vector<uint64_t> w(1024 * 8, 0);   // per-workgroup stamps of the grouped-ring selection
+        if (dlp::chain_wg_stamps_dump(w.data()) == hipSuccess)
+            if (FILE* f = std::fopen((std::string(path) + ".wg").c_str(), "wb")) {
+                std::fwrite(w.data(), sizeof(uint64_t), w.size(), f);
+                std::fclose(f);
+            }
     }
     if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
     clk.mark(s->gexec ? "free: graph exec" : "free: (no graph)");

@@ -60,5 +60,10 @@ t0 = full[0, 0]
 by_slot = {"start_after_first": [round(float(full[k, 0] - t0), 1) if ok[k] else -1 for k in range(64)],
            "ratio": [round(float(full[k, 6] - full[k, 0]), 1) if ok[k] else -1 for k in range(64)],
            "prow": [round(float(full[k, 11] - full[k, 8]), 1) if ok[k] else -1 for k in range(64)]}
-print(json.dumps({"pivots_sampled": int(ok.sum()), "bench_value": line["value"],
+wg = None
+if os.path.exists(path + ".wg"):   # the grouped-ring selection's per-workgroup stamps (tools/wg_stamps.py)
+    wg = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "wg_stamps.py"), path + ".wg"], check=True,
+                        capture_output=True, text=True).stdout
+    wg = json.loads(wg) if wg.strip() and json.loads(wg)["workgroups"] > 0 else None
+print(json.dumps({"pivots_sampled": int(ok.sum()), "bench_value": line["value"], "workgroups": wg,
                   "pass_ms": line["roofline"]["launch_ms"], "median_us": res, "by_slot_us": by_slot}, indent=1))

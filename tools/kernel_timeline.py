@@ -44,6 +44,9 @@ for bi in range(max(0, len(passes) - 1 - nblk), len(passes) - 1):
         "ratio_us": [round((x[1] - x[0]) / 1e3, 1) for x in rat],
         "prow_us": [round((x[1] - x[0]) / 1e3, 1) for x in prw],
         "period_us": [round(v / 1e3, 1) for v in np.diff(starts)],
+        # the chain's own time: its launches summed, and how long after the pass its last launch ended
+        "chain_busy_us": round(sum(x[1] - x[0] for x in chain) / 1e3, 1),
+        "chain_end_after_pass_us": round((max(x[1] for x in chain) - p0e) / 1e3, 1) if chain else None,
         "reset_cols_us": [round((x[1] - x[0]) / 1e3, 1) for x in ev[a - 2:b] if x[2] == "reset_cols"][:2],
         "ratio_name": rat[0][3].replace("(anonymous namespace)::", "").split("(")[0][-60:] if rat else None,
     })
