@@ -754,6 +754,10 @@ def main():
         raise SystemExit(f"timed window ended early: status {st} after {done} pivots")
     lookahead_on = sess.lookahead()
     chain_cus = sess.chain_cus() if hasattr(sess, "chain_cus") else None
+    # CUs the pass runs on (all of the device's unless the lookahead split gave the chain some of them;
+    # co-located rank processes' slices are not subtracted here)
+    dev_cus = torch.cuda.get_device_properties(local).multi_processor_count
+    pass_cus = dev_cus - chain_cus if (lookahead_on and chain_cus) else dev_cus
 
     tm, nsamp = sess.timings()
     launches, upd_total_ms, _ = sess.update_stats()
@@ -913,7 +917,13 @@ def main():
                          "fp64_tflops": (2.0 * K * rows_local * (N1 - 1) / (upd_ms * 1e-3) / 1e12
                                          if upd_ms > 0 else None),
                          "fp64_frac": (2.0 * K * rows_local * (N1 - 1) / (upd_ms * 1e-3) / 1e12 / FP64_PEAK_TFS
-                                       if upd_ms > 0 else None)},
+                                       if upd_ms > 0 else None),
+                         # under lookahead's CU split the pass holds only its own CUs: its fp64 peak is their
+                         # share (8 FLOP per algorithmic byte at K = 64 is above that share's ridge)
+                         "pass_cus": pass_cus,
+                         "fp64_frac_of_pass_cus": (2.0 * K * rows_local * (N1 - 1) / (upd_ms * 1e-3) / 1e12
+                                                   / (FP64_PEAK_TFS * pass_cus / dev_cus)
+                                                   if upd_ms > 0 and pass_cus else None)},
             "rank1_update_roofline": eager,
             "pivot_log_vs_oracle": parity,
             "cpu_baseline": cpu,
