@@ -680,7 +680,9 @@ __device__ inline void commit_row(double* __restrict__ T, int64_t ld, int64_t ro
 // other rank INT64_MIN for the int64 MAX exchange.
 constexpr int kProwRingSteps = 8;   // (RS: 16 measured equal, with the ratio ring's 16)
 constexpr size_t prow_ring_bytes(int rs) { return (size_t)4 * rs * 128 * sizeof(double); }
-template <bool LEAN, int RS = kProwRingSteps, int CHR = 16>
+// PG (the ring only, round 6): pivot rows retired per wait, their LDS reads issued together (PG = 1:
+// one wait and one LDS round trip per row, the 32-VGPR kernel beside the pass)
+template <bool LEAN, int RS = kProwRingSteps, int CHR = 16, int PG = 1>
 __device__ __forceinline__ void prow_defer_body(
     double* __restrict__ T, int64_t ld, int64_t rows, int64_t ncols, int64_t nprice,
     const DevState* st, const double* __restrict__ C, int64_t ldc, double* __restrict__ P,
@@ -691,8 +693,8 @@ __device__ __forceinline__ void prow_defer_body(
     __shared__ PricePart lds_pp[4];
     __shared__ SelView s_sel;
     __shared__ int s_selok;
-    __shared__ double s_cp[kMaxReplay];
-    __shared__ int32_t s_pl[kMaxReplay];
+    __shared__ double s_cp[kMaxReplay + (PG > 1 ? PG : 0)];   // (a group past S - 1 reads spares, dropped)
+    __shared__ int32_t s_pl[kMaxReplay + (PG > 1 ? PG : 0)];
     // LEAN: the replayed pivot rows stream through a per-wave LDS ring by LDS-DMA, RING steps
     // in flight (each lane's own 16 B of a row land at ring + 16 lane), instead of 4 rows per
     // round trip in the 32 VGPRs this kernel has beside the pass
@@ -817,17 +819,42 @@ __device__ __forceinline__ void prow_defer_body(
     if (owner_lane && LEAN) {
         d2 t = t0;
         asm volatile("" ::"v"(t.x), "v"(t.y));   // T0[p] in here (hipcc's own wait), not in the loop
-        for (int l = L0; l < S; ++l) {
-            vmwait<RING - 1>();   // step l's DMA retired: only ring DMAs issue in this loop
-            const d2 pv = *(const d2*)&s_ring[wv][l % RING][2 * wl];
-            const double cp = s_cp[l];
-            const bool piv = pl == s_pl[l];
-            if (l == Rx) t.x = 0.0;
-            if (l == Ry) t.y = 0.0;
-            const double ux = __builtin_fma(-cp, pv.x, t.x), uy = __builtin_fma(-cp, pv.y, t.y);
-            t.x = piv ? pv.x : (cp != 0.0 ? ux : t.x);   // (branch-free, as the ratio ring's step)
-            t.y = piv ? pv.y : (cp != 0.0 ? uy : t.y);
-            glds16(psrc(l + RING), lds_addr(&s_ring[wv][l % RING][0]));
+        if constexpr (PG == 1) {
+            for (int l = L0; l < S; ++l) {
+                vmwait<RING - 1>();   // step l's DMA retired: only ring DMAs issue in this loop
+                const d2 pv = *(const d2*)&s_ring[wv][l % RING][2 * wl];
+                const double cp = s_cp[l];
+                const bool piv = pl == s_pl[l];
+                if (l == Rx) t.x = 0.0;
+                if (l == Ry) t.y = 0.0;
+                const double ux = __builtin_fma(-cp, pv.x, t.x), uy = __builtin_fma(-cp, pv.y, t.y);
+                t.x = piv ? pv.x : (cp != 0.0 ? ux : t.x);   // (branch-free, as the ratio ring's step)
+                t.y = piv ? pv.y : (cp != 0.0 ? uy : t.y);
+                glds16(psrc(l + RING), lds_addr(&s_ring[wv][l % RING][0]));
+            }
+        } else {
+            // PG rows per wait: their LDS reads together, then the PG steps, then PG refills (a group
+            // past S - 1 reads clamped rows and drops them: every group issues PG DMAs)
+            for (int l0 = L0; l0 < S; l0 += PG) {
+                vmwait<RING - PG>();
+                d2 pv[PG];
+#pragma unroll
+                for (int g = 0; g < PG; ++g) pv[g] = *(const d2*)&s_ring[wv][(l0 + g) % RING][2 * wl];
+#pragma unroll
+                for (int g = 0; g < PG; ++g) {
+                    const int l = l0 + g;
+                    const double cp = s_cp[l];
+                    const bool piv = pl == s_pl[l];
+                    const bool ok = l < S;
+                    if (l == Rx) t.x = 0.0;
+                    if (l == Ry) t.y = 0.0;
+                    const double ux = __builtin_fma(-cp, pv[g].x, t.x), uy = __builtin_fma(-cp, pv[g].y, t.y);
+                    t.x = ok ? (piv ? pv[g].x : (cp != 0.0 ? ux : t.x)) : t.x;
+                    t.y = ok ? (piv ? pv[g].y : (cp != 0.0 ? uy : t.y)) : t.y;
+                }
+#pragma unroll
+                for (int g = 0; g < PG; ++g) glds16(psrc(l0 + g + RING), lds_addr(&s_ring[wv][(l0 + g) % RING][0]));
+            }
         }
         vmwait<0>();   // the ring drained (the clamped tail DMAs) before the block exits
         if (cd.on) cond_fix(t);
@@ -947,6 +974,12 @@ __global__ __launch_bounds__(256) void prow_defer_kernel(DLP_PROW_ARGS) {
 template <int RS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void prow_lean_kernel(DLP_PROW_ARGS) {
     prow_defer_body<true, RS>(DLP_PROW_PASS);
+}
+// The grouped ring (round 6): the pivot-row kernel of a chain on CUs of its own, RS rows in flight,
+// PG retired per wait (no 32-VGPR budget: no pass waves beside it)
+template <int RS, int PG>
+__global__ __launch_bounds__(256) void prow_ring_kernel(DLP_PROW_ARGS) {
+    prow_defer_body<true, RS, 16, PG>(DLP_PROW_PASS);
 }
 // MID (round 5): beside the MFMA pass (form 22: 3 waves x 136 VGPRs per SIMD leave 104), the
 // register replay of the fat kernel with 2 x 8 pivot rows in flight instead of 2 x 16, and no
@@ -2647,6 +2680,16 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     const bool pub = bp && bp->cnt && bp->Tn && prev_seal >= 0;
     static const int fat_env = std::getenv("DLP_FAT_PROW") ? std::atoi(std::getenv("DLP_FAT_PROW")) : -1;
+    // the chain on CUs of its own: the grouped ring (DLP_PROW_GROUP = 4) or the register kernel
+    static const int pg_env = std::getenv("DLP_PROW_GROUP") ? std::atoi(std::getenv("DLP_PROW_GROUP")) : 0;
+    if (prev_seal >= 0 && d.K > 32 && own_cus && fat_env < 0 && pg_env == 4) {
+        prow_ring_kernel<16, 4><<<blocks, 256, prow_ring_bytes(16), s>>>(
+            g.T, g.ld, g.rows, g.ncols, g.nprice, st, d.C, d.ldc, d.P, prow_bits, pp, tol_dj, log, log_cap,
+            nranks == 1 ? 1 : 0, prev->C, prev->P, prev_seal, nranks == 1 ? nullptr : xp, xseq,
+            pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,
+            pub ? bp->Tn : nullptr, xc, g.cd);
+        return hipGetLastError();
+    }
     const bool fat = fat_env >= 0 ? fat_env == 1 : own_cus;
     static const int mid_env = std::getenv("DLP_MID_CHAIN") ? std::atoi(std::getenv("DLP_MID_CHAIN")) : -1;
     const bool mid = !fat && (mid_env >= 0 ? mid_env == 1 : d.form == 22);

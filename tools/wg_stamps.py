@@ -11,6 +11,9 @@ import numpy as np
 w = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(1024, 8)
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else int((w[:, 0] > 0).sum())
 w = w[:nb]
+if nb == 0 or not (w[:, 0] > 0).all():   # no grouped-ring selection stamped this run
+    print(json.dumps({"workgroups": 0}))
+    sys.exit(0)
 t = w[:, :6].astype(np.float64)
 t0 = t[:, 0].min()
 rel = (t - t0) / 100.0
