@@ -2597,7 +2597,12 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
         d.P, d.rhs, d.nzc, partials, cand_out, nranks, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, prev_seal, \
         xp, xseq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,   \
         pub ? bp->Tn : nullptr, xfuse ? 1 : 0, g.cd)
-            if (rrows == 64)
+            // (DLP_RATIO_RP=12: 12 DMAs in flight, 48 KB of ring per 256-lane workgroup, so three share a
+            // CU and C3's 129 workgroups are resident at once on 64 CUs; tuning)
+            static const int rp_env = std::getenv("DLP_RATIO_RP") ? std::atoi(std::getenv("DLP_RATIO_RP")) : 16;
+            if (rrows == 64 && rp_env == 12)
+                DLP_RATIO_RING(64, 12, 4);
+            else if (rrows == 64)
                 DLP_RATIO_RING(64, 16, 4);
             else if (rrows == 32)
                 DLP_RATIO_RING(32, 16, 4);

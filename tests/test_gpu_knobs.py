@@ -56,7 +56,7 @@ def _run(kind, args=(), env=None):
     e = dict(os.environ)
     for k in ("DLP_LEAN_LCH", "DLP_Q_DEPTH", "DLP_BATCH_LDS", "DLP_CLUSTER_WG", "DLP_BAND_PUB", "DLP_CHAIN_CUS",
               "DLP_FAT_PROW", "DLP_TEST_MASK_FAIL", "DLP_CONDENSED", "DLP_Q_U", "DLP_RATIO_ROWS", "DLP_CHAIN_RING",
-              "DLP_RATIO_THREADS", "DLP_PASS_LDS", "DLP_PROW_GROUP"):
+              "DLP_RATIO_THREADS", "DLP_PASS_LDS", "DLP_PROW_GROUP", "DLP_RATIO_RP"):
         e.pop(k, None)
     e.update(env or {})
     p = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, kind, *map(str, args)], env=e,
@@ -75,7 +75,8 @@ def _ref(kind, *args):
                                  {"DLP_FAT_PROW": "0"}, {"DLP_RATIO_THREADS": "64"},
                                  {"DLP_RATIO_THREADS": "128"}, {"DLP_RATIO_THREADS": "256"},
                                  {"DLP_CHAIN_RING": "16"}, {"DLP_CHAIN_RING": "16", "DLP_FAT_PROW": "0"},
-                                 {"DLP_PROW_GROUP": "4"}, {"DLP_PROW_GROUP": "4", "DLP_RATIO_ROWS": "16"}])
+                                 {"DLP_PROW_GROUP": "4"}, {"DLP_PROW_GROUP": "4", "DLP_RATIO_ROWS": "16"},
+                                 {"DLP_RATIO_ROWS": "64", "DLP_RATIO_RP": "12"}])
 def test_lookahead_chain_knobs(env):
     ref = _ref("defer", 1)
     # 4,096 rows: the chain on 128 CUs, the pass on the other 128 (chain_cus_policy)
