@@ -654,6 +654,13 @@ int chain_cus_policy(const dlp_session* s) {
         // the block from 5.62 to 4.73-4.79 ms (13.4-13.5 k vs 11.4 k pivots/s; 32 CUs 12.7 k, 96
         // 12.6 k; profiles/r06f/)
         n = std::min(s->rows > 8192 ? 64 : 128, cus / 2);
+        // A rank alone on its device, condensed, moved the balance again (alternating pairs,
+        // profiles/r06zh/, r06zi/): up to 8,192 rows 96 chain CUs (c3r8 27.99-28.36 k vs 27.58-27.64 k
+        // pivots/s with 128; c3r4 24.30-24.55 k vs 23.90-24.05 k; 64 equal to 96), 16,384 rows 128
+        // (c3r2 19.10-19.46 k vs 18.71-18.74 k with 64; 160 loses), C3 64.  Ranks sharing a device keep
+        // the budget above for their slices.
+        if (s->g.cd.on && s->coloc_n <= 1)
+            n = std::min(s->rows <= 8192 ? 96 : (s->rows < 32768 ? 128 : 64), cus / 2);
     }
     const int nco = std::max(1, s->coloc_n);
     if (n <= 0 || nco == 1) return n;

@@ -79,8 +79,8 @@ def _ref(kind, *args):
                                  {"DLP_RATIO_ROWS": "64", "DLP_RATIO_RP": "12"}])
 def test_lookahead_chain_knobs(env):
     ref = _ref("defer", 1)
-    # 4,096 rows: the chain on 128 CUs, the pass on the other 128 (chain_cus_policy)
-    assert ref["lookahead"] and ref["form"] == 21 and ref["done"] == 136 and ref["chain_cus"] == 128
+    # 4,096 rows, condensed, alone on the device: the chain on 96 CUs, the pass on the other 160 (chain_cus_policy)
+    assert ref["lookahead"] and ref["form"] == 21 and ref["done"] == 136 and ref["chain_cus"] == 96
     got = _run("defer", [1], env)
     if "DLP_CHAIN_CUS" in env:
         assert got.pop("chain_cus") == int(env["DLP_CHAIN_CUS"])
@@ -97,14 +97,16 @@ def test_full_tableau_knob(la):
     assert ref["condensed"]
     got = _run("defer", [la], {"DLP_CONDENSED": "0"})
     assert got.pop("condensed") is False
-    assert got == {k: v for k, v in ref.items() if k != "condensed"}
+    # (the chain's CU budget follows the layout: 96 condensed, 128 full at 4,096 rows; the bits do not)
+    got.pop("chain_cus")
+    assert got == {k: v for k, v in ref.items() if k not in ("condensed", "chain_cus")}
 
 
 def test_cu_split_with_the_form23_pass():
-    """8,192 rows (one rank of C3 at P = 4): the chain on 128 CUs and the LDS-ring pass (form 23)
+    """8,192 rows (one rank of C3 at P = 4): the chain on 96 CUs and the LDS-ring pass (form 23)
     on the rest, against both streams unmasked with the form-21 pass: the same bits."""
     ref = _run("defer", [1, "p4"])
-    assert ref["lookahead"] and ref["form"] == 23 and ref["chain_cus"] == 128
+    assert ref["lookahead"] and ref["form"] == 23 and ref["chain_cus"] == 96
     got = _run("defer", [1, "p4"], {"DLP_CHAIN_CUS": "0"})
     assert got.pop("form") == 21 and got.pop("chain_cus") == 0
     assert got == {k: v for k, v in ref.items() if k not in ("form", "chain_cus")}
@@ -138,7 +140,7 @@ def test_form23_rows_per_group(env):
     lookahead) and on the lookahead's CU split at 8,192 rows."""
     assert _run("defer", [0], env) == _ref("defer", 0)
     ref = _ref("defer", 1, "p4")
-    assert ref["form"] == 23 and ref["chain_cus"] == 128
+    assert ref["form"] == 23 and ref["chain_cus"] == 96
     assert _run("defer", [1, "p4"], env) == ref
 
 
@@ -146,9 +148,9 @@ def test_form23_rows_per_group(env):
 def test_ratio_ring_rows(rows):
     """The selection kernel of a chain on CUs of its own: the LEAN ring (0) or the grouped ring with 16 /
     32 / 64 rows per wave (ratio_ring_kernel, 512 / 256 / 128 lanes per 128-row workgroup): the same
-    bits (4,096 rows: the chain on 128 CUs)."""
+    bits (4,096 rows: the chain on 96 CUs)."""
     ref = _ref("defer", 1)
-    assert ref["chain_cus"] == 128
+    assert ref["chain_cus"] == 96
     assert _run("defer", [1], {"DLP_RATIO_ROWS": rows}) == ref
 
 

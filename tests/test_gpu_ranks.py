@@ -212,14 +212,14 @@ def _split_sha(s, width, cut, chunk=512):
 def test_rccl_rank_session_lookahead_on_cu_split():
     """an RCCL-exchange rank session keeps lookahead when the chain has CUs of its
     own (the collectives never share a CU with the pass): the rank_split LP as one 1-rank RCCL
-    session (8,192 rows: 128 chain CUs, form 23 on the rest), 136 + 64 pivots against the
+    session (8,192 rows: 96 chain CUs, form 23 on the rest), 136 + 64 pivots against the
     oracle's stops (both row blocks, objective row, log, basis)."""
     g = load_golden("digests.json")["rank_split"]
     with dlp.Session(dlp.Problem.random(g["m"], g["n"], g["seed"]), rank=0, nranks=1,
                      rccl_id=dlp.comm_unique_id(), exchange=L.XCHG_RCCL, defer=0, check_interval=64 * 20,
                      max_pivots=300) as s:
         assert s.get_exchange() == L.XCHG_RCCL
-        assert s.lookahead() and s.chain_cus() == 128 and s.get_defer_tuning()[1:] == (23, 64)
+        assert s.lookahead() and s.chain_cus() == 96 and s.get_defer_tuning()[1:] == (23, 64)
         total = 0
         for w in (136, 64):
             st, done = s.run(w)
