@@ -673,6 +673,10 @@ int main(int argc, char** argv) {
             const unsigned nb2 = (unsigned)((ld / 2 + 255) / 256), nb1 = (unsigned)((ld + 255) / 256);
             if (!std::strcmp(var, "fat"))
                 p_fat<16><<<nb2, 256, 0, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "fat24"))
+                p_fat<24><<<nb2, 256, 0, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
+            else if (!std::strcmp(var, "fat32"))
+                p_fat<32><<<nb2, 256, 0, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
             else if (!std::strcmp(var, "fat1"))
                 p_fat1<32><<<nb1, 256, 0, s>>>(ch, ld, d_start, d_sv, d_si, J, n, d_out);
             else if (!std::strcmp(var, "ringg"))
