@@ -721,6 +721,7 @@ __device__ __forceinline__ void prow_defer_body(
         sv.piv = st->piv;
         sv.zq = 0.0;
         sv.npivots = st->npivots;
+        sv.sq = -1;
     }
     const int64_t slot = sv.npivots - 1;
     if constexpr (LEAN) if (tile == 0) CHAIN_STAMP(slot, 8);
@@ -767,7 +768,7 @@ __device__ __forceinline__ void prow_defer_body(
     // leaving variable's unit 1)
     int32_t Rx = -1, Ry = -1, sq = -1;
     if (cd.on) {
-        sq = st->sq;
+        sq = onelaunch ? sv.sq : st->sq;   // (one launch: the record's, published with the selection)
         if (owner_lane) {
             const int bs = st->bser, ss = kp > 0 ? st->seal[prev_seal].ser : -2;
             // (a sealed-block restart matters only where row p is replayed through the sealed
@@ -1007,23 +1008,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(104))) void pro
         int bnt, const double *Tn, int xs, Cond cd
 // (xs = 2, passed at launch: as a compile-time constant hipcc gave the LEAN instance 34 VGPRs, at
 // run time 30 of the 32 the form-21 pass leaves per SIMD)
-#define DLP_PX_BODIES(KM, LEAN_, LCH_, RP_, RS_)                                                                 \
+#define DLP_PX_BODIES(KM, LEAN_, LCH_, RP_, RS_, CD_)                                                               \
     if ((int)blockIdx.x < nrat) {                                                                                \
         ratio_defer_body<KM, false, LEAN_, LCH_, RP_>(T, ld, rows, rows_elig, ncols, row_first, basis, pp,       \
                                                      ntiles, st, C, ldc, Cc, ldcc, P, rhs, nzc, nullptr,          \
                                                      nullptr, 2, tol_dj, tol_piv, pricing, log, log_cap, nrat,    \
-                                                     Ccp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xs, xseq, Cond{}); \
+                                                     Ccp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn, xs, xseq, CD_); \
         return;                                                                                                  \
     }                                                                                                            \
     prow_defer_body<LEAN_, RS_>(T, ld, rows, ncols, nprice, st, C, ldc, P, nullptr, pp,      \
                                 tol_dj, log, log_cap, 0, Cp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn, 1,     \
-                                (int)blockIdx.x - nrat, 1, Cond{})
+                                (int)blockIdx.x - nrat, 1, CD_)
 template <int KMAX>
 __global__ __launch_bounds__(256) void pivot_x_kernel(DLP_PX_RATIO_ARGS) {
-    DLP_PX_BODIES(KMAX, false, 4, kRatioRingPairs, kProwRingSteps);
+    DLP_PX_BODIES(KMAX, false, 4, kRatioRingPairs, kProwRingSteps, cd);
 }
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32))) void pivot_x_lean_kernel(DLP_PX_RATIO_ARGS) {
-    DLP_PX_BODIES(128, true, 0, kRatioRingPairs, kProwRingSteps);
+    // (no condensed build: its 32 VGPRs are full; launch_pivot_x refuses a condensed session here)
+    DLP_PX_BODIES(128, true, 0, kRatioRingPairs, kProwRingSteps, Cond{});
+}
+// The chain on CUs of its own (round 6): the grouped-ring selection with ROWS rows per wave (256 lanes
+// cover the session's rthreads = 4 ROWS rows, so the exchange's candidate slots are unchanged) and the
+// register pivot-row kernel, no VGPR budget; every workgroup resident (the caller's chain CUs hold two
+// each at the ring's 64 KB)
+template <int ROWS>
+__global__ __launch_bounds__(256) void pivot_x_ring_kernel(DLP_PX_RATIO_ARGS) {
+    if ((int)blockIdx.x < nrat) {
+        ratio_defer_body<128, false, true, 0, 16, false, ROWS, 4>(
+            T, ld, rows, rows_elig, ncols, row_first, basis, pp, ntiles, st, C, ldc, Cc, ldcc, P, rhs, nzc, nullptr,
+            nullptr, 2, tol_dj, tol_piv, pricing, log, log_cap, nrat, Ccp, Pp, prev_seal, xp, xseq, bcnt, brb, bnt, Tn,
+            xs, xseq, cd);
+        return;
+    }
+    prow_defer_body<false>(T, ld, rows, ncols, nprice, st, C, ldc, P, nullptr, pp, tol_dj, log, log_cap, 0, Cp, Pp,
+                           prev_seal, xp, xseq, bcnt, brb, bnt, Tn, 1, (int)blockIdx.x - nrat, 1, cd);
 }
 #undef DLP_PX_BODIES
 
@@ -2738,9 +2756,11 @@ hipError_t launch_prow_defer(const Geometry& g, const Defer& d, const DevState* 
 hipError_t launch_pivot_x(const Geometry& g, const Defer& d, int32_t* basis, PricePart* pp, DevState* st,
                           double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
                           hipStream_t s, const Defer* prev, int prev_seal, const XPeers* xp, uint32_t seq,
-                          const BandPub* bp) {
-    // 256-lane ratio blocks; no condensed-tableau instance (its selection record has no slot field)
-    if (!xp || g.rthreads != kRatioDeferThreads || g.cd.on) return hipErrorInvalidValue;
+                          const BandPub* bp, bool own_cus) {
+    // 256-lane ratio blocks (the ring instance: 128 or 256 rows each, on the chain's own CUs); the
+    // selection record carries the condensed tableau's entering slot
+    const bool ring = own_cus && d.K == 64 && (g.rthreads == 128 || g.rthreads == kRatioDeferThreads);
+    if (!xp || (!ring && g.rthreads != kRatioDeferThreads)) return hipErrorInvalidValue;
     if (prev_seal >= 0 && (!prev || prev_seal > 1 || 2 * d.K > kMaxReplay)) return hipErrorInvalidValue;
     const int ntiles = (int)((g.width + kDeferTile - 1) / kDeferTile);
     const int nrat = ratio_defer_blocks(g);
@@ -2755,7 +2775,13 @@ hipError_t launch_pivot_x(const Geometry& g, const Defer& d, int32_t* basis, Pri
         d.ldcc, d.P, d.rhs, d.nzc, nrat, tol_dj, tol_piv, pricing, log, log_cap, Ccp, Pp, Cp, prev_seal, xp, \
         seq, pub ? bp->cnt + prev_seal * bp->stride : nullptr, pub ? bp->rb : 1, pub ? bp->ntiles : 0,     \
         pub ? bp->Tn : nullptr, 2, g.cd
-    if (steps > 64)   // lookahead at K = 64, beside the form-21 pass
+    if (!ring && steps > 64 && g.cd.on) return hipErrorInvalidValue;   // (the LEAN instance has no condensed build)
+    if (ring) {
+        if (g.rthreads == 128)
+            pivot_x_ring_kernel<32><<<nrat + nprow, 256, (size_t)4 * 16 * 1024, s>>>(DLP_PX_ARGS);
+        else
+            pivot_x_ring_kernel<64><<<nrat + nprow, 256, (size_t)4 * 16 * 1024, s>>>(DLP_PX_ARGS);
+    } else if (steps > 64)   // lookahead at K = 64, beside the form-21 pass
         pivot_x_lean_kernel<<<nrat + nprow, 256, std::max(ratio_ring_bytes(kRatioRingPairs),
                                                           prow_ring_bytes(kProwRingSteps)), s>>>(DLP_PX_ARGS);
     else if (steps <= 16)

@@ -349,11 +349,12 @@ __device__ inline void sel_publish(DevState* st, uint32_t seq, int32_t status, d
     sel_store64(&r->piv, __builtin_bit_cast(uint64_t, st->piv));
     sel_store64(&r->zq, __builtin_bit_cast(uint64_t, zq));
     sel_store64(&r->npivots, (uint64_t)st->npivots);
+    sel_store32(&r->sq, st->sq);
     x_drain();
     __hip_atomic_store(&r->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 struct SelView {
-    int32_t status, p_local, blk;
+    int32_t status, p_local, blk, sq;
     double piv, zq;
     int64_t npivots;
 };
@@ -386,6 +387,7 @@ __device__ inline bool sel_wait(const XPeers* xp, const DevState* st, uint32_t s
             lds->status = __hip_atomic_load(&r->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             lds->p_local = __hip_atomic_load(&r->p_local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             lds->blk = __hip_atomic_load(&r->blk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lds->sq = __hip_atomic_load(&r->sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             lds->piv = __builtin_bit_cast(
                 double, __hip_atomic_load((const uint64_t*)&r->piv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             lds->zq = __builtin_bit_cast(
@@ -404,6 +406,7 @@ __device__ inline bool sel_wait(const XPeers* xp, const DevState* st, uint32_t s
     out->status = u32(lds->status);
     out->p_local = u32(lds->p_local);
     out->blk = u32(lds->blk);
+    out->sq = u32(lds->sq);
     out->piv = __builtin_bit_cast(double, u64(__builtin_bit_cast(uint64_t, lds->piv)));
     out->zq = __builtin_bit_cast(double, u64(__builtin_bit_cast(uint64_t, lds->zq)));
     out->npivots = (int64_t)u64((uint64_t)lds->npivots);

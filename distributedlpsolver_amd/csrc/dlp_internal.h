@@ -84,7 +84,8 @@ struct alignas(128) DevState {
         int32_t status, p_local, blk;
         double piv, zq;
         int64_t npivots;
-        uint32_t pad[22];
+        int32_t sq;   // condensed tableau: the entering slot
+        uint32_t pad[21];
     } sel;
     // condensed tableau (Cond): the entering variable's slot (written with q by the
     // ratio kernel), the open block's serial, and each step's entering slot
@@ -280,7 +281,7 @@ hipError_t launch_ratio_defer(const Geometry& g, const Defer& d, int32_t* basis,
 hipError_t launch_pivot_x(const Geometry& g, const Defer& d, int32_t* basis, PricePart* pp, DevState* st,
                           double tol_dj, double tol_piv, int pricing, dlp_pivot* log, int64_t log_cap,
                           hipStream_t s, const Defer* prev, int prev_seal, const XPeers* xp, uint32_t seq,
-                          const BandPub* bp);
+                          const BandPub* bp, bool own_cus = false);
 // nranks == 1: ratio test + selection + pivot row + objective row + pricing in ONE launch
 // (K <= 32; grid of fused_pivot_blocks(g), all of which must be resident at once).
 int fused_pivot_blocks(const Geometry& g);

@@ -1272,6 +1272,17 @@ bool peer_onelaunch() {
     return e && std::atoi(e) == 1;
 }
 
+// The one-launch peer pivot applies: 256-lane ratio workgroups, or 128-lane ones when the chain owns
+// its CUs (the ring instance covers them with 256 lanes); the condensed tableau's entering slot
+// travels in the selection record
+bool onelaunch_ok(const dlp_session* s) {
+    if (!peer_onelaunch()) return false;
+    if (s->chain_cus > 0 && s->d.K == 64)   // the ring instance (launch_pivot_x)
+        return s->g.rthreads == 128 || s->g.rthreads == dlp::kRatioDeferThreads;
+    // the LEAN instance beside the pass (lookahead on shared CUs) has no condensed build
+    return s->g.rthreads == dlp::kRatioDeferThreads && !(s->g.cd.on && s->la);
+}
+
 // The exchange kernels' peer table (X_PEER) or NULL.
 inline const dlp::XPeers* xp_of(const dlp_session* s) {
     return s->xmode == dlp_session::X_PEER ? s->xpeers : nullptr;
@@ -1318,11 +1329,11 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
         // selection, the selection record to the pivot-row workgroups, row push, commit).  Bit-exact,
         // but 1-3 % slower than two launches at the C3 rank geometries: the record's hand-off and its
         // ~130 pollers cost what the launch boundary did (profiles/r04i/, r04j/)
-        if (xf && peer_onelaunch() && !s->g.cd.on && s->g.rthreads == dlp::kRatioDeferThreads) {
+        if (xf && onelaunch_ok(s)) {
             s->xseq_c += 1;
             s->xseq_r += 1;   // (equal: every pivot, drive-out and carry step advances both)
             HIP_TRY(dlp::launch_pivot_x(gsel, *dcur, s->basis, s->pp, s->st, o.tol_dj, o.tol_piv, o.pricing, s->log,
-                                        s->log_cap, s->stream, dprev, pseal, xp, s->xseq_c, &bp));
+                                        s->log_cap, s->stream, dprev, pseal, xp, s->xseq_c, &bp, s->chain_cus > 0));
             if (ev) HIP_TRY(hipEventRecord(ev[1], s->stream));
             return DLP_OK;
         }
@@ -1339,7 +1350,7 @@ int pivot_defer_phase(dlp_session* s, int phase, int64_t slot, bool last) {
     }
     if (phase == 1) {
         if (!s->la && !s->exchange && s->fuse_pivot && s->fuse_fits && !s->g.cd.on && !ev) return DLP_OK;
-        if (xf && peer_onelaunch() && !s->g.cd.on && s->g.rthreads == dlp::kRatioDeferThreads) {   // (the whole pivot ran in phase 0's launch)
+        if (xf && onelaunch_ok(s)) {   // (the whole pivot ran in phase 0's launch)
             if (ev) HIP_TRY(hipEventRecord(ev[2], s->stream));
             return DLP_OK;
         }
